@@ -1,0 +1,184 @@
+#!/usr/bin/env python3
+"""Throughput benchmark of the photon-transport hot path (BASELINE.json metric:
+photon packets/s on a 128^3 fluence grid, 1/2/4/8 GPUs).
+
+Workload (the north-star "single-sphere HG scatterer"): geometry
+`sphere` of src/setupGeometry.f90:10-71 (r=1, mus=10, mua=0.1, g=0.9, n=1, in a 2^3 box),
+isotropic point source at the origin, 128^3 jmean grid with path-length deposition.
+A step = one launch of the transport kernel over a batch of photons per GPU (weak scaling:
+the per-GPU batch is fixed). Photon indices are disjoint across steps and ranks, so N GPUs
+run N independent shards of one Monte Carlo job; the tallies are summed with one RCCL
+all-reduce at the end of the timed region.
+
+Prints ONE JSON line on rank 0. Diagnostics go to stderr.
+"""
+import argparse
+import ctypes as C
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def workload(grid_n):
+    from rsmcrt_amd import builders, scene
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(grid_n, grid_n, grid_n, 1.0, 1.0, 1.0)
+    return sc, g, scene.point_source()
+
+
+def cpu_baseline(sc, g, src, seconds, eng):
+    """The CPU restatement (oracle/, 1 core) on a bounded sample of the same workload,
+    plus jmean agreement of the GPU on exactly the same photons."""
+    import numpy as np
+    from oracle import pyoracle as O
+    res = None
+    n = 0
+    chunk = 2000
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        res = O.run(sc, g, src, chunk, first_photon=n, result=res)
+        n += chunk
+    dt = time.perf_counter() - t0
+    gpu = eng.run(src, n)
+    fc, fg = res.normalised_fluence(), gpu.normalised_fluence()
+    rmse = float(np.sqrt(np.mean((fg - fc) ** 2)))
+    rel = float(np.max(np.abs(fg - fc)) / max(1e-300, float(np.max(np.abs(fc)))))
+    same_counters = gpu.counters_dict() == res.counters_dict()
+    return {"value": n / dt, "unit": "photon packets/s", "cores": 1, "kind": "port",
+            "sample": f"photons [0,{n}) of the same workload on 1 host core (oracle/ C restatement, gcc -O2)",
+            "seconds": round(dt, 2)}, {"jmean_rmse_vs_cpu_same_photons": rmse,
+                                      "jmean_max_rel_diff_vs_cpu": rel,
+                                      "counters_bit_exact_vs_cpu": same_counters,
+                                      "photons_compared": n}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4_000_000, help="photons per step per GPU")
+    ap.add_argument("--grid", type=int, default=128)
+    ap.add_argument("--seed", type=int, default=123456789)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from rsmcrt_amd import abi
+    from rsmcrt_amd.engine import Engine
+
+    sc, g, src = workload(args.grid)
+    eng = Engine(sc, g, device=torch.cuda.current_device())
+    nv = g.nx * g.ny * g.nz
+    jmean = torch.zeros(nv, dtype=torch.float64, device=dev)
+    absorb = torch.zeros(nv, dtype=torch.float64, device=dev)
+    nscatt = torch.zeros(1, dtype=torch.float64, device=dev)
+    counters = torch.zeros(abi.NCOUNTERS, dtype=torch.int64, device=dev)
+    dt_ = abi.DeviceTallies()
+    dt_.jmean, dt_.absorb = jmean.data_ptr(), absorb.data_ptr()
+    dt_.nscatt, dt_.counters = nscatt.data_ptr(), counters.data_ptr()
+    stream = torch.cuda.current_stream()
+    B = args.batch
+
+    def step(s):
+        cfg = Engine.config(B, seed=args.seed, flags=abi.FLAG_PATHLENGTH, first_photon=(s * world + rank) * B)
+        eng.run_device(src, cfg, dt_, stream.cuda_stream)
+
+    for s in range(args.warmup):
+        step(s)
+    torch.cuda.synchronize()
+    c0 = counters.clone()
+    if world > 1:
+        dist.all_reduce(c0)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for s in range(args.warmup, args.warmup + args.steps):
+        step(s)
+    ev1.record(stream)
+    if world > 1:
+        for t in (jmean, absorb, nscatt, counters):
+            dist.all_reduce(t)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # launches are back to back on `stream`
+    cdelta = (counters - c0).cpu().numpy()  # all ranks, timed steps only
+    photons = world * args.steps * B
+
+    out = None
+    if rank == 0:
+        deposits = float(cdelta[abi.CTR["deposits"]]) / world  # per rank, over the timed steps
+        dep_per_launch = deposits / args.steps
+        # algorithmic bytes of the deposition: one fp32 jmean read + write per deposit (8 B),
+        # SURVEY.md §8(d)
+        achieved = 8.0 * dep_per_launch / (kern_ms * 1e-3) / 1e9
+        out = {
+            "metric": "photon packets/sec (128^3 jmean grid, path-length deposition)",
+            "value": photons / elapsed,
+            "unit": "photon packets/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Philox photon streams; scene from setupGeometry.f90 'sphere')",
+            "config": {"workload": "M1 single-sphere HG scatterer: sphere r=1 mus=10 mua=0.1 g=0.9 n=1 in 2^3 box, "
+                                   "point source at origin, 128^3 grid (setupGeometry.f90:10-71)",
+                       "grid": [g.nx, g.ny, g.nz], "photons_per_step_per_gpu": B, "photons_timed": photons,
+                       "parallelism": f"photon-index shards x{world} + RCCL all-reduce of tallies"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8000.0, "traffic": None,
+                         "kernel": "transport_kernel", "avg_launch_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": 8.0 * dep_per_launch,
+                         "deposits_per_photon": deposits / (args.steps * B),
+                         "deposits_per_s": dep_per_launch / (kern_ms * 1e-3)},
+            "cpu_baseline": None,
+        }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        base, agree = cpu_baseline(sc, g, src, args.cpu_seconds, eng)
+        out["cpu_baseline"] = base
+        out["parity"] = agree
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,276 @@
+/*
+ * smcrt.h — C ABI of the MI355X photon-packet engine (rsmcrt_amd).
+ *
+ * Drop-in boundary for signedMCRT's per-photon hot path. The reference seam is
+ *   subroutine run_MCRT(input_file, history, packet, dict, distances, image, dects, array,
+ *                       nscatt, start, tev, spectrum)          /root/reference/src/kernelsMod.f90:1790-1898
+ * whose results are side effects on the module globals jmean/absorb/emission
+ * (src/iarray.f90:10-18), on nscatt (intent inout) and on dects(i)%p%data. Per-photon
+ * tauint2 calls (src/inttau2.f90:15) are not FFI-viable, so the whole photon loop
+ * (noBiasPropagation kernelsMod.f90:1901-1976 / survivalBiasPropagation :1979-2067) crosses
+ * this boundary at once.
+ *
+ * Everything here is plain C: POD structs, pointers and sizes; no HIP or torch types.
+ * A Fortran ISO_C_BINDING module that binds these entry points is given in INTEGRATION.md.
+ *
+ * Conventions
+ *  - All geometry is fp64 (reference constants.f90:18, wp = real64).
+ *  - Grids are (nx, ny, nz) with x fastest (Fortran column-major jmean(i,j,k), iarray.f90:12).
+ *  - Tallies are ACCUMULATED INTO (never overwritten), so checkpoint/resume and multi-run
+ *    accumulation work (kernelsMod.f90:52-72).
+ *  - Photon j of a run uses the counter-based Philox4x32-10 stream keyed by
+ *    (seed, first_photon + j): results do not depend on how photons are split across
+ *    launches or GPUs (replaces init_rng/ran2, random_mod.f90:44-90).
+ *  - Every entry point returns 0 on success or a negative smcrt_status; none aborts.
+ *    The reference's `error stop` paths inside the photon loop (inttau2.f90:276,515,572)
+ *    terminate only the offending photon and are counted in SMCRT_CTR_FAULTS.
+ */
+#ifndef SMCRT_H
+#define SMCRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SMCRT_ABI_VERSION 1
+
+typedef enum smcrt_status {
+  SMCRT_OK = 0,
+  SMCRT_ERR_INVALID_ARG = -1,
+  SMCRT_ERR_HIP = -2,
+  SMCRT_ERR_RCCL = -3,
+  SMCRT_ERR_DEVICE_FAULT = -4,
+  SMCRT_ERR_NO_DEVICE = -5,
+  SMCRT_ERR_OOM = -6,
+  SMCRT_ERR_UNSUPPORTED = -7
+} smcrt_status;
+
+/* ---------------------------------------------------------------- SDF scene ---- */
+/* Primitive kinds: reference src/sdfs/sdfs.f90 evaluate_* (494-735). */
+typedef enum smcrt_sdf_kind {
+  SMCRT_SDF_SPHERE = 1,   /* param[0]=radius                                   sdfs.f90:494-508 */
+  SMCRT_SDF_BOX = 2,      /* param[0..2]=HALF lengths (ctor halves, :455)      sdfs.f90:510-525 */
+  SMCRT_SDF_TORUS = 3,    /* param[0]=oradius param[1]=iradius                 sdfs.f90:527-542 */
+  SMCRT_SDF_CYLINDER = 4, /* param[0..2]=a param[3..5]=b param[6]=radius       sdfs.f90:544-581 */
+  SMCRT_SDF_TRIPRISM = 5, /* param[0]=h1 param[1]=h2                           sdfs.f90:583-597 */
+  SMCRT_SDF_SEGMENT = 6,  /* param[0..2]=a param[3..5]=b                       sdfs.f90:599-626 */
+  SMCRT_SDF_CAPSULE = 7,  /* param[0..2]=a param[3..5]=b param[6]=r            sdfs.f90:628-648 */
+  SMCRT_SDF_CONE = 8,     /* param[0..2]=a param[3..5]=b param[6]=ra param[7]=rb sdfs.f90:650-686 */
+  SMCRT_SDF_EGG = 9,      /* param[0]=r1 param[1]=r2 param[2]=h                sdfs.f90:688-718 */
+  SMCRT_SDF_PLANE = 10,   /* param[0..2]=a (unit normal)                       sdfs.f90:720-735 */
+  SMCRT_SDF_MODEL = 11    /* CSG fold over children       sdf_base.f90:146-161, sdfModifiers.f90:428-491 */
+} smcrt_sdf_kind;
+
+/* CSG operators of a MODEL node (sdfModifiers.f90:428-491). */
+typedef enum smcrt_csg_op {
+  SMCRT_OP_UNION = 0,        /* min(d1,d2)                                   */
+  SMCRT_OP_SMOOTH_UNION = 1, /* min(d1,d2) - h^3 k/6, h=max(k-|d1-d2|,0)/k   */
+  SMCRT_OP_SUBTRACTION = 2,  /* max(-d1,d2)                                  */
+  SMCRT_OP_INTERSECTION = 3  /* max(d1,d2)                                   */
+} smcrt_csg_op;
+
+/* One SDF node. The scene is a node table; `top` lists the top-level SDFs in the
+ * reference's sdfs_array order (their index+1 is the reference "layer" index used by
+ * tauint2's maxloc). A MODEL node folds its children nodes[first_child ..
+ * first_child+n_children-1] left to right with `op` (eval_model, sdf_base.f90:146-161).
+ * Optical properties are the reference `mono` inputs (opticalProperties.f90:107-125);
+ * kappa/albedo/g2 are derived by the library exactly as init_mono does. For a MODEL the
+ * reference uses its first child's properties (model_init, sdf_base.f90:133-134); the
+ * builder is expected to copy them into the model node. */
+typedef struct smcrt_sdf_node {
+  int32_t kind;        /* smcrt_sdf_kind */
+  int32_t layer;       /* sdf_base%layer: the reference ID (render/detector), not the array index */
+  int32_t op;          /* smcrt_csg_op, MODEL only */
+  int32_t first_child; /* MODEL only */
+  int32_t n_children;  /* MODEL only */
+  int32_t reserved[3];
+  double transform[16]; /* Fortran t(4,4), column-major: transform[(c-1)*4+(r-1)] = t(r,c).
+                           p = pos .dot. t (vector_class.f90:292-304) */
+  double param[12];
+  double k;            /* MODEL smoothing parameter */
+  double mus, mua, hgg, n;
+} smcrt_sdf_node;
+
+/* ----------------------------------------------------------------- grid ---------- */
+/* cart_grid (grid.f90:14-25, init_grid_cart :119-159): voxel faces at (i-1)*2*max/n. */
+typedef struct smcrt_grid {
+  int32_t nx, ny, nz, reserved;
+  double xmax, ymax, zmax; /* HALF extents */
+} smcrt_grid;
+
+/* ----------------------------------------------------------------- source -------- */
+typedef enum smcrt_source_kind {
+  SMCRT_SRC_POINT = 1,   /* isotropic point       photon.f90:311-359 (2 draws)  */
+  SMCRT_SRC_UNIFORM = 2, /* uniform parallelogram photon.f90:566-649 (2 draws)  */
+  SMCRT_SRC_PENCIL = 3   /* pencil beam           photon.f90:652-710 (0 draws)  */
+} smcrt_source_kind;
+
+typedef struct smcrt_source {
+  int32_t kind, reserved;
+  double pos[3];  /* photon_origin%pos (point, pencil) */
+  double dir[3];  /* photon_origin%n{x,y,z}p (uniform, pencil) */
+  double p1[3], p2[3], p3[3]; /* uniform: pos1 + r1*pos2 + r2*pos3 (photon.f90:596-612) */
+} smcrt_source;
+
+/* ----------------------------------------------------------------- detectors ----- */
+typedef enum smcrt_detector_kind {
+  SMCRT_DET_CIRCLE = 1,  /* detectors.f90:147-164  */
+  SMCRT_DET_ANNULUS = 2, /* detectors.f90:212-244  */
+  SMCRT_DET_CAMERA = 3,  /* detectors.f90:401-469  */
+  SMCRT_DET_FIBRE = 4    /* detectors.f90:246-393  */
+} smcrt_detector_kind;
+
+/* A constructed detector object (the fields the reference init_* functions set).
+ * 1-D detectors own nbins doubles (nbins already includes the reference's extra bin,
+ * init_circle_dect: out%nbins = nbins + 1); the camera owns nbins*nbins doubles laid
+ * out data(idx, idy) -> idx-1 + nbins*(idy-1). */
+typedef struct smcrt_detector {
+  int32_t kind;
+  int32_t nbins;       /* stored bin count (TOML nbins + 1) */
+  int32_t layer;
+  int32_t reserved;
+  double pos[3];       /* circle/annulus/fibre: centre; camera: p1 (first corner) */
+  double dir[3];       /* circle/annulus/fibre: surface normal; camera: n = normalised e2 x e1 */
+  double e1[3], e2[3]; /* camera edge vectors */
+  double radius;       /* circle */
+  double r1, r2;       /* annulus */
+  double width, height;/* camera */
+  double bin_wid;      /* 1-D bin width (camera: bin_wid_x) */
+  double bin_wid_y;    /* camera */
+  double fibre[11];    /* focalLength1, focalLength2, f1Aperture, f2Aperture, frontOffset,
+                          backOffset, frontToPinSep, pinToBackSep, pinAperture, acceptAngle,
+                          coreDiameter */
+} smcrt_detector;
+
+/* ----------------------------------------------------------------- run ----------- */
+enum {
+  SMCRT_FLAG_PATHLENGTH = 1u << 0,    /* -Dpathlength: path-length jmean deposition (inttau2.f90:408-445) */
+  SMCRT_FLAG_SURVIVAL_BIAS = 1u << 1, /* -DsurvivalBias: kernelsMod.f90:1979-2067 */
+  SMCRT_FLAG_RENDER_SOURCE = 1u << 2, /* state%render_source: emission tally (kernelsMod.f90:1945) */
+  SMCRT_FLAG_TEST_KERNEL = 1u << 3,   /* test_kernel semantics (kernelsMod.f90:2069-2182): no re-emission,
+                                         initial layer mask ds<=0, scatter-order moments */
+  SMCRT_FLAG_END_EARLY = 1u << 4,     /* test_kernel end_early: stop after the 4th scatter */
+  SMCRT_FLAG_RECORD_PHOTONS = 1u << 5 /* fill smcrt_tallies.records (debug/parity) */
+};
+
+typedef struct smcrt_run_config {
+  uint64_t n_photons;    /* photons in this call (int64: no int32 overflow, sim_state.f90:12) */
+  uint64_t first_photon; /* global index of the first photon (multi-GPU shards, resume) */
+  uint64_t seed;         /* state%iseed */
+  uint32_t flags;        /* SMCRT_FLAG_* */
+  int32_t reserved;
+} smcrt_run_config;
+
+/* Counter slots (uint64). Integer outputs: bit-exact between the HIP path and the CPU
+ * restatement for the same seed. */
+enum {
+  SMCRT_CTR_PHOTONS = 0,      /* photons completed */
+  SMCRT_CTR_EMIT_RETRIES,     /* re-emissions because the start cell was outside the grid */
+  SMCRT_CTR_SCATTERS,         /* == nscatt */
+  SMCRT_CTR_ABSORBED,         /* albedo roulette absorptions */
+  SMCRT_CTR_SDF_EVALS,        /* packet%cnts equivalent (top-level SDF evaluations) */
+  SMCRT_CTR_DEPOSITS,         /* jmean deposits (voxel crossings) */
+  SMCRT_CTR_GRID_UPDATES,     /* update_grids calls */
+  SMCRT_CTR_TAUINT,           /* tauint2 calls */
+  SMCRT_CTR_FRESNEL,          /* reflect_refract calls */
+  SMCRT_CTR_REFLECTIONS,      /* Fresnel reflections */
+  SMCRT_CTR_BOUNCE_ABORTS,    /* bounces > 1000 early returns (inttau2.f90:313-315) */
+  SMCRT_CTR_FAULTS,           /* would-be `error stop` events; photon terminated */
+  SMCRT_CTR_RNG_DRAWS,        /* ran2() calls */
+  SMCRT_CTR_DETECTOR_HITS,    /* detector bin increments */
+  SMCRT_CTR_ESCAPED,          /* photons terminated by leaving the grid/geometry */
+  SMCRT_NCOUNTERS = 16
+};
+
+/* Per-photon record (SMCRT_FLAG_RECORD_PHOTONS), for trajectory-level parity checks. */
+typedef struct smcrt_photon_record {
+  double pos[3];   /* final packet%pos */
+  double dir[3];   /* final direction */
+  double weight;
+  int32_t cell[3]; /* final packet%{x,y,z}cell (1-based, -1 outside) */
+  int32_t layer;
+  uint32_t nscatt;
+  uint32_t bounces;
+  uint32_t draws;  /* RNG draws consumed */
+  uint32_t status; /* 1 absorbed, 2 escaped, 3 fault, 4 end_early */
+} smcrt_photon_record;
+
+/* Host tallies. Every pointer may be NULL (that tally is skipped). All accumulate.
+ * fp32 grids keep the reference layout/type (iarray.f90:12-16); the engine sums in fp64
+ * internally and adds the run's total into the float arrays once, at the end of the call.
+ * The optional fp64 grids receive the same totals without the final rounding. */
+typedef struct smcrt_tallies {
+  float* jmean;      /* nx*ny*nz */
+  float* absorb;     /* nx*ny*nz */
+  float* emission;   /* nx*ny*nz */
+  double* jmean_f64; /* nx*ny*nz */
+  double* absorb_f64;
+  double* emission_f64;
+  double* det_bins;  /* concatenated detector data, in detector order */
+  double* nscatt;    /* scalar */
+  double* moments;   /* 24 doubles: [order 1..4][x,y,z] sums of pos, then of pos**2 (test_kernel) */
+  uint64_t* counters;/* SMCRT_NCOUNTERS */
+  smcrt_photon_record* records; /* n_photons entries, with SMCRT_FLAG_RECORD_PHOTONS */
+} smcrt_tallies;
+
+typedef struct smcrt_scene smcrt_scene;
+
+/* ABI version of the loaded library (== SMCRT_ABI_VERSION it was built with). */
+int smcrt_abi_version(void);
+/* Number of visible HIP devices (0 is a valid answer; a negative status on error). */
+int smcrt_device_count(int32_t* count);
+/* Message for the last error on this thread ("" when none). */
+const char* smcrt_last_error(void);
+
+/* Upload a scene (SDF table, grid, detectors) to HIP device `device`. The scene stays
+ * resident across smcrt_run calls (escape/inverse drivers reuse it, kernelsMod.f90:617,1642). */
+int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes,
+                       const int32_t* top, int32_t n_top,
+                       const smcrt_grid* grid,
+                       const smcrt_detector* dets, int32_t n_dets,
+                       int32_t device, smcrt_scene** out);
+void smcrt_scene_destroy(smcrt_scene* scene);
+
+/* Total doubles of detector data the scene's detectors own (size of det_bins). */
+int smcrt_scene_det_bins(const smcrt_scene* scene, int64_t* n_doubles);
+
+/* Replace the optical properties of top-level SDF `top_index` (updateOptProp,
+ * sdf_base.f90:255-263; used by inverse MCRT). */
+int smcrt_scene_set_optprops(smcrt_scene* scene, int32_t top_index,
+                             double mus, double mua, double hgg, double n);
+
+/* Run cfg->n_photons photons (the body of run_MCRT) and accumulate into `io`.
+ * Synchronous: returns when the tallies are in host memory. */
+int smcrt_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_run_config* cfg,
+              smcrt_tallies* io);
+
+/* Device-resident variant for multi-GPU and benchmarking: launches on `stream`
+ * (a hipStream_t; NULL = the legacy default stream) and accumulates into caller-owned
+ * DEVICE buffers (fp64 grids of nx*ny*nz, det bins, nscatt/moments/counters as in
+ * smcrt_tallies; any may be NULL). Asynchronous: nothing is copied to the host.
+ * The caller sums these buffers across ranks (one RCCL all-reduce per buffer). */
+typedef struct smcrt_device_tallies {
+  double* jmean;
+  double* absorb;
+  double* emission;
+  double* det_bins;
+  double* nscatt;
+  double* moments;
+  uint64_t* counters;
+  smcrt_photon_record* records;
+} smcrt_device_tallies;
+
+int smcrt_run_device(smcrt_scene* scene, const smcrt_source* src, const smcrt_run_config* cfg,
+                     smcrt_device_tallies* dev, void* stream);
+
+/* Normalisation of writer.f90:25-52 (normalise_fluence): grid *= nx*ny*nz / nphotons,
+ * i.e. (8*xmax*ymax*zmax)/(nphotons*dx*dy*dz). Host-side helper on an fp32 grid. */
+int smcrt_normalise_fluence(float* grid, const smcrt_grid* g, uint64_t nphotons);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMCRT_H */

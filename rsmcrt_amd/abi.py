@@ -1,0 +1,130 @@
+"""ctypes mirror of include/smcrt.h (the C ABI of the engine).
+
+Field order and sizes must match the header exactly; tests/test_abi.py checks the sizes
+against the library's own view of them.
+"""
+import ctypes as C
+
+SMCRT_ABI_VERSION = 1
+
+# smcrt_status
+OK = 0
+ERR_INVALID_ARG = -1
+ERR_HIP = -2
+ERR_RCCL = -3
+ERR_DEVICE_FAULT = -4
+ERR_NO_DEVICE = -5
+ERR_OOM = -6
+ERR_UNSUPPORTED = -7
+
+STATUS_NAMES = {
+    OK: "OK", ERR_INVALID_ARG: "INVALID_ARG", ERR_HIP: "HIP_ERROR", ERR_RCCL: "RCCL_ERROR",
+    ERR_DEVICE_FAULT: "DEVICE_FAULT", ERR_NO_DEVICE: "NO_DEVICE", ERR_OOM: "OUT_OF_MEMORY",
+    ERR_UNSUPPORTED: "UNSUPPORTED",
+}
+
+# smcrt_sdf_kind (reference src/sdfs/sdfs.f90)
+SDF_SPHERE, SDF_BOX, SDF_TORUS, SDF_CYLINDER, SDF_TRIPRISM = 1, 2, 3, 4, 5
+SDF_SEGMENT, SDF_CAPSULE, SDF_CONE, SDF_EGG, SDF_PLANE, SDF_MODEL = 6, 7, 8, 9, 10, 11
+
+# smcrt_csg_op (src/sdfs/sdfModifiers.f90:428-491)
+OP_UNION, OP_SMOOTH_UNION, OP_SUBTRACTION, OP_INTERSECTION = 0, 1, 2, 3
+
+# smcrt_source_kind
+SRC_POINT, SRC_UNIFORM, SRC_PENCIL = 1, 2, 3
+
+# smcrt_detector_kind
+DET_CIRCLE, DET_ANNULUS, DET_CAMERA, DET_FIBRE = 1, 2, 3, 4
+
+# run flags
+FLAG_PATHLENGTH = 1 << 0
+FLAG_SURVIVAL_BIAS = 1 << 1
+FLAG_RENDER_SOURCE = 1 << 2
+FLAG_TEST_KERNEL = 1 << 3
+FLAG_END_EARLY = 1 << 4
+FLAG_RECORD_PHOTONS = 1 << 5
+
+# counters
+COUNTER_NAMES = [
+    "photons", "emit_retries", "scatters", "absorbed", "sdf_evals", "deposits",
+    "grid_updates", "tauint", "fresnel", "reflections", "bounce_aborts", "faults",
+    "rng_draws", "detector_hits", "escaped", "reserved15",
+]
+NCOUNTERS = 16
+CTR = {name: i for i, name in enumerate(COUNTER_NAMES)}
+
+
+class SdfNode(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("layer", C.c_int32), ("op", C.c_int32),
+        ("first_child", C.c_int32), ("n_children", C.c_int32), ("reserved", C.c_int32 * 3),
+        ("transform", C.c_double * 16), ("param", C.c_double * 12), ("k", C.c_double),
+        ("mus", C.c_double), ("mua", C.c_double), ("hgg", C.c_double), ("n", C.c_double),
+    ]
+
+
+class Grid(C.Structure):
+    _fields_ = [("nx", C.c_int32), ("ny", C.c_int32), ("nz", C.c_int32), ("reserved", C.c_int32),
+                ("xmax", C.c_double), ("ymax", C.c_double), ("zmax", C.c_double)]
+
+
+class Source(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32),
+                ("pos", C.c_double * 3), ("dir", C.c_double * 3),
+                ("p1", C.c_double * 3), ("p2", C.c_double * 3), ("p3", C.c_double * 3)]
+
+
+class Detector(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32), ("nbins", C.c_int32), ("layer", C.c_int32), ("reserved", C.c_int32),
+        ("pos", C.c_double * 3), ("dir", C.c_double * 3), ("e1", C.c_double * 3), ("e2", C.c_double * 3),
+        ("radius", C.c_double), ("r1", C.c_double), ("r2", C.c_double),
+        ("width", C.c_double), ("height", C.c_double),
+        ("bin_wid", C.c_double), ("bin_wid_y", C.c_double), ("fibre", C.c_double * 11),
+    ]
+
+
+class RunConfig(C.Structure):
+    _fields_ = [("n_photons", C.c_uint64), ("first_photon", C.c_uint64), ("seed", C.c_uint64),
+                ("flags", C.c_uint32), ("reserved", C.c_int32)]
+
+
+class PhotonRecord(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("dir", C.c_double * 3), ("weight", C.c_double),
+                ("cell", C.c_int32 * 3), ("layer", C.c_int32), ("nscatt", C.c_uint32),
+                ("bounces", C.c_uint32), ("draws", C.c_uint32), ("status", C.c_uint32)]
+
+
+class Tallies(C.Structure):
+    _fields_ = [
+        ("jmean", C.POINTER(C.c_float)), ("absorb", C.POINTER(C.c_float)),
+        ("emission", C.POINTER(C.c_float)),
+        ("jmean_f64", C.POINTER(C.c_double)), ("absorb_f64", C.POINTER(C.c_double)),
+        ("emission_f64", C.POINTER(C.c_double)),
+        ("det_bins", C.POINTER(C.c_double)), ("nscatt", C.POINTER(C.c_double)),
+        ("moments", C.POINTER(C.c_double)), ("counters", C.POINTER(C.c_uint64)),
+        ("records", C.POINTER(PhotonRecord)),
+    ]
+
+
+class DeviceTallies(C.Structure):
+    _fields_ = [
+        ("jmean", C.c_void_p), ("absorb", C.c_void_p), ("emission", C.c_void_p),
+        ("det_bins", C.c_void_p), ("nscatt", C.c_void_p), ("moments", C.c_void_p),
+        ("counters", C.c_void_p), ("records", C.c_void_p),
+    ]
+
+
+# photon record as a numpy dtype (same layout)
+def record_dtype():
+    import numpy as np
+    return np.dtype([("pos", "<f8", 3), ("dir", "<f8", 3), ("weight", "<f8"), ("cell", "<i4", 3),
+                     ("layer", "<i4"), ("nscatt", "<u4"), ("bounces", "<u4"), ("draws", "<u4"),
+                     ("status", "<u4")])
+
+
+EXPORTED_SYMBOLS = [
+    "smcrt_abi_version", "smcrt_device_count", "smcrt_last_error", "smcrt_scene_create",
+    "smcrt_scene_destroy", "smcrt_scene_det_bins", "smcrt_scene_set_optprops", "smcrt_run",
+    "smcrt_run_device", "smcrt_normalise_fluence",
+]

@@ -1,0 +1,52 @@
+"""Build the HIP engine library in-tree: rsmcrt_amd/libsmcrt.so (gfx950).
+
+Plain hipcc, one translation unit, no torch extension machinery: the library is a C-ABI
+shared object (include/smcrt.h) that Fortran/C/Python can bind.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "libsmcrt.so")
+SOURCES = [os.path.join(PKG, "csrc", "smcrt.hip")]
+DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("transport.h", "detmath.h")] + [
+    os.path.join(ROOT, "include", "smcrt.h")]
+ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
+# -ffp-contract=off: no fused multiply-add, so fp64 trajectories are bit-identical to the
+# CPU restatement (oracle/), which is compiled the same way.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+         f"--offload-arch={ARCH}", "-Wall"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(d) <= t for d in DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    cmd = [hipcc(), *FLAGS, "-o", LIB + ".tmp", *SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

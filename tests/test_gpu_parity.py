@@ -1,0 +1,173 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU restatement (oracle/) on the
+same seeded inputs.
+
+Integer outputs (counters, nscatt, photon records, unit-weight absorb/emission/detector
+bins) must be bit-exact; each photon's final position/direction must be bit-identical
+(same Philox stream, same IEEE operations, no FMA contraction on either side). fp64 tallies
+built from many atomic adds (jmean, survival-bias absorb, moments) differ only by summation
+order: |gpu - cpu| <= 1e-12 * |cpu| + 1e-300 per voxel.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from rsmcrt_amd import abi, builders, scene
+from rsmcrt_amd.engine import Engine
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+SEED = 123456789
+
+
+def compare(gpu, cpu, exact_absorb=True):
+    assert gpu.counters_dict() == cpu.counters_dict()
+    assert gpu.nscatt[0] == cpu.nscatt[0]
+    if gpu.records.size:
+        for f in ("pos", "dir", "weight", "cell", "layer", "nscatt", "bounces", "draws", "status"):
+            assert np.array_equal(gpu.records[f], cpu.records[f]), f
+    np.testing.assert_allclose(gpu.jmean, cpu.jmean, rtol=RTOL, atol=1e-300)
+    if exact_absorb:
+        assert np.array_equal(gpu.absorb, cpu.absorb)
+        assert np.array_equal(gpu.emission, cpu.emission)
+    else:
+        np.testing.assert_allclose(gpu.absorb, cpu.absorb, rtol=RTOL, atol=1e-300)
+    assert np.array_equal(gpu.det_bins, cpu.det_bins)
+    np.testing.assert_allclose(gpu.moments, cpu.moments, rtol=RTOL, atol=1e-300)
+
+
+def both(sc, g, src, n, flags=abi.FLAG_PATHLENGTH, dets=(), first=0, seed=SEED):
+    with Engine(sc, g, dets) as eng:
+        gpu = eng.run(src, n, seed=seed, flags=flags, first_photon=first, records=True)
+    cpu = O.run(sc, g, src, n, seed=seed, flags=flags, dets=dets, first_photon=first, records=True)
+    return gpu, cpu
+
+
+def test_scat_test():
+    gpu, cpu = both(builders.setup_scat_test(10.0), scene.grid(64, 64, 64, 1, 1, 1), scene.point_source(), 4000)
+    compare(gpu, cpu)
+    assert cpu.counter("faults") == 0
+
+
+def test_scat_test_kernel_mode_and_offset():
+    gpu, cpu = both(builders.setup_scat_test(10.0), scene.grid(40, 41, 42, 1, 1, 1), scene.point_source(), 3000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_TEST_KERNEL, first=10 ** 12 + 7)
+    compare(gpu, cpu)
+
+
+def test_single_sphere_hg():
+    """M1, the north-star workload: one HG sphere (mus=10, mua=0.1, g=0.9), point source."""
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    gpu, cpu = both(sc, scene.grid(128, 128, 128, 1, 1, 1), scene.point_source(), 2000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE)
+    compare(gpu, cpu)
+    assert cpu.counter("absorbed") > 0
+
+
+def test_refracting_sphere_fresnel():
+    """aptran: n=1.33 sphere, Fresnel reflect/refract, uniform line source (vector direction)."""
+    sc = builders.setup_tran_and_jacques()
+    src = scene.uniform_source((-0.25, 0.0, 0.99999), (0.5, 0.0, 0.0), (0.0, 0.0, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, scene.grid(67, 67, 67, 1, 1, 1), src, 4000)
+    compare(gpu, cpu)
+    assert cpu.counter("fresnel") > 0 and cpu.counter("reflections") > 0
+
+
+def test_sphere_scene():
+    """sphere_scene: 40 non-scattering n=1.37 spheres, uniform source, many SDFs."""
+    sc = builders.setup_sphere_scene(builders.random_sphere_list(40))
+    src = scene.uniform_source((-1.0, -1.0, 0.9999999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, scene.grid(50, 50, 50, 1, 1, 1), src, 2000)
+    compare(gpu, cpu)
+
+
+def test_detectors_validation1():
+    sc = builders.setup_box(90.0, 10.0, 0.75, 1.0, (100.0, 100.0, 0.02), (100.0, 100.0, 0.03))
+    g = scene.grid(50, 50, 50, 50.0, 50.0, 0.015)
+    src = scene.pencil_source((0.0, 0.0, -0.01), (0.0, 0.0, 1.0))
+    dets = [scene.circle_dect((0.0, 0.0, -0.01), (0.0, 0.0, -1.0), 1, 20.0, 100),
+            scene.circle_dect((0.0, 0.0, 0.01), (0.0, 0.0, 1.0), 1, 20.0, 100)]
+    gpu, cpu = both(sc, g, src, 5000, dets=dets)
+    compare(gpu, cpu)
+    assert cpu.counter("detector_hits") > 0
+
+
+def test_detectors_all_kinds():
+    """res/test_dects.toml detectors (circle, annulus, camera) on scat_test."""
+    dets = [scene.circle_dect((-1.0, 0, 0), (-1.0, 0, 0), 4, 0.5, 10),
+            scene.annulus_dect((-1.0, 0, 0), (-1.0, 0, 0), 3, 0.5, 1.0, 10),
+            scene.camera((-1.0, -1.0, -1.0), (0.0, 2.0, 0.0), (0.0, 0.0, 2.0), 2, 10, 5000.0)]
+    gpu, cpu = both(builders.setup_scat_test(10.0), scene.grid(32, 32, 32, 1, 1, 1), scene.point_source(), 3000,
+                    dets=dets)
+    compare(gpu, cpu)
+
+
+def test_survival_bias():
+    sc = builders.setup_sphere(10.0, 1.0, 0.9, 1.0, 1.0)
+    gpu, cpu = both(sc, scene.grid(32, 32, 32, 1, 1, 1), scene.point_source(), 2000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_SURVIVAL_BIAS)
+    compare(gpu, cpu, exact_absorb=False)
+
+
+def test_no_pathlength_mode():
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    gpu, cpu = both(sc, scene.grid(32, 32, 32, 1, 1, 1), scene.point_source(), 2000, flags=0)
+    compare(gpu, cpu)
+    assert cpu.counter("deposits") == 0
+
+
+def test_csg_model_omg():
+    """omg: smooth-union model (torus + 9 cylinders), n=2.65."""
+    sc = builders.setup_omg_sdf()
+    src = scene.uniform_source((-1.0, -1.0, 0.9999999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, scene.grid(32, 32, 32, 1, 1, 1), src, 2000)
+    compare(gpu, cpu)
+
+
+def test_moments_scat_test2():
+    g = scene.grid(200, 200, 200, 100.0, 100.0, 100.0)
+    src = scene.pencil_source((0.0, 0.0, 0.0), (0.0, 0.0, 1.0))
+    gpu, cpu = both(builders.setup_scat_test2(10.0, 0.9), g, src, 20000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_TEST_KERNEL | abi.FLAG_END_EARLY)
+    compare(gpu, cpu)
+
+
+# ----------------------------------------------------- full-size properties (GPU only) --
+def test_kat_scat_test_full_size(kats):
+    """Reference KAT at 1e6 photons (10x the TOML) on the 128^3 metric grid."""
+    n = 1_000_000
+    with Engine(builders.setup_scat_test(10.0), scene.grid(128, 128, 128, 1, 1, 1)) as eng:
+        r = eng.run(scene.point_source(), n, flags=abi.FLAG_PATHLENGTH | abi.FLAG_TEST_KERNEL)
+    assert abs(r.nscatt[0] / n - kats["scat_test_nscatt"]["value"]) <= kats["scat_test_nscatt"]["thr"]
+    c = r.counters_dict()
+    assert c["photons"] == n and c["escaped"] + c["absorbed"] + c["faults"] == n and c["faults"] == 0
+
+
+def test_shard_invariance():
+    """Splitting a run into photon-index shards (what multi-GPU does) changes nothing:
+    integer tallies bit-exact, jmean equal up to summation order."""
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(64, 64, 64, 1, 1, 1)
+    src = scene.point_source()
+    n = 200_000
+    with Engine(sc, g) as eng:
+        whole = eng.run(src, n)
+        parts = None
+        for k in range(4):
+            parts = eng.run(src, n // 4, first_photon=k * (n // 4), result=parts)
+    assert whole.counters_dict() == parts.counters_dict()
+    assert np.array_equal(whole.absorb, parts.absorb)
+    np.testing.assert_allclose(whole.jmean, parts.jmean, rtol=1e-10, atol=1e-300)
+
+
+def test_point_source_symmetry():
+    """An isotropic point source at the centre of a sphere: the 8 octants of jmean agree
+    within Monte Carlo noise."""
+    n = 2_000_000
+    with Engine(builders.setup_scat_test(10.0), scene.grid(64, 64, 64, 1, 1, 1)) as eng:
+        r = eng.run(scene.point_source(), n)
+    j = r.jmean
+    octs = [j[a:a + 32, b:b + 32, c:c + 32].sum() for a in (0, 32) for b in (0, 32) for c in (0, 32)]
+    octs = np.array(octs)
+    assert np.all(np.abs(octs / octs.mean() - 1.0) < 0.01)
+    assert abs(j.sum() / n - 6.0) < 0.1  # ~6 cm path per photon (Survey §6 probe: 6.01-6.05)
