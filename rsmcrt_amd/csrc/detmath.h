@@ -33,17 +33,17 @@ __device__ __forceinline__ Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint3
 
 // Per-photon stream: draw d is the (d&1) half of Philox block d>>1, counter
 // (d>>1, 0, pid_lo, pid_hi), key (seed_lo, seed_hi); 53-bit double in [0,1).
+// The key is launch-uniform and passed in, so it stays in scalar registers.
 struct Rng {
-  uint32_t pid_lo, pid_hi, key0, key1;
+  uint32_t pid_lo, pid_hi;
   uint32_t draws;
   double cached;
 
-  __device__ __forceinline__ void init(uint64_t pid, uint64_t seed) {
+  __device__ __forceinline__ void init(uint64_t pid) {
     pid_lo = (uint32_t)pid; pid_hi = (uint32_t)(pid >> 32);
-    key0 = (uint32_t)seed; key1 = (uint32_t)(seed >> 32);
     draws = 0; cached = 0.0;
   }
-  __device__ __forceinline__ double next() {
+  __device__ __forceinline__ double next(uint32_t key0, uint32_t key1) {
     const uint32_t d = draws++;
     if (d & 1u) return cached;
     const Philox4 o = philox4x32_10(d >> 1, 0u, pid_lo, pid_hi, key0, key1);

@@ -1,0 +1,144 @@
+// geometry.h — fp64 vector helpers, SDF primitives and the flattened SDF program.
+//
+// Every function follows the reference's operation order (file:line cited) and the library
+// is built with -ffp-contract=off, so values are bit-identical to the CPU restatement.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/smcrt.h"
+
+namespace smcrt {
+
+struct V3 {
+  double x, y, z;
+};
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }   // vec*scal
+__device__ __forceinline__ V3 smul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }  // scal*vec
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ double len(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ V3 vabs(V3 a) { return v3(fabs(a.x), fabs(a.y), fabs(a.z)); }
+__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
+__device__ __forceinline__ double clampd(double v, double lo, double hi) { return dmin(dmax(v, lo), hi); }
+
+// vec_dot_mat, vector_class.f90:292-304 (transform column-major)
+__device__ __forceinline__ V3 dotmat(V3 a, const double* t) {
+  return v3(t[0] * a.x + t[1] * a.y + t[2] * a.z + t[3], t[4] * a.x + t[5] * a.y + t[6] * a.z + t[7],
+            t[8] * a.x + t[9] * a.y + t[10] * a.z + t[11]);
+}
+
+// CSG operators, sdfModifiers.f90:428-491
+__device__ __forceinline__ double csg(int32_t op, double d1, double d2, double k) {
+  switch (op) {
+    case SMCRT_OP_UNION: return dmin(d1, d2);
+    case SMCRT_OP_SMOOTH_UNION: {
+      const double h = dmax(k - fabs(d1 - d2), 0.0) / k;
+      return dmin(d1, d2) - h * h * h * k * (1.0 / 6.0);
+    }
+    case SMCRT_OP_SUBTRACTION: return dmax(-d1, d2);
+    default: return dmax(d1, d2);
+  }
+}
+
+// One primitive, sdfs.f90:494-735. `nd` is wave-uniform: its fields arrive by scalar loads
+// and the switch never diverges.
+__device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos) {
+  const double* P = nd->param;
+  const V3 p = dotmat(pos, nd->transform);
+  switch (nd->kind) {
+    case SMCRT_SDF_SPHERE:  // :494-508
+      return sqrt(p.x * p.x + p.y * p.y + p.z * p.z) - P[0];
+    case SMCRT_SDF_BOX: {  // :510-525
+      const V3 q = vabs(p) - v3(P[0], P[1], P[2]);
+      return len(v3(dmax(q.x, 0.0), dmax(q.y, 0.0), dmax(q.z, 0.0))) + dmin(dmax(q.x, dmax(q.y, q.z)), 0.0);
+    }
+    case SMCRT_SDF_TORUS: {  // :527-542
+      const V3 q = v3(len(v3(p.x, 0.0, p.z)) - P[0], p.y, 0.0);
+      return len(q) - P[1];
+    }
+    case SMCRT_SDF_CYLINDER: {  // :544-581
+      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const V3 ba = b - a, pa = p - a;
+      const double baba = dot(ba, ba), paba = dot(pa, ba);
+      const double x = len(mul(pa, baba) - mul(ba, paba)) - P[6] * baba;
+      const double y = fabs(paba - baba * 0.5) - baba * 0.5;
+      const double x2 = x * x, y2 = (y * y) * baba;
+      double d;
+      if (dmax(x, y) < 0.0) d = -dmin(x2, y2);
+      else if (x > 0.0 && y > 0.0) d = x2 + y2;
+      else if (x > 0.0) d = x2;
+      else if (y > 0.0) d = y2;
+      else d = 0.0;
+      return copysign(sqrt(fabs(d)) / baba, d);
+    }
+    case SMCRT_SDF_TRIPRISM: {  // :583-597
+      const V3 q = vabs(p);
+      return dmax(q.z - P[1], dmax(q.x * 0.866025 + p.y * 0.5, -p.y) - P[0] * 0.5);
+    }
+    case SMCRT_SDF_SEGMENT: {  // :599-626
+      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const V3 pa = p - a, ba = b - a;
+      const double h = clampd(dot(pa, ba) / dot(ba, ba), 0.0, 1.0);
+      return len(pa - mul(ba, h)) - 0.1;
+    }
+    case SMCRT_SDF_CAPSULE: {  // :628-648
+      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const V3 pa = p - a, ba = b - a;
+      const double h = clampd(dot(pa, ba) / dot(ba, ba), 0.0, 1.0);
+      return len(pa - mul(ba, h)) - P[6];
+    }
+    case SMCRT_SDF_CONE: {  // :650-686
+      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const double ra = P[6], rb = P[7];
+      const double rba = rb - ra;
+      const double baba = dot(b - a, b - a);
+      const double papa = dot(p - a, p - a);
+      const double paba = dot(p - a, b - a) / baba;
+      const double x = sqrt(papa - baba * (paba * paba));
+      const double cax = (paba < 0.5) ? dmax(0.0, x - ra) : dmax(0.0, x - rb);
+      const double cay = fabs(paba - 0.5) - 0.5;
+      const double k = rba * rba + baba;
+      const double f = clampd((rba * (x - ra) + paba * baba) / k, 0.0, 1.0);
+      const double cbx = x - ra - f * rba;
+      const double cby = paba - f;
+      const double s = (cbx < 0.0 && cay < 0.0) ? -1.0 : 1.0;
+      return s * sqrt(dmin(cax * cax + baba * (cay * cay), cbx * cbx + baba * (cby * cby)));
+    }
+    case SMCRT_SDF_EGG: {  // :688-718
+      const double r1 = P[0], r2 = P[1], hh = P[2];
+      const V3 pin = v3(fabs(p.x), p.y, p.z);
+      const double r = r1 - r2;
+      const double h_in = hh + r;
+      const double l = (h_in * h_in - r * r) / (2.0 * r);
+      if (pin.y <= 0.0) return len(pin) - r1;
+      if ((pin.y - h_in) * l > pin.x * h_in) return len(pin - v3(0.0, h_in, 0.0)) - ((r1 + l) - len(v3(h_in, l, 0.0)));
+      return len(pin + v3(l, 0.0, 0.0)) - (r1 + l);
+    }
+    case SMCRT_SDF_PLANE:  // :720-735
+      return dot(p, v3(P[0], P[1], P[2]));
+    default:
+      return __builtin_nan("");
+  }
+}
+
+// The SDF array flattened into one instruction stream, so the kernel evaluates every
+// top-level SDF (and every CSG child, folded left to right as eval_model does,
+// sdf_base.f90:146-161) with a single inlined copy of sdf_prim.
+enum : int32_t {
+  PROG_TOP = 0,         // primitive that is itself a top-level SDF
+  PROG_CHILD_FIRST = 1, // first child of a model: acc = d
+  PROG_CHILD = 2,       // later child: acc = op(acc, d)
+};
+struct ProgOp {
+  int32_t node;   // primitive node index
+  int32_t action; // PROG_*
+  int32_t top;    // 1-based top-level index completed by this op (0 if none)
+  int32_t op;     // CSG op for PROG_CHILD
+  double k;       // CSG parameter
+};
+
+}  // namespace smcrt

@@ -33,32 +33,430 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void transport_kernel(KParams K) {
-  Lane L;
-#pragma unroll
-  for (int i = 0; i < SMCRT_NCOUNTERS; ++i) L.c.v[i] = 0;
-  L.nscatt = 0.0;
-  L.fault = false;
-  const int lane = threadIdx.x & 63;
-  const bool rec_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) && K.records;
-  for (;;) {
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(K.queue, 64ull);
-    base = __shfl(base, 0, 64);
-    if (base >= K.n_photons) break;
-    const uint64_t j = base + (uint64_t)lane;
-    if (j < K.n_photons) run_photon(K, L, K.first_photon + j, rec_on ? K.records + j : nullptr);
+// Arrive at an EVAL program point: the query is evaluated in the next EVAL phase (its
+// point and captured indices are derived from the state, see eval_query).
+#define ARRIVE(state)                 \
+  do {                                \
+    L.st = (state); L.pend = true;    \
+    yield = true;                     \
+  } while (0)
+#define LCTR(c) (sh->ctr[(c)][threadIdx.x])
+
+// The query point of each EVAL state (the exact expressions of the reference).
+__device__ __forceinline__ V3 eval_query(const Lane& L) {
+  switch (L.st) {
+    case ST_H1: case ST_G0: case ST_F1: return L.ssp;
+    case ST_N1: return L.pos + mul(v3(1.0, -1.0, -1.0), 1e-6);   // calcNormal taps,
+    case ST_N2: return L.pos + mul(v3(-1.0, -1.0, 1.0), 1e-6);   // sdf_base.f90:176-184
+    case ST_N3: return L.pos + mul(v3(-1.0, 1.0, -1.0), 1e-6);
+    case ST_N4: return L.pos + mul(v3(1.0, 1.0, 1.0), 1e-6);
+    default: return L.pos;
   }
+}
+
+template <bool LDS_FACES>
+__global__ __launch_bounds__(256) void transport_kernel(KParams K) {
+  __shared__ LaneShared shm;
+  extern __shared__ double sh_faces[];
+  LaneShared* sh = &shm;
+  const double eps = 1e-8;  // inttau2.f90:56
+  const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
+  const bool survival = (K.flags & SMCRT_FLAG_SURVIVAL_BIAS) != 0;
+  const bool rec_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) && K.records;
+  const int lane_id = threadIdx.x & 63;
+
+  const double* xf = K.xface;
+  const double* yf = K.yface;
+  const double* zf = K.zface;
+  if constexpr (LDS_FACES) {
+    const int nf = (K.nx + 1) + (K.ny + 1) + (K.nz + 2);
+    for (int i = threadIdx.x; i < nf; i += blockDim.x) sh_faces[i] = K.xface[i];  // faces are contiguous
+    xf = sh_faces;
+    yf = sh_faces + (K.nx + 1);
+    zf = yf + (K.ny + 1);
+  }
+#pragma unroll
+  for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
+  __syncthreads();
+
+  Lane L;
+  L.st = ST_FETCH; L.pend = false; L.seg = false; L.fault = false; L.tflag = false;
+  L.c_sdf = L.c_dep = L.c_upd = 0;
+  L.pos = L.dir = L.startPos = L.ssp = L.old = v3(0.0, 0.0, 0.0);
+  L.weight = 1.0; L.tau = L.taurun = L.d = L.minabs = L.minv = 0.0;
+  L.xcell = L.ycell = L.zcell = L.layer = L.old_layer = L.new_layer = L.Ls = 0;
+  L.bounces = L.nscatt = L.status = L.hop = L.loopc = L.inter = L.dda_it = 0;
+  L.sd = L.slen = 0.0; L.ci = L.cj = L.ck = 0;
+  L.rng.init(0);
+
+  for (;;) {
+    // ---- photon fetch (wave-aggregated work queue) ------------------------------------
+    {
+      const uint64_t need = __ballot(L.st == ST_FETCH);
+      if (need) {
+        const uint32_t n = __popcll(need);
+        const int leader = __ffsll((long long)need) - 1;
+        unsigned long long base = 0;
+        if (lane_id == leader) base = atomicAdd(K.queue, (unsigned long long)n);
+        base = __shfl(base, leader, 64);
+        if (L.st == ST_FETCH) {
+          const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
+          const uint64_t idx = base + rank;
+          if (idx < K.n_photons) { L.rng.init(K.first_photon + idx); L.st = ST_EMIT; }
+          else L.st = ST_IDLE;
+        }
+      }
+      if (__ballot(L.st != ST_IDLE) == 0) break;
+    }
+
+    // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
+    if (L.seg) {
+#pragma unroll
+      for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {
+        if (L.seg) dda_step(K, L, xf, yf, zf);
+      }
+    }
+
+    // ---- EVAL phase: the SDF array at the lane's query point ----------------------------
+    EvalOut R;
+    R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
+    if (!L.seg && L.pend) {
+      const bool fres = (L.st == ST_F0 || L.st == ST_F1);
+      const bool tap = (L.st >= ST_N1 && L.st <= ST_N4);
+      const int32_t capi = fres ? L.new_layer : (tap ? L.Ls : 0);
+      const int32_t capj = fres ? L.old_layer : 0;
+      R = eval_sdfs(K, eval_query(L), test_kernel && L.st == ST_LAYER, capi, capj);
+      // packet%cnts counts the evaluations of tauint2's ds/dsNew arrays only (inttau2.f90:67,83,
+      // 138,183,219,232): not the initial layer search, the Fresnel ds lookups or calcNormal.
+      if (L.st == ST_H0 || L.st == ST_H1 || L.st == ST_H3 || L.st == ST_M1 || L.st == ST_G0)
+        L.c_sdf += (uint32_t)K.n_top;
+    }
+
+    // ---- ADVANCE phase: reference control flow up to the next EVAL / deposit ------------
+    bool rec = false;
+    V3 rec_start = v3(0.0, 0.0, 0.0), rec_dir = rec_start;
+    double rec_sep = 0.0, rec_w = 0.0;
+    int32_t rec_layer = 0;
+    if (!L.seg && L.st != ST_IDLE && L.st != ST_FETCH) {
+      bool have = L.pend;
+      L.pend = false;
+      bool yield = false;
+      for (int guard = 0; guard < 64 && !yield; ++guard) {
+        switch (L.st) {
+          case ST_EMIT: {  // kernelsMod.f90:1937-1945
+            L.fault = false; L.status = 0; L.nscatt = 0; L.layer = 0; L.inter = 0;
+            L.xcell = L.ycell = L.zcell = 0;
+            emit(K, L);
+            if (!test_kernel) {
+              int64_t tries = 0;
+              while (cell_out(K, L)) {
+                if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
+                LCTR(LC_RETRIES)++;
+                emit(K, L);
+              }
+              if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, K.emission, L, 1.0);
+            }
+            if (L.fault) { L.st = ST_DONE; break; }
+            ARRIVE(ST_LAYER);
+            break;
+          }
+          case ST_LAYER:  // :1948-1952 (test_kernel: mask ds<=0, :2136)
+            have = false;
+            L.layer = R.maxloc;
+            if (L.layer == 0) { L.fault = true; L.st = ST_DONE; break; }
+            L.st = ST_T2;
+            break;
+          case ST_T2:  // tauint2 entry, inttau2.f90:48-60
+            L.startPos = L.pos;
+            sh->entry[0][threadIdx.x] = L.pos.x; sh->entry[1][threadIdx.x] = L.pos.y;
+            sh->entry[2][threadIdx.x] = L.pos.z; sh->entry[3][threadIdx.x] = L.dir.x;
+            sh->entry[4][threadIdx.x] = L.dir.y; sh->entry[5][threadIdx.x] = L.dir.z;
+            LCTR(LC_TAU)++;
+            L.tau = -det_log(L.rng.next(K.key0, K.key1));
+            L.taurun = 0.0;
+            L.hop = 0;
+            L.st = ST_H0;
+            break;
+          case ST_H0:  // hop loop head, :61-73
+            if (!have) {
+              if (!(L.taurun <= L.tau)) { L.st = ST_T2END; break; }
+              if (++L.hop > (uint32_t)MAX_HOP_ITERS) { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }
+              ARRIVE(ST_H0);
+              break;
+            }
+            have = false;
+            L.minabs = R.minabs; L.minv = R.minv;
+            L.d = R.minabs;
+            L.loopc = 0;  // march guard
+            if (L.d < eps) {  // on a surface: micro-step, :73-84
+              L.d = R.minabs + 2.0 * eps;
+              L.ssp = L.pos + smul(L.d, L.dir);
+              ARRIVE(ST_H1);
+              break;
+            }
+            L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;  // :149-152
+            break;
+          case ST_H1: {  // forward / backward micro-step, :86-123
+            have = false;
+            const double kap = K.props[L.layer - 1].kappa;
+            const V3 oldpos = L.pos;
+            const double t = L.d * kap;
+            if (R.maxloc == L.layer) {
+              if (L.taurun + t < L.tau) { L.pos = L.pos + smul(L.d, L.dir); L.taurun = L.taurun + t; }
+              else { L.d = (L.tau - L.taurun) / kap; L.taurun = L.taurun + t; }
+            } else {
+              if (L.taurun + t < L.tau) { L.pos = L.pos - smul(L.d, L.dir); L.taurun = L.taurun + t; }
+              else { L.d = (L.tau - L.taurun) / kap; L.pos = L.pos - smul(L.d, L.dir); }
+            }
+            L.st = ST_H2;
+            yield = start_segment(K, L, oldpos, L.d);
+            break;
+          }
+          case ST_H2:  // detectors, :125-131
+            rec = true; rec_start = L.startPos; rec_dir = L.dir; rec_sep = pointsep(L.pos, L.startPos);
+            rec_layer = L.layer; rec_w = L.weight;
+            L.startPos = L.pos;
+            ARRIVE(ST_H3);
+            break;
+          case ST_H3:  // :133-152
+            have = false;
+            L.minabs = R.minabs; L.minv = R.minv;
+            L.d = R.minabs;
+            if (R.minv > 0.0) L.tflag = true;
+            L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;
+            break;
+          case ST_M0: {  // march loop head, :155-176
+            if (!(L.d >= eps)) { L.st = ST_B0; break; }
+            if (++L.loopc > (uint32_t)MAX_MARCH_ITERS) { L.fault = true; L.tflag = true; L.st = ST_B0; break; }
+            const double kap = K.props[L.layer - 1].kappa;
+            const double t = L.d * kap;
+            const V3 oldpos = L.pos;
+            if (L.taurun + t < L.tau) {
+              L.taurun = L.taurun + t;
+              L.pos = L.pos + smul(L.d, L.dir);
+              start_segment(K, L, oldpos, L.d);
+              ARRIVE(ST_M1);
+            } else {
+              L.d = (L.tau - L.taurun) / kap;
+              L.taurun = L.tau;
+              L.pos = L.pos + smul(L.d, L.dir);
+              L.st = ST_B0;
+              yield = start_segment(K, L, oldpos, L.d);
+            }
+            break;
+          }
+          case ST_M1:  // :177-191
+            have = false;
+            L.minabs = R.minabs; L.minv = R.minv;
+            L.d = R.minabs;
+            if (R.minv > 0.0) { L.tflag = true; L.st = ST_B0; }
+            else L.st = ST_M0;
+            break;
+          case ST_B0:  // detectors and boundary probe, :195-221
+            rec = true; rec_start = L.startPos; rec_dir = L.dir; rec_sep = pointsep(L.pos, L.startPos);
+            rec_layer = L.layer; rec_w = L.weight;
+            L.startPos = L.pos;
+            if (L.taurun >= L.tau || L.tflag) { L.st = ST_T2END; break; }
+            L.d = L.minabs + 2.0 * eps;
+            L.ssp = L.pos + smul(L.d, L.dir);
+            L.old_layer = L.layer;
+            L.loopc = 0;  // glancing guard
+            ARRIVE(ST_G0);
+            break;
+          case ST_G0: {  // new layer and the glancing loop, :220-245
+            have = false;
+            L.new_layer = R.maxloc;
+            if (L.new_layer == L.old_layer && R.minabs < eps) {
+              if (++L.loopc > (uint32_t)MAX_GLANCE_ITERS) { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }
+              L.d = L.d + eps;
+              L.ssp = L.pos + smul(L.d, L.dir);
+              ARRIVE(ST_G0);
+              break;
+            }
+            if (L.new_layer == 0) { L.tflag = true; L.st = ST_T2END; break; }
+            const double n1 = K.props[L.layer - 1].n, n2 = K.props[L.new_layer - 1].n;
+            if (n1 != n2) { ARRIVE(ST_F0); break; }
+            L.layer = L.new_layer;  // equal n: cross, :318-328
+            L.st = ST_X1;
+            yield = start_segment(K, L, L.pos, L.d);
+            break;
+          }
+          case ST_X1:  // after the crossing deposit, :294-303 / :326-335
+            L.taurun = L.taurun + L.d * K.props[L.layer - 1].kappa;
+            L.pos = L.ssp;
+            rec = true; rec_start = L.startPos; rec_dir = L.dir; rec_sep = pointsep(L.pos, L.startPos);
+            rec_layer = L.layer; rec_w = L.weight;
+            L.startPos = L.pos;
+            if (L.tflag) { L.st = ST_T2END; break; }
+            L.st = ST_H0;
+            break;
+          case ST_F0:  // ds(new), ds(old) at pos (kept in sd/slen: no segment is active)
+            have = false;
+            L.sd = R.va; L.slen = R.vb;
+            ARRIVE(ST_F1);
+            break;
+          case ST_F1: {  // which SDF's normal, :250-277
+            have = false;
+            const double ds_new = L.sd, ds_old = L.slen, dn_new = R.va, dn_old = R.vb;
+            if (dn_new < 0.0 && ds_new >= 0.0) L.Ls = L.new_layer;
+            else if (dn_old >= 0.0 && ds_old < 0.0) L.Ls = L.old_layer;
+            else if (dn_new < 0.0 && dn_old < 0.0) L.Ls = L.new_layer;
+            else if (ds_old >= 0.0 && dn_old >= 0.0) L.Ls = L.old_layer;
+            else { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }  // error stop :264-277
+            ARRIVE(ST_N1);
+            break;
+          }
+          case ST_N1: have = false; L.old.x = R.va; ARRIVE(ST_N2); break;  // calcNormal taps in old.xyz
+          case ST_N2: have = false; L.old.y = R.va; ARRIVE(ST_N3); break;
+          case ST_N3: have = false; L.old.z = R.va; ARRIVE(ST_N4); break;
+          case ST_N4: {  // calcNormal (sdf_base.f90:166-190) + reflect_refract (surfaces.f90:14-84)
+            have = false;
+            const double e4 = R.va;
+            const V3 xyy = v3(1.0, -1.0, -1.0), yyx = v3(-1.0, -1.0, 1.0), yxy = v3(-1.0, 1.0, -1.0),
+                     xxx = v3(1.0, 1.0, 1.0);
+            const V3 nn = ((mul(xyy, L.old.x) + mul(yyx, L.old.y)) + mul(yxy, L.old.z)) + mul(xxx, e4);
+            const double ln = len(nn);
+            const V3 N = v3(nn.x / ln, nn.y / ln, nn.z / ln);
+            const double n1 = K.props[L.layer - 1].n, n2 = K.props[L.new_layer - 1].n;
+            LCTR(LC_FRES)++;
+            const double Rf = fresnel(L.dir, N, n1, n2);
+            if (L.rng.next(K.key0, K.key1) <= Rf) {  // reflect :42-55, :304-316
+              const double s2 = 2.0 * dot(N, L.dir);
+              L.dir = L.dir - smul(s2, N);
+              LCTR(LC_REFL)++;
+              L.startPos = L.pos;
+              L.bounces += 1;
+              if (L.bounces > 1000) {  // :313-315: return without write-back
+                LCTR(LC_BABORT)++;
+                L.pos = v3(sh->entry[0][threadIdx.x], sh->entry[1][threadIdx.x], sh->entry[2][threadIdx.x]);
+                L.dir = v3(sh->entry[3][threadIdx.x], sh->entry[4][threadIdx.x], sh->entry[5][threadIdx.x]);
+                L.st = ST_INTERACT;
+                break;
+              }
+              L.st = ST_H0;
+            } else {  // refract :57-84, transmit :284-303
+              const double eta = n1 / n2;
+              V3 Nt = N;
+              double c1 = dot(Nt, L.dir);
+              if (c1 < 0.0) c1 = -c1;
+              else Nt = smul(-1.0, N);
+              const double c2 = sqrt(1.0 - (eta * eta) * (1.0 - c1 * c1));
+              L.dir = smul(eta, L.dir) + smul(eta * c1 - c2, Nt);
+              L.layer = L.new_layer;
+              L.st = ST_X1;
+              yield = start_segment(K, L, L.pos, L.d);
+            }
+            break;
+          }
+          case ST_T2END:  // tauint2 write-back checks, :341-362
+            if (fabs(L.pos.x) > K.xmax) L.tflag = true;
+            if (fabs(L.pos.y) > K.ymax) L.tflag = true;
+            if (fabs(L.pos.z) > K.zmax) L.tflag = true;
+            L.st = ST_INTERACT;
+            break;
+          case ST_INTERACT: {  // kernelsMod.f90:1958-1975 / 2036-2065 / 2126-2170
+            if (L.tflag || L.fault) { L.st = ST_DONE; break; }
+            if (++L.inter > (uint32_t)MAX_INTERACTIONS) { L.fault = true; L.st = ST_DONE; break; }
+            const double ran = L.rng.next(K.key0, K.key1);
+            const TopProps pr = K.props[L.layer - 1];
+            if (survival) {
+              const double w_abs = L.weight * (1.0 - pr.albedo);
+              L.weight = L.weight - w_abs;
+              add_cell(K, K.absorb, L, w_abs);
+              if (L.weight < 0.01) {
+                if (ran < 0.1) L.weight = L.weight / 0.1;
+                else { L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++; L.st = ST_DONE; break; }
+              }
+              scatter(K, L, pr.hgg);
+              L.nscatt++; LCTR(LC_SCATTERS)++;
+            } else if (ran < pr.albedo) {
+              scatter(K, L, pr.hgg);
+              L.nscatt++; LCTR(LC_SCATTERS)++;
+              if (test_kernel) {
+                const uint32_t st = L.nscatt;
+                if (st >= 1 && st <= 4) {
+                  if (K.moments) {
+                    double* m = K.moments + 3 * (st - 1);
+                    double* m2 = K.moments + 12 + 3 * (st - 1);
+                    atomic_add_nr(m + 0, L.pos.x); atomic_add_nr(m + 1, L.pos.y); atomic_add_nr(m + 2, L.pos.z);
+                    atomic_add_nr(m2 + 0, L.pos.x * L.pos.x);
+                    atomic_add_nr(m2 + 1, L.pos.y * L.pos.y);
+                    atomic_add_nr(m2 + 2, L.pos.z * L.pos.z);
+                  }
+                } else if (K.flags & SMCRT_FLAG_END_EARLY) {
+                  L.tflag = true;
+                  L.status = 4;
+                }
+              }
+            } else {
+              L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++;
+              if (!test_kernel) add_cell(K, K.absorb, L, 1.0);  // recordWeight(packet, 1.0)
+              L.st = ST_DONE;
+              break;
+            }
+            L.st = ST_T2;
+            break;
+          }
+          case ST_DONE: {  // photon finished
+            if (L.fault) { L.status = 3; LCTR(LC_FAULTS)++; }
+            else if (L.status == 0) { L.status = 2; LCTR(LC_ESCAPED)++; }
+            LCTR(LC_PHOTONS)++;
+            LCTR(LC_DRAWS) += L.rng.draws;
+            if (rec_on) {
+              const uint64_t pid = ((uint64_t)L.rng.pid_hi << 32) | L.rng.pid_lo;
+              smcrt_photon_record* r = K.records + (pid - K.first_photon);
+              r->pos[0] = L.pos.x; r->pos[1] = L.pos.y; r->pos[2] = L.pos.z;
+              r->dir[0] = L.dir.x; r->dir[1] = L.dir.y; r->dir[2] = L.dir.z;
+              r->weight = L.weight;
+              r->cell[0] = L.xcell; r->cell[1] = L.ycell; r->cell[2] = L.zcell;
+              r->layer = L.layer;
+              r->nscatt = L.nscatt;
+              r->bounces = L.bounces;
+              r->draws = L.rng.draws;
+              r->status = L.status;
+            }
+            L.tflag = false; L.fault = false;
+            L.st = ST_FETCH;
+            yield = true;
+            break;
+          }
+          default:
+            yield = true;
+            break;
+        }
+      }
+    }
+    if (K.n_dets && rec) LCTR(LC_HITS) += record_hits(K, rec_start, rec_dir, rec_sep, rec_layer, rec_w);
+  }
+
+  // ---- per-wave counter reduction ------------------------------------------------------
   if (K.counters) {
+    uint32_t c[SMCRT_NCOUNTERS];
+    c[SMCRT_CTR_PHOTONS] = LCTR(LC_PHOTONS);
+    c[SMCRT_CTR_EMIT_RETRIES] = LCTR(LC_RETRIES);
+    c[SMCRT_CTR_SCATTERS] = LCTR(LC_SCATTERS);
+    c[SMCRT_CTR_ABSORBED] = LCTR(LC_ABSORBED);
+    c[SMCRT_CTR_SDF_EVALS] = L.c_sdf;
+    c[SMCRT_CTR_DEPOSITS] = L.c_dep;
+    c[SMCRT_CTR_GRID_UPDATES] = L.c_upd;
+    c[SMCRT_CTR_TAUINT] = LCTR(LC_TAU);
+    c[SMCRT_CTR_FRESNEL] = LCTR(LC_FRES);
+    c[SMCRT_CTR_REFLECTIONS] = LCTR(LC_REFL);
+    c[SMCRT_CTR_BOUNCE_ABORTS] = LCTR(LC_BABORT);
+    c[SMCRT_CTR_FAULTS] = LCTR(LC_FAULTS);
+    c[SMCRT_CTR_RNG_DRAWS] = LCTR(LC_DRAWS);
+    c[SMCRT_CTR_DETECTOR_HITS] = LCTR(LC_HITS);
+    c[SMCRT_CTR_ESCAPED] = LCTR(LC_ESCAPED);
+    c[15] = 0;
 #pragma unroll
     for (int i = 0; i < SMCRT_NCOUNTERS; ++i) {
-      const uint32_t s = wave_sum_u32(L.c.v[i]);
-      if (lane == 0 && s) atomicAdd(K.counters + i, (unsigned long long)s);
+      const uint32_t s = wave_sum_u32(c[i]);
+      if (lane_id == 0 && s) atomicAdd(K.counters + i, (unsigned long long)s);
     }
   }
-  if (K.nscatt) {
-    const double s = wave_sum_f64(L.nscatt);
-    if (lane == 0 && s != 0.0) atomic_add_nr(K.nscatt, s);
+  if (K.nscatt) {  // nscatt = number of scatters (kernelsMod.f90:1966)
+    const uint32_t s = wave_sum_u32(LCTR(LC_SCATTERS));
+    if (lane_id == 0 && s) atomic_add_nr(K.nscatt, (double)s);
   }
 }
 
@@ -101,7 +499,9 @@ struct smcrt_scene {
   std::vector<smcrt_detector> h_dets;
   std::vector<int64_t> h_det_off;
   smcrt_sdf_node* d_nodes = nullptr;
-  int32_t* d_top = nullptr;
+  ProgOp* d_prog = nullptr;
+  int n_prog = 0;
+  double inv2[3] = {0.0, 0.0, 0.0};
   TopProps* d_props = nullptr;
   double* d_faces = nullptr;
   smcrt_detector* d_dets = nullptr;
@@ -115,6 +515,8 @@ struct smcrt_scene {
   size_t records_cap = 0;
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
+  bool lds_faces = false;
+  size_t face_bytes = 0;
   std::mutex mu;
 };
 
@@ -147,7 +549,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  void* ptrs[] = {s->d_nodes, s->d_top, s->d_props, s->d_faces, s->d_dets, s->d_det_off,
+  void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off,
                   s->d_queue, s->d_grids, s->d_small, s->d_counters, s->d_records};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -221,7 +623,27 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   };
   if (hipSetDevice(device) != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, "hipSetDevice failed"));
   int st;
-  if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_top, n_top)) || (st = dalloc(&s->d_props, n_top)) ||
+  // flatten the SDF array into one evaluation program (eval_model fold order)
+  std::vector<ProgOp> prog;
+  for (int32_t i = 0; i < n_top; ++i) {
+    const smcrt_sdf_node& nd = nodes[top[i]];
+    if (nd.kind != SMCRT_SDF_MODEL) {
+      prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0});
+    } else {
+      for (int32_t c = 0; c < nd.n_children; ++c)
+        prog.push_back(ProgOp{nd.first_child + c, c == 0 ? PROG_CHILD_FIRST : PROG_CHILD,
+                              c == nd.n_children - 1 ? i + 1 : 0, nd.op, nd.k});
+    }
+  }
+  s->n_prog = (int)prog.size();
+  // n*p/(2*max) may be computed as n*p*inv exactly when 2*max is a power of two
+  const double maxes[3] = {grid->xmax, grid->ymax, grid->zmax};
+  for (int a = 0; a < 3; ++a) {
+    int ex = 0;
+    const double m = std::frexp(2.0 * maxes[a], &ex);
+    s->inv2[a] = (m == 0.5 && std::isfinite(1.0 / (2.0 * maxes[a]))) ? 1.0 / (2.0 * maxes[a]) : 0.0;
+  }
+  if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
       (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, 1)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
@@ -229,7 +651,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     return cleanup_fail(st);
   hipError_t e = hipSuccess;
   if (e == hipSuccess) e = hipMemcpy(s->d_nodes, nodes, sizeof(smcrt_sdf_node) * n_nodes, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(s->d_top, top, sizeof(int32_t) * n_top, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(s->d_prog, prog.data(), sizeof(ProgOp) * prog.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_props, s->h_props.data(), sizeof(TopProps) * n_top, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_faces, faces.data(), sizeof(double) * faces.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && n_dets)
@@ -239,8 +661,12 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
   int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel, 256, 0) != hipSuccess || per_cu < 1)
-    per_cu = 1;
+  s->face_bytes = faces.size() * sizeof(double);
+  s->lds_faces = s->face_bytes <= 32768;  // stage the voxel faces in LDS when they fit
+  hipError_t oe = s->lds_faces
+      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel<true>, 256, s->face_bytes)
+      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel<false>, 256, 0);
+  if (oe != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   s->grid_blocks = cus * per_cu;
   *out = s;
@@ -271,7 +697,9 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   if (cfg->n_photons == 0) return SMCRT_OK;
   KParams K;
   K.nodes = s->d_nodes;
-  K.top = s->d_top;
+  K.prog = s->d_prog;
+  K.n_prog = s->n_prog;
+  K.inv2x = s->inv2[0]; K.inv2y = s->inv2[1]; K.inv2z = s->inv2[2];
   K.props = s->d_props;
   K.xface = s->d_faces;
   K.yface = s->d_faces + (s->grid.nx + 1);
@@ -287,6 +715,8 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.n_photons = cfg->n_photons;
   K.first_photon = cfg->first_photon;
   K.seed = cfg->seed;
+  K.key0 = (uint32_t)cfg->seed;
+  K.key1 = (uint32_t)(cfg->seed >> 32);
   K.jmean = dt.jmean; K.absorb = dt.absorb; K.emission = dt.emission;
   K.det_bins = dt.det_bins; K.nscatt = dt.nscatt; K.moments = dt.moments;
   K.counters = (unsigned long long*)dt.counters;
@@ -296,7 +726,10 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   const uint64_t waves_needed = (cfg->n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
   const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
-  hipLaunchKernelGGL(transport_kernel, dim3(blocks), dim3(256), 0, stream, K);
+  if (s->lds_faces)
+    hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K);
+  else
+    hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K);
   HIPCHK(hipGetLastError());
   return SMCRT_OK;
 }
