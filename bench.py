@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--seed", type=int, default=123456789)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
+    ap.add_argument("--source", default="point", choices=["point", "uniform"],
+                    help="diagnostic: uniform = parallelogram source over the z=0.99 plane")
     args = ap.parse_args()
 
     import torch
@@ -91,6 +94,10 @@ def main():
     from rsmcrt_amd.engine import Engine
 
     sc, g, src = workload(args.grid)
+    if args.source == "uniform":
+        from rsmcrt_amd import scene as _scene
+        src = _scene.uniform_source((-1.0, -1.0, 0.99), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    run_flags = 0 if args.no_deposit else abi.FLAG_PATHLENGTH
     eng = Engine(sc, g, device=torch.cuda.current_device())
     nv = g.nx * g.ny * g.nz
     jmean = torch.zeros(nv, dtype=torch.float64, device=dev)
@@ -104,7 +111,7 @@ def main():
     B = args.batch
 
     def step(s):
-        cfg = Engine.config(B, seed=args.seed, flags=abi.FLAG_PATHLENGTH, first_photon=(s * world + rank) * B)
+        cfg = Engine.config(B, seed=args.seed, flags=run_flags, first_photon=(s * world + rank) * B)
         eng.run_device(src, cfg, dt_, stream.cuda_stream)
 
     for s in range(args.warmup):

@@ -1,0 +1,156 @@
+! smcrt_mod.f90 — ISO_C_BINDING interface to the MI355X engine (include/smcrt.h).
+!
+! The module a signedMCRT maintainer adds next to src/kernelsMod.f90 so that run_MCRT
+! (kernelsMod.f90:1790-1898) can hand its photon loop to the GPU. Every type below is
+! bind(C) and matches the C struct of the same name field for field; every interface binds
+! one entry point of include/smcrt.h. See INTEGRATION.md for the run_MCRT body that uses it.
+module smcrt_mod
+    use iso_c_binding
+    implicit none
+
+    integer(c_int), parameter :: SMCRT_OK = 0
+    ! smcrt_sdf_kind
+    integer(c_int32_t), parameter :: SMCRT_SDF_SPHERE = 1, SMCRT_SDF_BOX = 2, SMCRT_SDF_TORUS = 3, &
+        SMCRT_SDF_CYLINDER = 4, SMCRT_SDF_TRIPRISM = 5, SMCRT_SDF_SEGMENT = 6, SMCRT_SDF_CAPSULE = 7, &
+        SMCRT_SDF_CONE = 8, SMCRT_SDF_EGG = 9, SMCRT_SDF_PLANE = 10, SMCRT_SDF_MODEL = 11
+    ! smcrt_csg_op
+    integer(c_int32_t), parameter :: SMCRT_OP_UNION = 0, SMCRT_OP_SMOOTH_UNION = 1, &
+        SMCRT_OP_SUBTRACTION = 2, SMCRT_OP_INTERSECTION = 3
+    ! smcrt_source_kind
+    integer(c_int32_t), parameter :: SMCRT_SRC_POINT = 1, SMCRT_SRC_UNIFORM = 2, SMCRT_SRC_PENCIL = 3
+    ! smcrt_detector_kind
+    integer(c_int32_t), parameter :: SMCRT_DET_CIRCLE = 1, SMCRT_DET_ANNULUS = 2, SMCRT_DET_CAMERA = 3, &
+        SMCRT_DET_FIBRE = 4
+    ! run flags
+    integer(c_int32_t), parameter :: SMCRT_FLAG_PATHLENGTH = 1, SMCRT_FLAG_SURVIVAL_BIAS = 2, &
+        SMCRT_FLAG_RENDER_SOURCE = 4, SMCRT_FLAG_TEST_KERNEL = 8, SMCRT_FLAG_END_EARLY = 16, &
+        SMCRT_FLAG_RECORD_PHOTONS = 32
+    integer, parameter :: SMCRT_NCOUNTERS = 16
+
+    type, bind(C) :: smcrt_sdf_node
+        integer(c_int32_t) :: kind = 0, layer = 0, op = 0, first_child = 0, n_children = 0
+        integer(c_int32_t) :: reserved(3) = 0
+        real(c_double)     :: transform(16) = 0._c_double   ! = reshape(sdf%transform, [16])
+        real(c_double)     :: param(12) = 0._c_double
+        real(c_double)     :: k = 0._c_double
+        real(c_double)     :: mus = 0._c_double, mua = 0._c_double, hgg = 0._c_double, n = 1._c_double
+    end type smcrt_sdf_node
+
+    type, bind(C) :: smcrt_grid
+        integer(c_int32_t) :: nx, ny, nz, reserved = 0
+        real(c_double)     :: xmax, ymax, zmax
+    end type smcrt_grid
+
+    type, bind(C) :: smcrt_source
+        integer(c_int32_t) :: kind, reserved = 0
+        real(c_double)     :: pos(3) = 0._c_double, dir(3) = 0._c_double
+        real(c_double)     :: p1(3) = 0._c_double, p2(3) = 0._c_double, p3(3) = 0._c_double
+    end type smcrt_source
+
+    type, bind(C) :: smcrt_detector
+        integer(c_int32_t) :: kind = 0, nbins = 0, layer = 0, reserved = 0
+        real(c_double)     :: pos(3) = 0._c_double, dir(3) = 0._c_double
+        real(c_double)     :: e1(3) = 0._c_double, e2(3) = 0._c_double
+        real(c_double)     :: radius = 0._c_double, r1 = 0._c_double, r2 = 0._c_double
+        real(c_double)     :: width = 0._c_double, height = 0._c_double
+        real(c_double)     :: bin_wid = 0._c_double, bin_wid_y = 0._c_double
+        real(c_double)     :: fibre(11) = 0._c_double
+    end type smcrt_detector
+
+    type, bind(C) :: smcrt_run_config
+        integer(c_int64_t) :: n_photons, first_photon = 0, seed
+        integer(c_int32_t) :: flags, reserved = 0
+    end type smcrt_run_config
+
+    type, bind(C) :: smcrt_tallies
+        type(c_ptr) :: jmean = c_null_ptr, absorb = c_null_ptr, emission = c_null_ptr
+        type(c_ptr) :: jmean_f64 = c_null_ptr, absorb_f64 = c_null_ptr, emission_f64 = c_null_ptr
+        type(c_ptr) :: det_bins = c_null_ptr, nscatt = c_null_ptr, moments = c_null_ptr
+        type(c_ptr) :: counters = c_null_ptr, records = c_null_ptr
+    end type smcrt_tallies
+
+    interface
+        integer(c_int) function smcrt_abi_version() bind(C, name="smcrt_abi_version")
+            import :: c_int
+        end function smcrt_abi_version
+
+        integer(c_int) function smcrt_device_count(count) bind(C, name="smcrt_device_count")
+            import :: c_int, c_int32_t
+            integer(c_int32_t), intent(out) :: count
+        end function smcrt_device_count
+
+        type(c_ptr) function smcrt_last_error() bind(C, name="smcrt_last_error")
+            import :: c_ptr
+        end function smcrt_last_error
+
+        integer(c_int) function smcrt_scene_create(nodes, n_nodes, top, n_top, grid, dets, n_dets, &
+                                                   device, scene) bind(C, name="smcrt_scene_create")
+            import :: c_int, c_int32_t, c_ptr, smcrt_sdf_node, smcrt_grid, smcrt_detector
+            type(smcrt_sdf_node), intent(in)  :: nodes(*)
+            integer(c_int32_t), value         :: n_nodes
+            integer(c_int32_t), intent(in)    :: top(*)
+            integer(c_int32_t), value         :: n_top
+            type(smcrt_grid), intent(in)      :: grid
+            type(smcrt_detector), intent(in)  :: dets(*)
+            integer(c_int32_t), value         :: n_dets, device
+            type(c_ptr), intent(out)          :: scene
+        end function smcrt_scene_create
+
+        subroutine smcrt_scene_destroy(scene) bind(C, name="smcrt_scene_destroy")
+            import :: c_ptr
+            type(c_ptr), value :: scene
+        end subroutine smcrt_scene_destroy
+
+        integer(c_int) function smcrt_scene_det_bins(scene, n) bind(C, name="smcrt_scene_det_bins")
+            import :: c_int, c_int64_t, c_ptr
+            type(c_ptr), value              :: scene
+            integer(c_int64_t), intent(out) :: n
+        end function smcrt_scene_det_bins
+
+        integer(c_int) function smcrt_scene_set_optprops(scene, top_index, mus, mua, hgg, n) &
+                bind(C, name="smcrt_scene_set_optprops")
+            import :: c_int, c_int32_t, c_double, c_ptr
+            type(c_ptr), value        :: scene
+            integer(c_int32_t), value :: top_index
+            real(c_double), value     :: mus, mua, hgg, n
+        end function smcrt_scene_set_optprops
+
+        integer(c_int) function smcrt_run(scene, src, cfg, io) bind(C, name="smcrt_run")
+            import :: c_int, c_ptr, smcrt_source, smcrt_run_config, smcrt_tallies
+            type(c_ptr), value                 :: scene
+            type(smcrt_source), intent(in)     :: src
+            type(smcrt_run_config), intent(in) :: cfg
+            type(smcrt_tallies), intent(inout) :: io
+        end function smcrt_run
+
+        integer(c_int) function smcrt_normalise_fluence(grid_data, grid, nphotons) &
+                bind(C, name="smcrt_normalise_fluence")
+            import :: c_int, c_int64_t, c_float, smcrt_grid
+            real(c_float), intent(inout) :: grid_data(*)
+            type(smcrt_grid), intent(in) :: grid
+            integer(c_int64_t), value    :: nphotons
+        end function smcrt_normalise_fluence
+    end interface
+
+contains
+
+    function smcrt_error_message() result(msg)
+        !! Copy smcrt_last_error() into a Fortran string.
+        character(len=:), allocatable :: msg
+        character(kind=c_char), pointer :: p(:)
+        integer :: i, n
+        type(c_ptr) :: cp
+        cp = smcrt_last_error()
+        call c_f_pointer(cp, p, [4096])
+        n = 0
+        do i = 1, 4096
+            if (p(i) == c_null_char) exit
+            n = i
+        end do
+        allocate(character(len=n) :: msg)
+        do i = 1, n
+            msg(i:i) = p(i)
+        end do
+    end function smcrt_error_message
+
+end module smcrt_mod

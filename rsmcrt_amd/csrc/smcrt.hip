@@ -33,13 +33,6 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-// Arrive at an EVAL program point: the query is evaluated in the next EVAL phase (its
-// point and captured indices are derived from the state, see eval_query).
-#define ARRIVE(state)                 \
-  do {                                \
-    L.st = (state); L.pend = true;    \
-    yield = true;                     \
-  } while (0)
 #define LCTR(c) (sh->ctr[(c)][threadIdx.x])
 
 // The query point of each EVAL state (the exact expressions of the reference).
@@ -55,9 +48,11 @@ __device__ __forceinline__ V3 eval_query(const Lane& L) {
 }
 
 template <bool LDS_FACES>
-__global__ __launch_bounds__(256) void transport_kernel(KParams K) {
+__global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
+                                                        const ProgOp* __restrict__ prog,
+                                                        const smcrt_detector* __restrict__ dets,
+                                                        const int64_t* __restrict__ det_off) {
   __shared__ LaneShared shm;
-  extern __shared__ double sh_faces[];
   LaneShared* sh = &shm;
   const double eps = 1e-8;  // inttau2.f90:56
   const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
@@ -65,12 +60,21 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K) {
   const bool rec_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) && K.records;
   const int lane_id = threadIdx.x & 63;
 
+  extern __shared__ double sh_dyn[];  // [props (4 doubles per top-level SDF) | faces]
+  const TopProps* props = K.props;
   const double* xf = K.xface;
   const double* yf = K.yface;
   const double* zf = K.zface;
   if constexpr (LDS_FACES) {
+    // per-lane (divergent) lookups go to LDS, never to vector memory: a vector load would
+    // make the wave wait for all of its outstanding deposit atomics
+    const int np = 4 * K.n_top;
+    const double* gp = (const double*)K.props;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) sh_dyn[i] = gp[i];
     const int nf = (K.nx + 1) + (K.ny + 1) + (K.nz + 2);
+    double* sh_faces = sh_dyn + np;
     for (int i = threadIdx.x; i < nf; i += blockDim.x) sh_faces[i] = K.xface[i];  // faces are contiguous
+    props = (const TopProps*)sh_dyn;
     xf = sh_faces;
     yf = sh_faces + (K.nx + 1);
     zf = yf + (K.ny + 1);
@@ -88,23 +92,40 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K) {
   L.bounces = L.nscatt = L.status = L.hop = L.loopc = L.inter = L.dda_it = 0;
   L.sd = L.slen = 0.0; L.ci = L.cj = L.ck = 0;
   L.rng.init(0);
+  uint64_t chunk_base = 0;  // wave-uniform photon chunk
+  uint32_t chunk_left = 0;
 
   for (;;) {
     // ---- photon fetch (wave-aggregated work queue) ------------------------------------
+    // A wave takes FETCH_CHUNK photon indices per (returning) queue atomic and hands them
+    // to its lanes as they free up: a returning atomic waits for all of the wave's
+    // outstanding deposits, so it must be rare.
     {
-      const uint64_t need = __ballot(L.st == ST_FETCH);
-      if (need) {
-        const uint32_t n = __popcll(need);
-        const int leader = __ffsll((long long)need) - 1;
-        unsigned long long base = 0;
-        if (lane_id == leader) base = atomicAdd(K.queue, (unsigned long long)n);
-        base = __shfl(base, leader, 64);
-        if (L.st == ST_FETCH) {
-          const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
-          const uint64_t idx = base + rank;
-          if (idx < K.n_photons) { L.rng.init(K.first_photon + idx); L.st = ST_EMIT; }
-          else L.st = ST_IDLE;
+      uint64_t need = __ballot(L.st == ST_FETCH);
+      while (need) {
+        if (chunk_left == 0) {
+          unsigned long long base = 0;
+          if (lane_id == 0) base = atomicAdd(K.queue, (unsigned long long)SMCRT_FETCH_CHUNK);
+          chunk_base = __shfl(base, 0, 64);
+          chunk_left = (chunk_base < K.n_photons)
+                           ? (uint32_t)((K.n_photons - chunk_base) < SMCRT_FETCH_CHUNK ? (K.n_photons - chunk_base)
+                                                                                       : SMCRT_FETCH_CHUNK)
+                           : 0u;
+          if (chunk_left == 0) {  // queue exhausted
+            if (L.st == ST_FETCH) L.st = ST_IDLE;
+            break;
+          }
         }
+        const uint32_t n = __popcll(need);
+        const uint32_t take = n < chunk_left ? n : chunk_left;
+        const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
+        if (L.st == ST_FETCH && rank < take) {
+          L.rng.init(K.first_photon + chunk_base + rank);
+          L.st = ST_EMIT;
+        }
+        chunk_base += take;
+        chunk_left -= take;
+        need = __ballot(L.st == ST_FETCH);
       }
       if (__ballot(L.st != ST_IDLE) == 0) break;
     }
@@ -118,261 +139,244 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K) {
     }
 
     // ---- EVAL phase: the SDF array at the lane's query point ----------------------------
+    const bool have = !L.seg && L.pend;
     EvalOut R;
     R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
-    if (!L.seg && L.pend) {
+    if (__ballot(have)) {  // wave-uniform: the SDF program stays on the scalar path
       const bool fres = (L.st == ST_F0 || L.st == ST_F1);
       const bool tap = (L.st >= ST_N1 && L.st <= ST_N4);
       const int32_t capi = fres ? L.new_layer : (tap ? L.Ls : 0);
       const int32_t capj = fres ? L.old_layer : 0;
-      R = eval_sdfs(K, eval_query(L), test_kernel && L.st == ST_LAYER, capi, capj);
+      R = eval_sdfs(nodes, prog, K.n_prog, eval_query(L), test_kernel && L.st == ST_LAYER, capi, capj);
       // packet%cnts counts the evaluations of tauint2's ds/dsNew arrays only (inttau2.f90:67,83,
       // 138,183,219,232): not the initial layer search, the Fresnel ds lookups or calcNormal.
-      if (L.st == ST_H0 || L.st == ST_H1 || L.st == ST_H3 || L.st == ST_M1 || L.st == ST_G0)
-        L.c_sdf += (uint32_t)K.n_top;
+      if (have) {
+        L.pend = false;
+        if (L.st == ST_H0 || L.st == ST_H1 || L.st == ST_H3 || L.st == ST_M1 || L.st == ST_G0)
+          L.c_sdf += (uint32_t)K.n_top;
+      }
     }
 
-    // ---- ADVANCE phase: reference control flow up to the next EVAL / deposit ------------
-    bool rec = false;
-    V3 rec_start = v3(0.0, 0.0, 0.0), rec_dir = rec_start;
-    double rec_sep = 0.0, rec_w = 0.0;
-    int32_t rec_layer = 0;
-    if (!L.seg && L.st != ST_IDLE && L.st != ST_FETCH) {
-      bool have = L.pend;
-      L.pend = false;
-      bool yield = false;
-      for (int guard = 0; guard < 64 && !yield; ++guard) {
-        switch (L.st) {
-          case ST_EMIT: {  // kernelsMod.f90:1937-1945
-            L.fault = false; L.status = 0; L.nscatt = 0; L.layer = 0; L.inter = 0;
-            L.xcell = L.ycell = L.zcell = 0;
-            emit(K, L);
-            if (!test_kernel) {
-              int64_t tries = 0;
-              while (cell_out(K, L)) {
-                if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
-                LCTR(LC_RETRIES)++;
-                emit(K, L);
-              }
-              if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, K.emission, L, 1.0);
-            }
-            if (L.fault) { L.st = ST_DONE; break; }
-            ARRIVE(ST_LAYER);
-            break;
-          }
-          case ST_LAYER:  // :1948-1952 (test_kernel: mask ds<=0, :2136)
-            have = false;
-            L.layer = R.maxloc;
-            if (L.layer == 0) { L.fault = true; L.st = ST_DONE; break; }
-            L.st = ST_T2;
-            break;
-          case ST_T2:  // tauint2 entry, inttau2.f90:48-60
-            L.startPos = L.pos;
-            sh->entry[0][threadIdx.x] = L.pos.x; sh->entry[1][threadIdx.x] = L.pos.y;
-            sh->entry[2][threadIdx.x] = L.pos.z; sh->entry[3][threadIdx.x] = L.dir.x;
-            sh->entry[4][threadIdx.x] = L.dir.y; sh->entry[5][threadIdx.x] = L.dir.z;
-            LCTR(LC_TAU)++;
-            L.tau = -det_log(L.rng.next(K.key0, K.key1));
-            L.taurun = 0.0;
-            L.hop = 0;
-            L.st = ST_H0;
-            break;
-          case ST_H0:  // hop loop head, :61-73
-            if (!have) {
-              if (!(L.taurun <= L.tau)) { L.st = ST_T2END; break; }
-              if (++L.hop > (uint32_t)MAX_HOP_ITERS) { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }
-              ARRIVE(ST_H0);
-              break;
-            }
-            have = false;
-            L.minabs = R.minabs; L.minv = R.minv;
-            L.d = R.minabs;
-            L.loopc = 0;  // march guard
-            if (L.d < eps) {  // on a surface: micro-step, :73-84
-              L.d = R.minabs + 2.0 * eps;
-              L.ssp = L.pos + smul(L.d, L.dir);
-              ARRIVE(ST_H1);
-              break;
-            }
-            L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;  // :149-152
-            break;
-          case ST_H1: {  // forward / backward micro-step, :86-123
-            have = false;
-            const double kap = K.props[L.layer - 1].kappa;
-            const V3 oldpos = L.pos;
-            const double t = L.d * kap;
-            if (R.maxloc == L.layer) {
-              if (L.taurun + t < L.tau) { L.pos = L.pos + smul(L.d, L.dir); L.taurun = L.taurun + t; }
-              else { L.d = (L.tau - L.taurun) / kap; L.taurun = L.taurun + t; }
-            } else {
-              if (L.taurun + t < L.tau) { L.pos = L.pos - smul(L.d, L.dir); L.taurun = L.taurun + t; }
-              else { L.d = (L.tau - L.taurun) / kap; L.pos = L.pos - smul(L.d, L.dir); }
-            }
-            L.st = ST_H2;
-            yield = start_segment(K, L, oldpos, L.d);
-            break;
-          }
-          case ST_H2:  // detectors, :125-131
-            rec = true; rec_start = L.startPos; rec_dir = L.dir; rec_sep = pointsep(L.pos, L.startPos);
-            rec_layer = L.layer; rec_w = L.weight;
-            L.startPos = L.pos;
-            ARRIVE(ST_H3);
-            break;
-          case ST_H3:  // :133-152
-            have = false;
-            L.minabs = R.minabs; L.minv = R.minv;
-            L.d = R.minabs;
-            if (R.minv > 0.0) L.tflag = true;
-            L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;
-            break;
-          case ST_M0: {  // march loop head, :155-176
-            if (!(L.d >= eps)) { L.st = ST_B0; break; }
-            if (++L.loopc > (uint32_t)MAX_MARCH_ITERS) { L.fault = true; L.tflag = true; L.st = ST_B0; break; }
-            const double kap = K.props[L.layer - 1].kappa;
-            const double t = L.d * kap;
-            const V3 oldpos = L.pos;
-            if (L.taurun + t < L.tau) {
-              L.taurun = L.taurun + t;
-              L.pos = L.pos + smul(L.d, L.dir);
-              start_segment(K, L, oldpos, L.d);
-              ARRIVE(ST_M1);
-            } else {
-              L.d = (L.tau - L.taurun) / kap;
-              L.taurun = L.tau;
-              L.pos = L.pos + smul(L.d, L.dir);
-              L.st = ST_B0;
-              yield = start_segment(K, L, oldpos, L.d);
-            }
-            break;
-          }
-          case ST_M1:  // :177-191
-            have = false;
-            L.minabs = R.minabs; L.minv = R.minv;
-            L.d = R.minabs;
-            if (R.minv > 0.0) { L.tflag = true; L.st = ST_B0; }
-            else L.st = ST_M0;
-            break;
-          case ST_B0:  // detectors and boundary probe, :195-221
-            rec = true; rec_start = L.startPos; rec_dir = L.dir; rec_sep = pointsep(L.pos, L.startPos);
-            rec_layer = L.layer; rec_w = L.weight;
-            L.startPos = L.pos;
-            if (L.taurun >= L.tau || L.tflag) { L.st = ST_T2END; break; }
-            L.d = L.minabs + 2.0 * eps;
+    // ---- P3: consume the EVAL result ----------------------------------------------------
+    if (have) {
+      switch (L.st) {
+        case ST_LAYER:  // kernelsMod.f90:1948-1952 (test_kernel: mask ds<=0, :2136)
+          L.layer = R.maxloc;
+          if (L.layer == 0) { L.fault = true; L.st = ST_DONE; }
+          else L.st = ST_T2;
+          break;
+        case ST_H0:  // inttau2.f90:63-84, 149-152
+          L.minabs = R.minabs; L.minv = R.minv;
+          L.d = R.minabs;
+          L.loopc = 0;  // march guard
+          if (L.d < eps) {  // on a surface: micro-step
+            L.d = R.minabs + 2.0 * eps;
             L.ssp = L.pos + smul(L.d, L.dir);
-            L.old_layer = L.layer;
-            L.loopc = 0;  // glancing guard
-            ARRIVE(ST_G0);
-            break;
-          case ST_G0: {  // new layer and the glancing loop, :220-245
-            have = false;
-            L.new_layer = R.maxloc;
-            if (L.new_layer == L.old_layer && R.minabs < eps) {
-              if (++L.loopc > (uint32_t)MAX_GLANCE_ITERS) { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }
-              L.d = L.d + eps;
-              L.ssp = L.pos + smul(L.d, L.dir);
-              ARRIVE(ST_G0);
-              break;
-            }
-            if (L.new_layer == 0) { L.tflag = true; L.st = ST_T2END; break; }
-            const double n1 = K.props[L.layer - 1].n, n2 = K.props[L.new_layer - 1].n;
-            if (n1 != n2) { ARRIVE(ST_F0); break; }
-            L.layer = L.new_layer;  // equal n: cross, :318-328
-            L.st = ST_X1;
-            yield = start_segment(K, L, L.pos, L.d);
+            L.st = ST_H1; L.pend = true;
+          } else {
+            L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;
+          }
+          break;
+        case ST_H1: {  // forward / backward micro-step, :86-123
+          const double kap = props[L.layer - 1].kappa;
+          const V3 oldpos = L.pos;
+          const double t = L.d * kap;
+          if (R.maxloc == L.layer) {
+            if (L.taurun + t < L.tau) { L.pos = L.pos + smul(L.d, L.dir); L.taurun = L.taurun + t; }
+            else { L.d = (L.tau - L.taurun) / kap; L.taurun = L.taurun + t; }
+          } else {
+            if (L.taurun + t < L.tau) { L.pos = L.pos - smul(L.d, L.dir); L.taurun = L.taurun + t; }
+            else { L.d = (L.tau - L.taurun) / kap; L.pos = L.pos - smul(L.d, L.dir); }
+          }
+          L.st = ST_H2;
+          start_segment(K, L, oldpos, L.d);
+          break;
+        }
+        case ST_H3:  // :133-152
+          L.minabs = R.minabs; L.minv = R.minv;
+          L.d = R.minabs;
+          if (R.minv > 0.0) L.tflag = true;
+          L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;
+          break;
+        case ST_M1:  // :177-191
+          L.minabs = R.minabs; L.minv = R.minv;
+          L.d = R.minabs;
+          if (R.minv > 0.0) { L.tflag = true; L.st = ST_B0; }
+          else L.st = ST_M0;
+          break;
+        case ST_G0: {  // new layer and the glancing loop, :220-245
+          L.new_layer = R.maxloc;
+          if (L.new_layer == L.old_layer && R.minabs < eps) {
+            if (++L.loopc > (uint32_t)MAX_GLANCE_ITERS) { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }
+            L.d = L.d + eps;
+            L.ssp = L.pos + smul(L.d, L.dir);
+            L.pend = true;  // evaluate G0 again
             break;
           }
-          case ST_X1:  // after the crossing deposit, :294-303 / :326-335
-            L.taurun = L.taurun + L.d * K.props[L.layer - 1].kappa;
-            L.pos = L.ssp;
-            rec = true; rec_start = L.startPos; rec_dir = L.dir; rec_sep = pointsep(L.pos, L.startPos);
-            rec_layer = L.layer; rec_w = L.weight;
+          if (L.new_layer == 0) { L.tflag = true; L.st = ST_T2END; break; }
+          const double n1 = props[L.layer - 1].n, n2 = props[L.new_layer - 1].n;
+          if (n1 != n2) { L.st = ST_F0; L.pend = true; break; }
+          L.layer = L.new_layer;  // equal n: cross, :318-328
+          L.st = ST_X1;
+          start_segment(K, L, L.pos, L.d);
+          break;
+        }
+        case ST_F0:  // ds(new), ds(old) at pos (kept in sd/slen: no segment is active)
+          L.sd = R.va; L.slen = R.vb;
+          L.st = ST_F1; L.pend = true;
+          break;
+        case ST_F1: {  // which SDF's normal, :250-277
+          const double ds_new = L.sd, ds_old = L.slen, dn_new = R.va, dn_old = R.vb;
+          if (dn_new < 0.0 && ds_new >= 0.0) L.Ls = L.new_layer;
+          else if (dn_old >= 0.0 && ds_old < 0.0) L.Ls = L.old_layer;
+          else if (dn_new < 0.0 && dn_old < 0.0) L.Ls = L.new_layer;
+          else if (ds_old >= 0.0 && dn_old >= 0.0) L.Ls = L.old_layer;
+          else { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }  // error stop :264-277
+          L.st = ST_N1; L.pend = true;
+          break;
+        }
+        case ST_N1: L.old.x = R.va; L.st = ST_N2; L.pend = true; break;  // calcNormal taps in old.xyz
+        case ST_N2: L.old.y = R.va; L.st = ST_N3; L.pend = true; break;
+        case ST_N3: L.old.z = R.va; L.st = ST_N4; L.pend = true; break;
+        case ST_N4: {  // calcNormal (sdf_base.f90:166-190) + reflect_refract (surfaces.f90:14-84)
+          const double e4 = R.va;
+          const V3 xyy = v3(1.0, -1.0, -1.0), yyx = v3(-1.0, -1.0, 1.0), yxy = v3(-1.0, 1.0, -1.0),
+                   xxx = v3(1.0, 1.0, 1.0);
+          const V3 nn = ((mul(xyy, L.old.x) + mul(yyx, L.old.y)) + mul(yxy, L.old.z)) + mul(xxx, e4);
+          const double ln = len(nn);
+          const V3 N = v3(nn.x / ln, nn.y / ln, nn.z / ln);
+          const double n1 = props[L.layer - 1].n, n2 = props[L.new_layer - 1].n;
+          LCTR(LC_FRES)++;
+          const double Rf = fresnel(L.dir, N, n1, n2);
+          if (L.rng.next(K.key0, K.key1) <= Rf) {  // reflect :42-55, :304-316
+            const double s2 = 2.0 * dot(N, L.dir);
+            L.dir = L.dir - smul(s2, N);
+            LCTR(LC_REFL)++;
             L.startPos = L.pos;
-            if (L.tflag) { L.st = ST_T2END; break; }
-            L.st = ST_H0;
-            break;
-          case ST_F0:  // ds(new), ds(old) at pos (kept in sd/slen: no segment is active)
-            have = false;
-            L.sd = R.va; L.slen = R.vb;
-            ARRIVE(ST_F1);
-            break;
-          case ST_F1: {  // which SDF's normal, :250-277
-            have = false;
-            const double ds_new = L.sd, ds_old = L.slen, dn_new = R.va, dn_old = R.vb;
-            if (dn_new < 0.0 && ds_new >= 0.0) L.Ls = L.new_layer;
-            else if (dn_old >= 0.0 && ds_old < 0.0) L.Ls = L.old_layer;
-            else if (dn_new < 0.0 && dn_old < 0.0) L.Ls = L.new_layer;
-            else if (ds_old >= 0.0 && dn_old >= 0.0) L.Ls = L.old_layer;
-            else { L.fault = true; L.tflag = true; L.st = ST_T2END; break; }  // error stop :264-277
-            ARRIVE(ST_N1);
-            break;
-          }
-          case ST_N1: have = false; L.old.x = R.va; ARRIVE(ST_N2); break;  // calcNormal taps in old.xyz
-          case ST_N2: have = false; L.old.y = R.va; ARRIVE(ST_N3); break;
-          case ST_N3: have = false; L.old.z = R.va; ARRIVE(ST_N4); break;
-          case ST_N4: {  // calcNormal (sdf_base.f90:166-190) + reflect_refract (surfaces.f90:14-84)
-            have = false;
-            const double e4 = R.va;
-            const V3 xyy = v3(1.0, -1.0, -1.0), yyx = v3(-1.0, -1.0, 1.0), yxy = v3(-1.0, 1.0, -1.0),
-                     xxx = v3(1.0, 1.0, 1.0);
-            const V3 nn = ((mul(xyy, L.old.x) + mul(yyx, L.old.y)) + mul(yxy, L.old.z)) + mul(xxx, e4);
-            const double ln = len(nn);
-            const V3 N = v3(nn.x / ln, nn.y / ln, nn.z / ln);
-            const double n1 = K.props[L.layer - 1].n, n2 = K.props[L.new_layer - 1].n;
-            LCTR(LC_FRES)++;
-            const double Rf = fresnel(L.dir, N, n1, n2);
-            if (L.rng.next(K.key0, K.key1) <= Rf) {  // reflect :42-55, :304-316
-              const double s2 = 2.0 * dot(N, L.dir);
-              L.dir = L.dir - smul(s2, N);
-              LCTR(LC_REFL)++;
-              L.startPos = L.pos;
-              L.bounces += 1;
-              if (L.bounces > 1000) {  // :313-315: return without write-back
-                LCTR(LC_BABORT)++;
-                L.pos = v3(sh->entry[0][threadIdx.x], sh->entry[1][threadIdx.x], sh->entry[2][threadIdx.x]);
-                L.dir = v3(sh->entry[3][threadIdx.x], sh->entry[4][threadIdx.x], sh->entry[5][threadIdx.x]);
-                L.st = ST_INTERACT;
-                break;
-              }
-              L.st = ST_H0;
-            } else {  // refract :57-84, transmit :284-303
-              const double eta = n1 / n2;
-              V3 Nt = N;
-              double c1 = dot(Nt, L.dir);
-              if (c1 < 0.0) c1 = -c1;
-              else Nt = smul(-1.0, N);
-              const double c2 = sqrt(1.0 - (eta * eta) * (1.0 - c1 * c1));
-              L.dir = smul(eta, L.dir) + smul(eta * c1 - c2, Nt);
-              L.layer = L.new_layer;
-              L.st = ST_X1;
-              yield = start_segment(K, L, L.pos, L.d);
+            L.bounces += 1;
+            if (L.bounces > 1000) {  // :313-315: return without write-back
+              LCTR(LC_BABORT)++;
+              L.pos = v3(sh->entry[0][threadIdx.x], sh->entry[1][threadIdx.x], sh->entry[2][threadIdx.x]);
+              L.dir = v3(sh->entry[3][threadIdx.x], sh->entry[4][threadIdx.x], sh->entry[5][threadIdx.x]);
+              L.st = ST_INTERACT;
+            } else {
+              L.st = ST_H0;  // arrives in P8
             }
-            break;
+          } else {  // refract :57-84, transmit :284-303
+            const double eta = n1 / n2;
+            V3 Nt = N;
+            double c1 = dot(Nt, L.dir);
+            if (c1 < 0.0) c1 = -c1;
+            else Nt = smul(-1.0, N);
+            const double c2 = sqrt(1.0 - (eta * eta) * (1.0 - c1 * c1));
+            L.dir = smul(eta, L.dir) + smul(eta * c1 - c2, Nt);
+            L.layer = L.new_layer;
+            L.st = ST_X1;
+            start_segment(K, L, L.pos, L.d);
           }
-          case ST_T2END:  // tauint2 write-back checks, :341-362
-            if (fabs(L.pos.x) > K.xmax) L.tflag = true;
-            if (fabs(L.pos.y) > K.ymax) L.tflag = true;
-            if (fabs(L.pos.z) > K.zmax) L.tflag = true;
-            L.st = ST_INTERACT;
-            break;
-          case ST_INTERACT: {  // kernelsMod.f90:1958-1975 / 2036-2065 / 2126-2170
-            if (L.tflag || L.fault) { L.st = ST_DONE; break; }
-            if (++L.inter > (uint32_t)MAX_INTERACTIONS) { L.fault = true; L.st = ST_DONE; break; }
+          break;
+        }
+        default:
+          break;
+      }
+    }
+
+    // ---- P4: a march step starts its deposit segment, :155-176 -------------------------
+    if (!L.seg && L.st == ST_M0) {
+      if (!(L.d >= eps)) {
+        L.st = ST_B0;
+      } else if (++L.loopc > (uint32_t)MAX_MARCH_ITERS) {
+        L.fault = true; L.tflag = true; L.st = ST_B0;
+      } else {
+        const double kap = props[L.layer - 1].kappa;
+        const double t = L.d * kap;
+        const V3 oldpos = L.pos;
+        if (L.taurun + t < L.tau) {
+          L.taurun = L.taurun + t;
+          L.pos = L.pos + smul(L.d, L.dir);
+          L.st = ST_M1; L.pend = true;
+        } else {
+          L.d = (L.tau - L.taurun) / kap;
+          L.taurun = L.tau;
+          L.pos = L.pos + smul(L.d, L.dir);
+          L.st = ST_B0;
+        }
+        start_segment(K, L, oldpos, L.d);
+      }
+    }
+
+    // ---- P5: after a deposit segment: detectors and the next program point -------------
+    bool rec = false;
+    V3 rec_start = v3(0.0, 0.0, 0.0);
+    double rec_sep = 0.0;
+    if (!L.seg && (L.st == ST_H2 || L.st == ST_B0 || L.st == ST_X1)) {
+      if (L.st == ST_X1) {  // :294-303 / :326-335
+        L.taurun = L.taurun + L.d * props[L.layer - 1].kappa;
+        L.pos = L.ssp;
+      }
+      rec = true; rec_start = L.startPos; rec_sep = pointsep(L.pos, L.startPos);  // :125-131, 195-201
+      L.startPos = L.pos;
+      if (L.st == ST_H2) {
+        L.st = ST_H3; L.pend = true;
+      } else if (L.st == ST_X1) {
+        L.st = L.tflag ? ST_T2END : ST_H0;
+      } else if (L.taurun >= L.tau || L.tflag) {  // B0, :204-207
+        L.st = ST_T2END;
+      } else {  // boundary probe, :213-222
+        L.d = L.minabs + 2.0 * eps;
+        L.ssp = L.pos + smul(L.d, L.dir);
+        L.old_layer = L.layer;
+        L.loopc = 0;  // glancing guard
+        L.st = ST_G0; L.pend = true;
+      }
+    }
+    if (K.n_dets && rec) LCTR(LC_HITS) += record_hits(K, dets, det_off, rec_start, L.dir, rec_sep, L.layer, L.weight);
+
+    // ---- P6: tauint2 write-back checks, :341-362 -----------------------------------------
+    if (!L.seg && L.st == ST_T2END) {
+      if (fabs(L.pos.x) > K.xmax) L.tflag = true;
+      if (fabs(L.pos.y) > K.ymax) L.tflag = true;
+      if (fabs(L.pos.z) > K.zmax) L.tflag = true;
+      L.st = ST_INTERACT;
+    }
+
+    // ---- P7: photon events (interaction, tauint2 entry, emission, completion) ----------
+    // These are the expensive, rare program points; a wave runs them together once enough
+    // lanes wait for one (or nothing else is left), instead of paying for them every trip.
+    {
+      const bool ev = (L.st == ST_INTERACT || L.st == ST_T2 || L.st == ST_EMIT || L.st == ST_DONE);
+      const uint64_t evm = __ballot(ev);
+      const uint64_t busy = __ballot(L.st != ST_IDLE && L.st != ST_FETCH);
+      const uint32_t nev = __popcll(evm);
+      if (nev && (nev >= SMCRT_EVENT_LANES || evm == busy)) {
+        if (L.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2036-2065 / 2126-2170
+          if (L.tflag || L.fault) {
+            L.st = ST_DONE;
+          } else if (++L.inter > (uint32_t)MAX_INTERACTIONS) {
+            L.fault = true; L.st = ST_DONE;
+          } else {
             const double ran = L.rng.next(K.key0, K.key1);
-            const TopProps pr = K.props[L.layer - 1];
+            const TopProps pr = props[L.layer - 1];
+            bool sc = false;
             if (survival) {
               const double w_abs = L.weight * (1.0 - pr.albedo);
               L.weight = L.weight - w_abs;
               add_cell(K, K.absorb, L, w_abs);
+              sc = true;
               if (L.weight < 0.01) {
                 if (ran < 0.1) L.weight = L.weight / 0.1;
-                else { L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++; L.st = ST_DONE; break; }
+                else { L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++; sc = false; }
               }
-              scatter(K, L, pr.hgg);
-              L.nscatt++; LCTR(LC_SCATTERS)++;
             } else if (ran < pr.albedo) {
+              sc = true;
+            } else {
+              L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++;
+              if (!test_kernel) add_cell(K, K.absorb, L, 1.0);  // recordWeight(packet, 1.0)
+            }
+            if (sc) {
               scatter(K, L, pr.hgg);
               L.nscatt++; LCTR(LC_SCATTERS)++;
-              if (test_kernel) {
+              if (test_kernel && !survival) {
                 const uint32_t st = L.nscatt;
                 if (st >= 1 && st <= 4) {
                   if (K.moments) {
@@ -388,45 +392,69 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K) {
                   L.status = 4;
                 }
               }
+              L.st = ST_T2;
             } else {
-              L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++;
-              if (!test_kernel) add_cell(K, K.absorb, L, 1.0);  // recordWeight(packet, 1.0)
               L.st = ST_DONE;
-              break;
             }
-            L.st = ST_T2;
-            break;
           }
-          case ST_DONE: {  // photon finished
-            if (L.fault) { L.status = 3; LCTR(LC_FAULTS)++; }
-            else if (L.status == 0) { L.status = 2; LCTR(LC_ESCAPED)++; }
-            LCTR(LC_PHOTONS)++;
-            LCTR(LC_DRAWS) += L.rng.draws;
-            if (rec_on) {
-              const uint64_t pid = ((uint64_t)L.rng.pid_hi << 32) | L.rng.pid_lo;
-              smcrt_photon_record* r = K.records + (pid - K.first_photon);
-              r->pos[0] = L.pos.x; r->pos[1] = L.pos.y; r->pos[2] = L.pos.z;
-              r->dir[0] = L.dir.x; r->dir[1] = L.dir.y; r->dir[2] = L.dir.z;
-              r->weight = L.weight;
-              r->cell[0] = L.xcell; r->cell[1] = L.ycell; r->cell[2] = L.zcell;
-              r->layer = L.layer;
-              r->nscatt = L.nscatt;
-              r->bounces = L.bounces;
-              r->draws = L.rng.draws;
-              r->status = L.status;
+        }
+        if (L.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
+          L.startPos = L.pos;
+          sh->entry[0][threadIdx.x] = L.pos.x; sh->entry[1][threadIdx.x] = L.pos.y;
+          sh->entry[2][threadIdx.x] = L.pos.z; sh->entry[3][threadIdx.x] = L.dir.x;
+          sh->entry[4][threadIdx.x] = L.dir.y; sh->entry[5][threadIdx.x] = L.dir.z;
+          LCTR(LC_TAU)++;
+          L.tau = -det_log(L.rng.next(K.key0, K.key1));
+          L.taurun = 0.0;
+          L.hop = 0;
+          L.st = ST_H0;  // arrives in P8
+        }
+        if (L.st == ST_EMIT) {  // kernelsMod.f90:1937-1945
+          L.fault = false; L.status = 0; L.nscatt = 0; L.layer = 0; L.inter = 0; L.bounces = 0;
+          L.xcell = L.ycell = L.zcell = 0;
+          emit(K, L);
+          if (!test_kernel) {
+            int64_t tries = 0;
+            while (cell_out(K, L)) {
+              if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
+              LCTR(LC_RETRIES)++;
+              emit(K, L);
             }
-            L.tflag = false; L.fault = false;
-            L.st = ST_FETCH;
-            yield = true;
-            break;
+            if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, K.emission, L, 1.0);
           }
-          default:
-            yield = true;
-            break;
+          if (L.fault) L.st = ST_DONE;
+          else { L.st = ST_LAYER; L.pend = true; }
+        }
+        if (L.st == ST_DONE) {  // photon finished
+          if (L.fault) { L.status = 3; LCTR(LC_FAULTS)++; }
+          else if (L.status == 0) { L.status = 2; LCTR(LC_ESCAPED)++; }
+          LCTR(LC_PHOTONS)++;
+          LCTR(LC_DRAWS) += L.rng.draws;
+          if (rec_on) {
+            const uint64_t pid = ((uint64_t)L.rng.pid_hi << 32) | L.rng.pid_lo;
+            smcrt_photon_record* r = K.records + (pid - K.first_photon);
+            r->pos[0] = L.pos.x; r->pos[1] = L.pos.y; r->pos[2] = L.pos.z;
+            r->dir[0] = L.dir.x; r->dir[1] = L.dir.y; r->dir[2] = L.dir.z;
+            r->weight = L.weight;
+            r->cell[0] = L.xcell; r->cell[1] = L.ycell; r->cell[2] = L.zcell;
+            r->layer = L.layer;
+            r->nscatt = L.nscatt;
+            r->bounces = L.bounces;
+            r->draws = L.rng.draws;
+            r->status = L.status;
+          }
+          L.tflag = false; L.fault = false;
+          L.st = ST_FETCH;
         }
       }
     }
-    if (K.n_dets && rec) LCTR(LC_HITS) += record_hits(K, rec_start, rec_dir, rec_sep, rec_layer, rec_w);
+
+    // ---- P8: arrive at the hop-loop head, :61 ---------------------------------------------
+    if (!L.seg && L.st == ST_H0 && !L.pend) {
+      if (!(L.taurun <= L.tau)) L.st = ST_T2END;
+      else if (++L.hop > (uint32_t)MAX_HOP_ITERS) { L.fault = true; L.tflag = true; L.st = ST_T2END; }
+      else L.pend = true;
+    }
   }
 
   // ---- per-wave counter reduction ------------------------------------------------------
@@ -661,8 +689,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
   int per_cu = 0, cus = 0;
-  s->face_bytes = faces.size() * sizeof(double);
-  s->lds_faces = s->face_bytes <= 32768;  // stage the voxel faces in LDS when they fit
+  s->face_bytes = faces.size() * sizeof(double) + sizeof(TopProps) * (size_t)n_top;
+  s->lds_faces = s->face_bytes <= 40960;  // stage props + voxel faces in LDS when they fit
   hipError_t oe = s->lds_faces
       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel<true>, 256, s->face_bytes)
       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel<false>, 256, 0);
@@ -727,9 +755,11 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
   const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
   if (s->lds_faces)
-    hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K);
+    hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K, K.nodes, K.prog,
+                       K.dets, K.det_off);
   else
-    hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K);
+    hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K, K.nodes, K.prog, K.dets,
+                       K.det_off);
   HIPCHK(hipGetLastError());
   return SMCRT_OK;
 }

@@ -38,6 +38,14 @@ constexpr int64_t MAX_INTERACTIONS = 100000000;
 #ifndef SMCRT_DDA_PER_ITER
 #define SMCRT_DDA_PER_ITER 2
 #endif
+// A wave runs the photon-event phase once this many lanes wait for it (or no lane has
+// anything else to do).
+#ifndef SMCRT_FETCH_CHUNK
+#define SMCRT_FETCH_CHUNK 64
+#endif
+#ifndef SMCRT_EVENT_LANES
+#define SMCRT_EVENT_LANES 16
+#endif
 
 // Optical properties of a top-level SDF, derived as init_mono does
 // (opticalProperties.f90:107-125).
@@ -125,15 +133,16 @@ __device__ __forceinline__ int64_t f_int(double x) {
 
 // record_hit on every detector for one path segment (detector_base.f90:137-235,
 // detectors.f90:147-469). Returns the number of bin increments.
-__device__ __forceinline__ uint32_t record_hits(const KParams& K, V3 start, V3 dir, double pointSep, int32_t layer,
-                                                double weight) {
+__device__ __forceinline__ uint32_t record_hits(const KParams& K, const smcrt_detector* __restrict__ dets,
+                                                const int64_t* __restrict__ det_off, V3 start, V3 dir,
+                                                double pointSep, int32_t layer, double weight) {
   uint32_t hits = 0;
   double value1D = (double)layer;  // hit_t%value1D <- packet%layer
   for (int32_t di = 0; di < K.n_dets; ++di) {
-    const smcrt_detector* D = K.dets + di;
+    const smcrt_detector* D = dets + di;
     const V3 dpos = v3(D->pos[0], D->pos[1], D->pos[2]);
     const V3 ddir = v3(D->dir[0], D->dir[1], D->dir[2]);
-    double* data = K.det_bins ? K.det_bins + K.det_off[di] : nullptr;
+    double* data = K.det_bins ? K.det_bins + det_off[di] : nullptr;
     double t;
     int64_t bin = -1;
     double w = weight;
@@ -413,38 +422,41 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
       if (last) { dcell = L.slen - L.sd; L.sd = L.slen; }
       else L.sd = L.sd + dcell;
       L.c_dep++;
+#if defined(SMCRT_DIAG_NO_ATOMIC)
+      if (K.jmean && dcell == -1.0) atomic_add_nr(K.jmean, dcell);  // diagnostic: keep the value live
+#elif defined(SMCRT_DIAG_SCATTER_ATOMIC)
+      if (K.jmean) {  // diagnostic: same atomics, addresses hashed over the grid (no hot voxels)
+        uint32_t h = (uint32_t)lin(K, L.ci, L.cj, L.ck) * 2654435761u;
+        h ^= h >> 15;
+        atomic_add_nr(K.jmean + (h % (uint32_t)(K.nx * K.ny * K.nz)), (double)(float)dcell * L.weight);
+      }
+#else
       if (K.jmean) atomic_add_nr(K.jmean + lin(K, L.ci, L.cj, L.ck), (double)(float)dcell * L.weight);
+#endif
       if (last) {  // update_pos(.false.)
         L.old.x = L.old.x + dir.x * dcell;
         L.old.y = L.old.y + dir.y * dcell;
         L.old.z = L.old.z + dir.z * dcell;
         done = true;
-      } else {  // update_pos(.true.), :538-582
+      } else if (!(lx || ly || lz)) {  // error stop :570-573
+        L.fault = true; L.tflag = true; done = true;
+      } else {
+        // update_pos(.true.), :538-582: the first axis with ldir set is snapped to its wall
+        // +- delta (unchanged if its direction is 0), the other two advance by dcell. Written
+        // as selects over the same expressions, so `old` stays in registers.
         const double delta = 1e-8;  // local delta, :393
-        if (lx) {
-          if (dir.x > 0.0) L.old.x = xf[L.ci] + delta;
-          else if (dir.x < 0.0) L.old.x = xf[L.ci - 1] - delta;
-          L.old.y = L.old.y + dir.y * dcell;
-          L.old.z = L.old.z + dir.z * dcell;
-        } else if (ly) {
-          if (dir.y > 0.0) L.old.y = yf[L.cj] + delta;
-          else if (dir.y < 0.0) L.old.y = yf[L.cj - 1] - delta;
-          L.old.x = L.old.x + dir.x * dcell;
-          L.old.z = L.old.z + dir.z * dcell;
-        } else if (lz) {
-          if (dir.z > 0.0) L.old.z = zf[L.ck] + delta;
-          else if (dir.z < 0.0) L.old.z = zf[L.ck - 1] - delta;
-          L.old.x = L.old.x + dir.x * dcell;
-          L.old.y = L.old.y + dir.y * dcell;
-        } else {
-          L.fault = true; L.tflag = true; done = true;
-        }
-        if (!done) {
-          L.ci = cell_of(L.old.x, K.nx, K.xmax, K.inv2x);
-          L.cj = cell_of(L.old.y, K.ny, K.ymax, K.inv2y);
-          L.ck = cell_of(L.old.z, K.nz, K.zmax, K.inv2z);
-          if (L.ci == -1 || L.cj == -1 || L.ck == -1) { L.tflag = true; done = true; }
-        }
+        const double ax = L.old.x + dir.x * dcell, ay = L.old.y + dir.y * dcell, az = L.old.z + dir.z * dcell;
+        const double sx = dir.x > 0.0 ? xf[L.ci] + delta : (dir.x < 0.0 ? xf[L.ci - 1] - delta : L.old.x);
+        const double sy = dir.y > 0.0 ? yf[L.cj] + delta : (dir.y < 0.0 ? yf[L.cj - 1] - delta : L.old.y);
+        const double sz = dir.z > 0.0 ? zf[L.ck] + delta : (dir.z < 0.0 ? zf[L.ck - 1] - delta : L.old.z);
+        const bool snx = lx, sny = !lx && ly, snz = !lx && !ly;
+        L.old.x = snx ? sx : ax;
+        L.old.y = sny ? sy : ay;
+        L.old.z = snz ? sz : az;
+        L.ci = cell_of(L.old.x, K.nx, K.xmax, K.inv2x);
+        L.cj = cell_of(L.old.y, K.ny, K.ymax, K.inv2y);
+        L.ck = cell_of(L.old.z, K.nz, K.zmax, K.inv2z);
+        if (L.ci == -1 || L.cj == -1 || L.ck == -1) { L.tflag = true; done = true; }
       }
     }
   }
@@ -461,7 +473,11 @@ struct EvalOut {
   int32_t maxloc;
 };
 
-__device__ __forceinline__ EvalOut eval_sdfs(const KParams& K, V3 q, bool mask_le, int32_t capi, int32_t capj) {
+// `nodes` and `prog` must come from `const __restrict__` kernel parameters: that is what lets
+// the compiler prove them unclobbered and keep the wave-uniform loads on the scalar path.
+__device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ nodes,
+                                             const ProgOp* __restrict__ prog, int32_t n_prog, V3 q,
+                                             bool mask_le, int32_t capi, int32_t capj) {
   EvalOut r;
   r.minabs = __builtin_inf();
   r.minv = __builtin_inf();
@@ -469,9 +485,11 @@ __device__ __forceinline__ EvalOut eval_sdfs(const KParams& K, V3 q, bool mask_l
   r.maxloc = 0;
   double best = -__builtin_inf();
   double acc = 0.0;
-  for (int32_t ip = 0; ip < K.n_prog; ++ip) {
-    const ProgOp op = K.prog[ip];
-    const double v = sdf_prim(K.nodes + op.node, q);
+  for (int32_t ip = 0; ip < n_prog; ++ip) {
+    const ProgOp op = prog[ip];
+    // the program is wave-uniform: keep node parameters on the scalar path
+    const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
+    const double v = sdf_prim(nodes + node, q);
     if (op.action == PROG_TOP) acc = v;
     else if (op.action == PROG_CHILD_FIRST) acc = v;
     else acc = csg(op.op, acc, v, op.k);

@@ -18,7 +18,7 @@ from . import abi
 from .scene import detector_array
 from .tallies import Result
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsmcrt.so")
+LIB_PATH = os.environ.get("SMCRT_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsmcrt.so")
 _lock = threading.Lock()
 _lib = None
 

@@ -1,0 +1,21 @@
+#!/bin/bash
+# rocprofv3 passes over a short bench run: kernel trace + stats, then PMC counters in
+# separate passes (never combined with runtime/sys tracing). Output under gpurun_out/prof.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof
+mkdir -p $OUT
+ARGS=${PROF_ARGS:-"--no-cpu --steps 3 --warmup 1"}
+fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS \
+    > $OUT/$name.log 2>&1
+  local rc=$?; echo "$name rc=$rc"; if fatal $rc; then exit $rc; fi
+}
+run trace --kernel-trace --stats
+run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE
+run pmc_fetch --pmc FETCH_SIZE
+run pmc_write --pmc WRITE_SIZE
+run pmc_tcc --pmc TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum
+find $OUT -name "*.csv" | head -50
