@@ -1,0 +1,220 @@
+// deposit.h — binned path-length deposition into jmean.
+//
+// The reference adds every voxel crossing straight into jmean with `!$omp atomic`
+// (inttau2.f90:426-434). On MI355X a scattered device-scope atomic is a 64-B request at the
+// memory side: ~22 G/s for the whole chip whatever its scope, type or locality (measured,
+// profiles/r01_atomic_microbench.txt), and a wave cannot overlap them with its own
+// compute. So the transport kernel instead appends 8-byte deposit records
+// (voxel << 32 | f32 value) with wave-compacted stores into 128-KiB chunks of a record
+// pool, and four small kernels fold them in:
+//   bin_hist     records -> per-tile counts (tile = TILE_VOXELS consecutive voxels)
+//   bin_scan     counts  -> tile offsets and the list of reduce pieces
+//   bin_scatter  records -> tile-sorted order (one returning atomic per tile per chunk)
+//   bin_reduce   one piece of one tile per block: fp64 LDS accumulation, then the
+//                tile's non-zero sums are added to the fp64 jmean
+// Every record is read three times and written twice (40 B of HBM traffic per deposit,
+// streamed and coalesced) instead of one scattered atomic.
+// The value of a record is real(dcell,sp)*weight rounded to fp32, which is exact for the
+// reference's unit-weight packets (noBiasPropagation); survival-bias runs use the atomic
+// path so their fp64 weights are kept.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace smcrt {
+
+constexpr uint32_t CHUNK_RECORDS = 16384;  // 128 KiB per chunk
+constexpr uint32_t TILE_SHIFT = 13;        // 8192 voxels per tile: 64 KiB of fp64 in LDS
+constexpr uint32_t TILE_VOXELS = 1u << TILE_SHIFT;
+constexpr uint32_t MAX_TILES = 8192;       // grids up to 2^26 voxels use the binned path
+constexpr uint32_t PIECE_RECORDS = 1u << 18;
+
+struct Piece {
+  uint32_t tile, start, count, pad;
+};
+
+// Wave-uniform record-log cursor. Lives in scalar registers: it is only touched in
+// wave-uniform control flow.
+struct RecLog {
+  uint32_t chunk;  // current chunk index (n_chunks: none yet / exhausted)
+  uint32_t fill;   // records written into it
+};
+
+// Append one deposit per lane with dep == true. Must be called in wave-uniform control
+// flow (every lane of the wave reaches it).
+constexpr uint32_t LOG_NONE = 0xFFFFFFFFu;       // no chunk taken yet
+constexpr uint32_t LOG_EXHAUSTED = 0xFFFFFFFEu;  // pool full: deposits fall back to atomics
+
+__device__ __forceinline__ unsigned long long pack_record(uint32_t vox, double val) {
+  return ((unsigned long long)vox << 32) | (unsigned long long)__float_as_uint((float)val);
+}
+
+__device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool dep, uint32_t vox, double val,
+                                              uint32_t& overflow) {
+  const uint64_t m = __ballot(dep);
+  if (!m) return;
+  const uint32_t n = __popcll(m);
+  const int lane = threadIdx.x & 63;
+  const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+  uint32_t before = 0;  // lanes that still fit in the current chunk
+  if (W.chunk < K.n_chunks) before = (CHUNK_RECORDS - W.fill) < n ? (CHUNK_RECORDS - W.fill) : n;
+  if (dep && rank < before) K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + W.fill + rank] = pack_record(vox, val);
+  W.fill += before;
+  if (before < n) {  // chunk full or none yet: retire it, take the next one
+    const uint32_t rest = n - before;
+    if (W.chunk != LOG_EXHAUSTED) {
+      if (W.chunk < K.n_chunks && lane == 0) K.chunk_fill[W.chunk] = W.fill;
+      uint32_t c = 0;
+      if (lane == 0) c = atomicAdd(K.dep_ctl, 1u);
+      c = __shfl(c, 0, 64);
+      W.chunk = c < K.n_chunks ? c : LOG_EXHAUSTED;
+      W.fill = 0;
+    }
+    if (W.chunk < K.n_chunks) {  // rest <= 64 < CHUNK_RECORDS
+      if (dep && rank >= before)
+        K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + (rank - before)] = pack_record(vox, val);
+      W.fill = rest;
+    } else {  // pool exhausted: stay correct with fp64 atomics
+      if (dep && rank >= before) atomic_add_nr(K.jmean + vox, val);
+      overflow += rest;
+    }
+  }
+}
+
+__device__ __forceinline__ void close_log(const KParams& K, RecLog& W, uint32_t overflow) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) {
+    if (W.chunk < K.n_chunks) K.chunk_fill[W.chunk] = W.fill;
+    if (overflow) atomicAdd(K.dep_ctl + 1, overflow);
+  }
+}
+
+// ---- bin_hist: per-tile record counts -------------------------------------------------
+__global__ __launch_bounds__(1024) void bin_hist(const unsigned long long* __restrict__ pool,
+                                                 const uint32_t* __restrict__ chunk_fill,
+                                                 const uint32_t* __restrict__ dep_ctl, uint32_t n_chunks,
+                                                 uint32_t n_tiles, uint32_t* __restrict__ tile_count) {
+  __shared__ uint32_t hist[MAX_TILES];
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) hist[t] = 0;
+  __syncthreads();
+  const uint32_t used = dep_ctl[0] < n_chunks ? dep_ctl[0] : n_chunks;
+  for (uint32_t c = blockIdx.x; c < used; c += gridDim.x) {
+    const uint32_t fill = chunk_fill[c];
+    const unsigned long long* r = pool + (uint64_t)c * CHUNK_RECORDS;
+    for (uint32_t i = threadIdx.x; i < fill; i += blockDim.x)
+      atomicAdd(&hist[(uint32_t)(r[i] >> 32) >> TILE_SHIFT], 1u);
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x)
+    if (hist[t]) atomicAdd(tile_count + t, hist[t]);
+}
+
+// ---- bin_scan: tile offsets and reduce pieces (one block) ----------------------------------
+__global__ __launch_bounds__(1024) void bin_scan(const uint32_t* __restrict__ tile_count, uint32_t n_tiles,
+                                                 uint32_t* __restrict__ tile_cursor, Piece* __restrict__ pieces,
+                                                 uint32_t* __restrict__ dep_ctl) {
+  __shared__ uint32_t part[1024][2];
+  const uint32_t per = (n_tiles + blockDim.x - 1) / blockDim.x;
+  const uint32_t t0 = threadIdx.x * per, t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
+  uint32_t s = 0, np = 0;
+  for (uint32_t t = t0; t < t1; ++t) {
+    s += tile_count[t];
+    np += (tile_count[t] + PIECE_RECORDS - 1) / PIECE_RECORDS;
+  }
+  part[threadIdx.x][0] = s;
+  part[threadIdx.x][1] = np;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // n_tiles <= 8192: a serial scan over 1024 partials is short
+    uint32_t a = 0, b = 0;
+    for (uint32_t i = 0; i < blockDim.x; ++i) {
+      const uint32_t x = part[i][0], y = part[i][1];
+      part[i][0] = a; part[i][1] = b;
+      a += x; b += y;
+    }
+    dep_ctl[2] = b;  // number of pieces
+    dep_ctl[3] = a;  // number of records
+  }
+  __syncthreads();
+  uint32_t off = part[threadIdx.x][0], pc = part[threadIdx.x][1];
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t c = tile_count[t];
+    tile_cursor[t] = off;
+    for (uint32_t k = 0; k < c; k += PIECE_RECORDS) {
+      Piece p;
+      p.tile = t; p.start = off + k; p.count = (c - k) < PIECE_RECORDS ? (c - k) : PIECE_RECORDS; p.pad = 0;
+      pieces[pc++] = p;
+    }
+    off += c;
+  }
+}
+
+// ---- bin_scatter: records into tile order ----------------------------------------------
+constexpr int SCATTER_THREADS = 1024;
+constexpr int SCATTER_PER_THREAD = CHUNK_RECORDS / SCATTER_THREADS;  // 16
+
+__global__ __launch_bounds__(SCATTER_THREADS) void bin_scatter(const unsigned long long* __restrict__ pool,
+                                                               const uint32_t* __restrict__ chunk_fill,
+                                                               const uint32_t* __restrict__ dep_ctl,
+                                                               uint32_t n_chunks, uint32_t n_tiles,
+                                                               uint32_t* __restrict__ tile_cursor,
+                                                               unsigned long long* __restrict__ sorted) {
+  __shared__ uint32_t cnt[MAX_TILES];
+  __shared__ uint32_t base[MAX_TILES];
+  const uint32_t used = dep_ctl[0] < n_chunks ? dep_ctl[0] : n_chunks;
+  for (uint32_t c = blockIdx.x; c < used; c += gridDim.x) {
+    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) cnt[t] = 0;
+    __syncthreads();
+    const uint32_t fill = chunk_fill[c];
+    const unsigned long long* r = pool + (uint64_t)c * CHUNK_RECORDS;
+    unsigned long long v[SCATTER_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < SCATTER_PER_THREAD; ++k) {
+      const uint32_t i = threadIdx.x + k * SCATTER_THREADS;
+      v[k] = i < fill ? r[i] : ~0ull;
+      if (i < fill) atomicAdd(&cnt[(uint32_t)(v[k] >> 32) >> TILE_SHIFT], 1u);
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
+      const uint32_t n = cnt[t];
+      if (n) base[t] = atomicAdd(tile_cursor + t, n);
+      cnt[t] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SCATTER_PER_THREAD; ++k) {
+      if (v[k] != ~0ull) {
+        const uint32_t t = (uint32_t)(v[k] >> 32) >> TILE_SHIFT;
+        sorted[base[t] + atomicAdd(&cnt[t], 1u)] = v[k];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---- bin_reduce: one tile piece per block, fp64 LDS sums added into jmean ----------------
+__global__ __launch_bounds__(1024) void bin_reduce(const unsigned long long* __restrict__ sorted,
+                                                   const Piece* __restrict__ pieces,
+                                                   const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
+                                                   double* __restrict__ jmean) {
+  __shared__ double acc[TILE_VOXELS];
+  const uint32_t n_pieces = dep_ctl[2];
+  for (uint32_t pi = blockIdx.x; pi < n_pieces; pi += gridDim.x) {
+    const Piece p = pieces[pi];
+    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    const unsigned long long* r = sorted + p.start;
+    for (uint32_t i = threadIdx.x; i < p.count; i += blockDim.x) {
+      const unsigned long long x = r[i];
+      atomicAdd(&acc[(uint32_t)(x >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x));
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)p.tile << TILE_SHIFT;
+    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) {
+      const double a = acc[i];
+      if (a != 0.0 && base + i < n_voxels) atomic_add_nr(jmean + base + i, a);
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace smcrt

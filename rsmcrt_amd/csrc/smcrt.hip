@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -18,6 +19,7 @@
 
 #include "../../include/smcrt.h"
 #include "transport.h"
+#include "deposit.h"
 
 using namespace smcrt;
 
@@ -92,6 +94,10 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   L.bounces = L.nscatt = L.status = L.hop = L.loopc = L.inter = L.dda_it = 0;
   L.sd = L.slen = 0.0; L.ci = L.cj = L.ck = 0;
   L.rng.init(0);
+  const bool binned = K.rec_pool != nullptr && K.jmean != nullptr;
+  RecLog W;
+  W.chunk = LOG_NONE; W.fill = 0;
+  uint32_t overflow = 0;
   uint64_t chunk_base = 0;  // wave-uniform photon chunk
   uint32_t chunk_left = 0;
 
@@ -131,10 +137,16 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     }
 
     // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
-    if (L.seg) {
+    if (__ballot(L.seg)) {  // wave-uniform, so deposit records can be wave-compacted
 #pragma unroll
       for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {
-        if (L.seg) dda_step(K, L, xf, yf, zf);
+        bool dep = false;
+        uint32_t vox = 0;
+        double val = 0.0;
+        if (L.seg) dda_step(K, L, xf, yf, zf, dep, vox, val);
+        if (dep) L.c_dep++;
+        if (binned) emit_deposits(K, W, dep, vox, val, overflow);
+        else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
       }
     }
 
@@ -457,6 +469,8 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     }
   }
 
+  if (binned) close_log(K, W, overflow);
+
   // ---- per-wave counter reduction ------------------------------------------------------
   if (K.counters) {
     uint32_t c[SMCRT_NCOUNTERS];
@@ -545,6 +559,21 @@ struct smcrt_scene {
   int grid_blocks = 0;
   bool lds_faces = false;
   size_t face_bytes = 0;
+  // binned jmean deposition (deposit.h)
+  uint32_t n_tiles = 0;
+  unsigned long long* d_pool = nullptr;    // record log, cap records
+  unsigned long long* d_sorted = nullptr;  // tile-sorted records
+  uint32_t* d_chunk_fill = nullptr;
+  uint32_t* d_dep_ctl = nullptr;      // [0] chunks taken [1] overflow [2] pieces [3] records
+  uint32_t* d_tile_count = nullptr;   // n_tiles
+  uint32_t* d_tile_cursor = nullptr;  // n_tiles
+  Piece* d_pieces = nullptr;
+  uint64_t pool_chunks = 0, max_pieces = 0;
+  double rpp_est = 1024.0;           // deposit records per photon, refined from past launches
+  uint32_t* h_ctl = nullptr;         // pinned copy of dep_ctl of the last launch
+  hipEvent_t ctl_ev = nullptr;
+  bool ctl_pending = false;
+  bool force_atomic = false;  // SMCRT_DEPOSIT=atomic
   std::mutex mu;
 };
 
@@ -578,7 +607,11 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off,
-                  s->d_queue, s->d_grids, s->d_small, s->d_counters, s->d_records};
+                  s->d_queue, s->d_grids, s->d_small, s->d_counters, s->d_records,
+                  s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_dep_ctl, s->d_tile_count,
+                  s->d_tile_cursor, s->d_pieces};
+  if (s->ctl_ev) (void)hipEventDestroy(s->ctl_ev);
+  if (s->h_ctl) (void)hipHostFree(s->h_ctl);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -688,6 +721,22 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     e = hipMemcpy(s->d_det_off, s->h_det_off.data(), sizeof(int64_t) * (n_dets + 1), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
+  {  // binned deposition state (deposit.h)
+    const uint64_t nv = (uint64_t)grid->nx * grid->ny * grid->nz;
+    const uint64_t tiles = (nv + TILE_VOXELS - 1) / TILE_VOXELS;
+    s->n_tiles = (tiles <= MAX_TILES && nv < 0xFFFFFFFFull) ? (uint32_t)tiles : 0;
+    const char* fa = std::getenv("SMCRT_DEPOSIT");
+    s->force_atomic = fa && std::string(fa) == "atomic";
+    if (s->n_tiles) {
+      if ((st = dalloc(&s->d_dep_ctl, 4)) || (st = dalloc(&s->d_tile_count, s->n_tiles)) ||
+          (st = dalloc(&s->d_tile_cursor, s->n_tiles)))
+        return cleanup_fail(st);
+      if (hipHostMalloc((void**)&s->h_ctl, 8 * sizeof(uint32_t)) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ctl_ev, hipEventDisableTiming) != hipSuccess)
+        return cleanup_fail(fail(SMCRT_ERR_HIP, "pinned/event allocation failed"));
+      std::memset(s->h_ctl, 0, 8 * sizeof(uint32_t));
+    }
+  }
   int per_cu = 0, cus = 0;
   s->face_bytes = faces.size() * sizeof(double) + sizeof(TopProps) * (size_t)n_top;
   s->lds_faces = s->face_bytes <= 40960;  // stage props + voxel faces in LDS when they fit
@@ -719,6 +768,74 @@ int smcrt_scene_set_optprops(smcrt_scene* s, int32_t i, double mus, double mua, 
   return SMCRT_OK;
 }
 
+// Records the record pool must hold for one launch of n photons.
+static uint64_t pool_records_for(const smcrt_scene* s, uint64_t n) {
+  const double want = (double)n * s->rpp_est * 1.25 + (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
+  return (uint64_t)std::min(want, 2147483648.0);
+}
+
+// Make sure the record pool holds `records` (grow only). Returns false if it cannot.
+static bool ensure_pool(smcrt_scene* s, uint64_t records) {
+  const uint64_t chunks = (records + CHUNK_RECORDS - 1) / CHUNK_RECORDS;
+  if (chunks <= s->pool_chunks) return true;
+  const void* old[] = {s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_pieces};
+  for (const void* p : old)
+    if (p) (void)hipFree((void*)p);
+  s->d_pool = s->d_sorted = nullptr; s->d_chunk_fill = nullptr; s->d_pieces = nullptr; s->pool_chunks = 0;
+  const uint64_t cap = chunks * CHUNK_RECORDS;
+  const uint64_t pieces = cap / PIECE_RECORDS + s->n_tiles + 1;
+  if (hipMalloc((void**)&s->d_pool, cap * 8) != hipSuccess || hipMalloc((void**)&s->d_sorted, cap * 8) != hipSuccess ||
+      hipMalloc((void**)&s->d_chunk_fill, chunks * 4) != hipSuccess ||
+      hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) != hipSuccess) {
+    (void)hipGetLastError();
+    const void* bad[] = {s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_pieces};
+    for (const void* p : bad)
+      if (p) (void)hipFree((void*)p);
+    s->d_pool = s->d_sorted = nullptr; s->d_chunk_fill = nullptr; s->d_pieces = nullptr;
+    return false;
+  }
+  s->pool_chunks = chunks;
+  s->max_pieces = pieces;
+  return true;
+}
+
+static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
+  HIPCHK(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), stream));
+  const bool binned = K.rec_pool != nullptr;
+  if (binned) {
+    HIPCHK(hipMemsetAsync(s->d_dep_ctl, 0, 4 * sizeof(uint32_t), stream));
+    HIPCHK(hipMemsetAsync(s->d_tile_count, 0, s->n_tiles * sizeof(uint32_t), stream));
+  }
+  const uint64_t waves_needed = (K.n_photons + 63) / 64;
+  const uint64_t blocks_needed = (waves_needed + 3) / 4;
+  const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
+  if (s->lds_faces)
+    hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K, K.nodes, K.prog,
+                       K.dets, K.det_off);
+  else
+    hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K, K.nodes, K.prog, K.dets,
+                       K.det_off);
+  HIPCHK(hipGetLastError());
+  if (binned) {
+    const uint32_t nch = (uint32_t)s->pool_chunks;
+    const uint64_t nv = (uint64_t)s->grid.nx * s->grid.ny * s->grid.nz;
+    hipLaunchKernelGGL(bin_hist, dim3(1024), dim3(1024), 0, stream, s->d_pool, s->d_chunk_fill, s->d_dep_ctl, nch,
+                       s->n_tiles, s->d_tile_count);
+    hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, stream, s->d_tile_count, s->n_tiles, s->d_tile_cursor,
+                       s->d_pieces, s->d_dep_ctl);
+    hipLaunchKernelGGL(bin_scatter, dim3(1024), dim3(SCATTER_THREADS), 0, stream, s->d_pool, s->d_chunk_fill,
+                       s->d_dep_ctl, nch, s->n_tiles, s->d_tile_cursor, s->d_sorted);
+    hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, stream, s->d_sorted, s->d_pieces, s->d_dep_ctl, nv,
+                       K.jmean);
+    HIPCHK(hipGetLastError());
+    // remember how many records this launch produced (read back lazily, never waited for)
+    HIPCHK(hipMemcpyAsync(s->h_ctl, s->d_dep_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipEventRecord(s->ctl_ev, stream));
+    s->ctl_pending = true;
+  }
+  return SMCRT_OK;
+}
+
 static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg,
                   const smcrt_device_tallies& dt, hipStream_t stream) {
   if (src->kind < SMCRT_SRC_POINT || src->kind > SMCRT_SRC_PENCIL) return fail(SMCRT_ERR_INVALID_ARG, "bad source kind");
@@ -740,27 +857,53 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.xmax = s->grid.xmax; K.ymax = s->grid.ymax; K.zmax = s->grid.zmax;
   K.flags = cfg->flags;
   K.src = *src;
-  K.n_photons = cfg->n_photons;
-  K.first_photon = cfg->first_photon;
   K.seed = cfg->seed;
   K.key0 = (uint32_t)cfg->seed;
   K.key1 = (uint32_t)(cfg->seed >> 32);
   K.jmean = dt.jmean; K.absorb = dt.absorb; K.emission = dt.emission;
   K.det_bins = dt.det_bins; K.nscatt = dt.nscatt; K.moments = dt.moments;
   K.counters = (unsigned long long*)dt.counters;
-  K.records = dt.records;
   K.queue = s->d_queue;
-  HIPCHK(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), stream));
-  const uint64_t waves_needed = (cfg->n_photons + 63) / 64;
-  const uint64_t blocks_needed = (waves_needed + 3) / 4;
-  const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
-  if (s->lds_faces)
-    hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K, K.nodes, K.prog,
-                       K.dets, K.det_off);
-  else
-    hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K, K.nodes, K.prog, K.dets,
-                       K.det_off);
-  HIPCHK(hipGetLastError());
+  K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
+
+  // refine the records-per-photon estimate from the last binned launch, if it has landed
+  if (s->ctl_pending && hipEventQuery(s->ctl_ev) == hipSuccess) {
+    s->ctl_pending = false;
+    if (s->h_ctl[4] > 0) {
+      const double rpp = (double)(s->h_ctl[3] + s->h_ctl[1]) / (double)s->h_ctl[4];
+      s->rpp_est = std::max(1.0, rpp);
+    }
+  }
+  // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
+  // values are exact only then) and a grid of at most MAX_TILES tiles
+  const bool binned = dt.jmean && (cfg->flags & SMCRT_FLAG_PATHLENGTH) && !(cfg->flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
+                      s->n_tiles > 0 && !s->force_atomic;
+  uint64_t batch = cfg->n_photons;
+  if (binned) {
+    uint64_t want = pool_records_for(s, cfg->n_photons);
+    if (!ensure_pool(s, want)) {
+      (void)ensure_pool(s, want / 4);  // smaller pool, more batches
+    }
+    if (s->pool_chunks) {
+      const double usable = (double)(s->pool_chunks * CHUNK_RECORDS) - (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
+      batch = (uint64_t)std::max(65536.0, usable / (s->rpp_est * 1.25));
+      // (taken after ensure_pool: it may have reallocated the pool)
+      K.rec_pool = s->d_pool;
+      K.chunk_fill = s->d_chunk_fill;
+      K.dep_ctl = s->d_dep_ctl;
+      K.n_chunks = (uint32_t)s->pool_chunks;
+    }
+  }
+  for (uint64_t done = 0; done < cfg->n_photons; done += batch) {
+    const uint64_t n = std::min<uint64_t>(batch, cfg->n_photons - done);
+    K.n_photons = n;
+    K.first_photon = cfg->first_photon + done;
+    K.records = dt.records ? dt.records + done : nullptr;
+    if (K.rec_pool) s->h_ctl[4] = 0;
+    int st = launch_one(s, K, stream);
+    if (st) return st;
+    if (K.rec_pool) s->h_ctl[4] = (uint32_t)std::min<uint64_t>(n, 0xFFFFFFFFull);
+  }
   return SMCRT_OK;
 }
 

@@ -80,6 +80,11 @@ struct KParams {
   unsigned long long* counters;
   smcrt_photon_record* records;
   unsigned long long* queue;  // photon work-queue head (zeroed before launch)
+  // binned jmean deposition (deposit.h): record log in chunks
+  unsigned long long* rec_pool;  // CHUNK_RECORDS records per chunk; NULL -> fp64 atomics into jmean
+  uint32_t* chunk_fill;          // records in each used chunk
+  uint32_t* dep_ctl;             // [0] next chunk, [1] overflowed deposits
+  uint32_t n_chunks;
 };
 
 // ------------------------------------------------------------------ voxels -------
@@ -398,7 +403,8 @@ __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, V3 p, d
 // One voxel crossing of the pending segment: wall_dist + deposit + update_pos
 // (inttau2.f90:417-441, 467-584). Clears L.seg when the segment ends.
 __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double* __restrict__ xf,
-                                         const double* __restrict__ yf, const double* __restrict__ zf) {
+                                         const double* __restrict__ yf, const double* __restrict__ zf,
+                                         bool& dep, uint32_t& dep_vox, double& dep_val) {
   const V3 dir = L.dir;
   bool done = false;
   if (++L.dda_it > (uint32_t)MAX_DDA_ITERS) { L.fault = true; L.tflag = true; done = true; }
@@ -421,18 +427,11 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
       const bool last = L.sd + dcell > L.slen;
       if (last) { dcell = L.slen - L.sd; L.sd = L.slen; }
       else L.sd = L.sd + dcell;
-      L.c_dep++;
-#if defined(SMCRT_DIAG_NO_ATOMIC)
-      if (K.jmean && dcell == -1.0) atomic_add_nr(K.jmean, dcell);  // diagnostic: keep the value live
-#elif defined(SMCRT_DIAG_SCATTER_ATOMIC)
-      if (K.jmean) {  // diagnostic: same atomics, addresses hashed over the grid (no hot voxels)
-        uint32_t h = (uint32_t)lin(K, L.ci, L.cj, L.ck) * 2654435761u;
-        h ^= h >> 15;
-        atomic_add_nr(K.jmean + (h % (uint32_t)(K.nx * K.ny * K.nz)), (double)(float)dcell * L.weight);
-      }
-#else
-      if (K.jmean) atomic_add_nr(K.jmean + lin(K, L.ci, L.cj, L.ck), (double)(float)dcell * L.weight);
-#endif
+      // jmean(cell) += real(dcell,sp)*weight (inttau2.f90:427,434): handed to the caller,
+      // which appends a deposit record (binned path) or adds it atomically
+      dep = true;
+      dep_vox = (uint32_t)lin(K, L.ci, L.cj, L.ck);
+      dep_val = (double)(float)dcell * L.weight;
       if (last) {  // update_pos(.false.)
         L.old.x = L.old.x + dir.x * dcell;
         L.old.y = L.old.y + dir.y * dcell;

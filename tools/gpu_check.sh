@@ -6,10 +6,10 @@ mkdir -p gpurun_out
 fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
 timeout -k 10 ${SMOKE_T:-240} python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log
-if fatal $rc; then exit $rc; fi
+if [ $rc -ne 0 ]; then exit $rc; fi  # a failing smoke may be a device fault: run nothing else
 timeout -k 10 ${TEST_T:-600} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
-if fatal $rc; then exit $rc; fi
+if fatal $rc || grep -q "DEVICE_FAULT\|illegal memory" gpurun_out/pytest_gpu.log; then exit 1; fi
 if [ -n "$NO_BENCH" ]; then exit 0; fi
 timeout -k 10 ${BENCH_T:-400} python bench.py ${BENCH_ARGS} > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.err
