@@ -35,8 +35,6 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
-#define LCTR(c) (sh->ctr[(c)][threadIdx.x])
-
 // The query point of each EVAL state (the exact expressions of the reference).
 __device__ __forceinline__ V3 eval_query(const Lane& L) {
   switch (L.st) {
@@ -83,21 +81,23 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   }
 #pragma unroll
   for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
+#pragma unroll
+  for (int c = 0; c < LU_N; ++c) sh->u[c][threadIdx.x] = 0;
   __syncthreads();
 
   Lane L;
   L.st = ST_FETCH; L.pend = false; L.seg = false; L.fault = false; L.tflag = false;
-  L.c_sdf = L.c_dep = L.c_upd = 0;
-  L.pos = L.dir = L.startPos = L.ssp = L.old = v3(0.0, 0.0, 0.0);
-  L.weight = 1.0; L.tau = L.taurun = L.d = L.minabs = L.minv = 0.0;
+  L.pos = L.dir = L.ssp = L.old = v3(0.0, 0.0, 0.0);
+  L.weight = 1.0; L.tau = L.taurun = L.d = L.minabs = 0.0;
   L.xcell = L.ycell = L.zcell = L.layer = L.old_layer = L.new_layer = L.Ls = 0;
-  L.bounces = L.nscatt = L.status = L.hop = L.loopc = L.inter = L.dda_it = 0;
+  L.hop = L.loopc = L.dda_it = 0;
   L.sd = L.slen = 0.0; L.ci = L.cj = L.ck = 0;
   L.rng.init(0);
   const bool binned = K.rec_pool != nullptr && K.jmean != nullptr;
   RecLog W;
   W.chunk = LOG_NONE; W.fill = 0;
   uint32_t overflow = 0;
+  uint32_t w_dep = 0, w_sdf = 0;  // wave totals (scalar registers)
   uint64_t chunk_base = 0;  // wave-uniform photon chunk
   uint32_t chunk_left = 0;
 
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         uint32_t vox = 0;
         double val = 0.0;
         if (L.seg) dda_step(K, L, xf, yf, zf, dep, vox, val);
-        if (dep) L.c_dep++;
+        w_dep += __popcll(__ballot(dep));
         if (binned) emit_deposits(K, W, dep, vox, val, overflow);
         else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
       }
@@ -162,11 +162,9 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
       R = eval_sdfs(nodes, prog, K.n_prog, eval_query(L), test_kernel && L.st == ST_LAYER, capi, capj);
       // packet%cnts counts the evaluations of tauint2's ds/dsNew arrays only (inttau2.f90:67,83,
       // 138,183,219,232): not the initial layer search, the Fresnel ds lookups or calcNormal.
-      if (have) {
-        L.pend = false;
-        if (L.st == ST_H0 || L.st == ST_H1 || L.st == ST_H3 || L.st == ST_M1 || L.st == ST_G0)
-          L.c_sdf += (uint32_t)K.n_top;
-      }
+      const bool counted = L.st == ST_H0 || L.st == ST_H1 || L.st == ST_H3 || L.st == ST_M1 || L.st == ST_G0;
+      w_sdf += __popcll(__ballot(have && counted)) * (uint32_t)K.n_top;
+      if (have) L.pend = false;
     }
 
     // ---- P3: consume the EVAL result ----------------------------------------------------
@@ -178,7 +176,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           else L.st = ST_T2;
           break;
         case ST_H0:  // inttau2.f90:63-84, 149-152
-          L.minabs = R.minabs; L.minv = R.minv;
+          L.minabs = R.minabs;
           L.d = R.minabs;
           L.loopc = 0;  // march guard
           if (L.d < eps) {  // on a surface: micro-step
@@ -201,17 +199,17 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             else { L.d = (L.tau - L.taurun) / kap; L.pos = L.pos - smul(L.d, L.dir); }
           }
           L.st = ST_H2;
-          start_segment(K, L, oldpos, L.d);
+          start_segment(K, L, sh, oldpos, L.d);
           break;
         }
         case ST_H3:  // :133-152
-          L.minabs = R.minabs; L.minv = R.minv;
+          L.minabs = R.minabs;
           L.d = R.minabs;
           if (R.minv > 0.0) L.tflag = true;
           L.st = (L.taurun >= L.tau || L.tflag) ? ST_T2END : ST_M0;
           break;
         case ST_M1:  // :177-191
-          L.minabs = R.minabs; L.minv = R.minv;
+          L.minabs = R.minabs;
           L.d = R.minabs;
           if (R.minv > 0.0) { L.tflag = true; L.st = ST_B0; }
           else L.st = ST_M0;
@@ -230,7 +228,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           if (n1 != n2) { L.st = ST_F0; L.pend = true; break; }
           L.layer = L.new_layer;  // equal n: cross, :318-328
           L.st = ST_X1;
-          start_segment(K, L, L.pos, L.d);
+          start_segment(K, L, sh, L.pos, L.d);
           break;
         }
         case ST_F0:  // ds(new), ds(old) at pos (kept in sd/slen: no segment is active)
@@ -264,9 +262,9 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             const double s2 = 2.0 * dot(N, L.dir);
             L.dir = L.dir - smul(s2, N);
             LCTR(LC_REFL)++;
-            L.startPos = L.pos;
-            L.bounces += 1;
-            if (L.bounces > 1000) {  // :313-315: return without write-back
+            sh->start[0][threadIdx.x] = L.pos.x; sh->start[1][threadIdx.x] = L.pos.y;
+            sh->start[2][threadIdx.x] = L.pos.z;
+            if (++LU(LU_BOUNCES) > 1000) {  // :313-315: return without write-back
               LCTR(LC_BABORT)++;
               L.pos = v3(sh->entry[0][threadIdx.x], sh->entry[1][threadIdx.x], sh->entry[2][threadIdx.x]);
               L.dir = v3(sh->entry[3][threadIdx.x], sh->entry[4][threadIdx.x], sh->entry[5][threadIdx.x]);
@@ -284,7 +282,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             L.dir = smul(eta, L.dir) + smul(eta * c1 - c2, Nt);
             L.layer = L.new_layer;
             L.st = ST_X1;
-            start_segment(K, L, L.pos, L.d);
+            start_segment(K, L, sh, L.pos, L.d);
           }
           break;
         }
@@ -313,7 +311,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           L.pos = L.pos + smul(L.d, L.dir);
           L.st = ST_B0;
         }
-        start_segment(K, L, oldpos, L.d);
+        start_segment(K, L, sh, oldpos, L.d);
       }
     }
 
@@ -326,8 +324,10 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         L.taurun = L.taurun + L.d * props[L.layer - 1].kappa;
         L.pos = L.ssp;
       }
-      rec = true; rec_start = L.startPos; rec_sep = pointsep(L.pos, L.startPos);  // :125-131, 195-201
-      L.startPos = L.pos;
+      rec = true;  // :125-131, 195-201
+      rec_start = v3(sh->start[0][threadIdx.x], sh->start[1][threadIdx.x], sh->start[2][threadIdx.x]);
+      rec_sep = pointsep(L.pos, rec_start);
+      sh->start[0][threadIdx.x] = L.pos.x; sh->start[1][threadIdx.x] = L.pos.y; sh->start[2][threadIdx.x] = L.pos.z;
       if (L.st == ST_H2) {
         L.st = ST_H3; L.pend = true;
       } else if (L.st == ST_X1) {
@@ -364,7 +364,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         if (L.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2036-2065 / 2126-2170
           if (L.tflag || L.fault) {
             L.st = ST_DONE;
-          } else if (++L.inter > (uint32_t)MAX_INTERACTIONS) {
+          } else if (++LU(LU_INTER) > (uint32_t)MAX_INTERACTIONS) {
             L.fault = true; L.st = ST_DONE;
           } else {
             const double ran = L.rng.next(K.key0, K.key1);
@@ -377,19 +377,19 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
               sc = true;
               if (L.weight < 0.01) {
                 if (ran < 0.1) L.weight = L.weight / 0.1;
-                else { L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++; sc = false; }
+                else { L.tflag = true; LU(LU_STATUS) = 1; LCTR(LC_ABSORBED)++; sc = false; }
               }
             } else if (ran < pr.albedo) {
               sc = true;
             } else {
-              L.tflag = true; L.status = 1; LCTR(LC_ABSORBED)++;
+              L.tflag = true; LU(LU_STATUS) = 1; LCTR(LC_ABSORBED)++;
               if (!test_kernel) add_cell(K, K.absorb, L, 1.0);  // recordWeight(packet, 1.0)
             }
             if (sc) {
               scatter(K, L, pr.hgg);
-              L.nscatt++; LCTR(LC_SCATTERS)++;
+              const uint32_t st = ++LU(LU_NSCATT);
+              LCTR(LC_SCATTERS)++;
               if (test_kernel && !survival) {
-                const uint32_t st = L.nscatt;
                 if (st >= 1 && st <= 4) {
                   if (K.moments) {
                     double* m = K.moments + 3 * (st - 1);
@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
                   }
                 } else if (K.flags & SMCRT_FLAG_END_EARLY) {
                   L.tflag = true;
-                  L.status = 4;
+                  LU(LU_STATUS) = 4;
                 }
               }
               L.st = ST_T2;
@@ -411,7 +411,8 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           }
         }
         if (L.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
-          L.startPos = L.pos;
+          sh->start[0][threadIdx.x] = L.pos.x; sh->start[1][threadIdx.x] = L.pos.y;
+          sh->start[2][threadIdx.x] = L.pos.z;
           sh->entry[0][threadIdx.x] = L.pos.x; sh->entry[1][threadIdx.x] = L.pos.y;
           sh->entry[2][threadIdx.x] = L.pos.z; sh->entry[3][threadIdx.x] = L.dir.x;
           sh->entry[4][threadIdx.x] = L.dir.y; sh->entry[5][threadIdx.x] = L.dir.z;
@@ -422,7 +423,8 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           L.st = ST_H0;  // arrives in P8
         }
         if (L.st == ST_EMIT) {  // kernelsMod.f90:1937-1945
-          L.fault = false; L.status = 0; L.nscatt = 0; L.layer = 0; L.inter = 0; L.bounces = 0;
+          L.fault = false; L.layer = 0;
+          LU(LU_STATUS) = 0; LU(LU_NSCATT) = 0; LU(LU_INTER) = 0; LU(LU_BOUNCES) = 0;
           L.xcell = L.ycell = L.zcell = 0;
           emit(K, L);
           if (!test_kernel) {
@@ -438,8 +440,8 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           else { L.st = ST_LAYER; L.pend = true; }
         }
         if (L.st == ST_DONE) {  // photon finished
-          if (L.fault) { L.status = 3; LCTR(LC_FAULTS)++; }
-          else if (L.status == 0) { L.status = 2; LCTR(LC_ESCAPED)++; }
+          if (L.fault) { LU(LU_STATUS) = 3; LCTR(LC_FAULTS)++; }
+          else if (LU(LU_STATUS) == 0) { LU(LU_STATUS) = 2; LCTR(LC_ESCAPED)++; }
           LCTR(LC_PHOTONS)++;
           LCTR(LC_DRAWS) += L.rng.draws;
           if (rec_on) {
@@ -450,10 +452,10 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             r->weight = L.weight;
             r->cell[0] = L.xcell; r->cell[1] = L.ycell; r->cell[2] = L.zcell;
             r->layer = L.layer;
-            r->nscatt = L.nscatt;
-            r->bounces = L.bounces;
+            r->nscatt = LU(LU_NSCATT);
+            r->bounces = LU(LU_BOUNCES);
             r->draws = L.rng.draws;
-            r->status = L.status;
+            r->status = LU(LU_STATUS);
           }
           L.tflag = false; L.fault = false;
           L.st = ST_FETCH;
@@ -478,9 +480,9 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     c[SMCRT_CTR_EMIT_RETRIES] = LCTR(LC_RETRIES);
     c[SMCRT_CTR_SCATTERS] = LCTR(LC_SCATTERS);
     c[SMCRT_CTR_ABSORBED] = LCTR(LC_ABSORBED);
-    c[SMCRT_CTR_SDF_EVALS] = L.c_sdf;
-    c[SMCRT_CTR_DEPOSITS] = L.c_dep;
-    c[SMCRT_CTR_GRID_UPDATES] = L.c_upd;
+    c[SMCRT_CTR_SDF_EVALS] = lane_id == 0 ? w_sdf : 0u;
+    c[SMCRT_CTR_DEPOSITS] = lane_id == 0 ? w_dep : 0u;
+    c[SMCRT_CTR_GRID_UPDATES] = LCTR(LC_UPD);
     c[SMCRT_CTR_TAUINT] = LCTR(LC_TAU);
     c[SMCRT_CTR_FRESNEL] = LCTR(LC_FRES);
     c[SMCRT_CTR_REFLECTIONS] = LCTR(LC_REFL);

@@ -254,15 +254,14 @@ struct Lane {
   V3 pos, dir;
   double weight;
   int32_t xcell, ycell, zcell, layer;
-  uint32_t bounces, nscatt, status;
-  bool tflag, fault;
+  bool tflag, fault;  // bounces, nscatt, status: LDS (LaneShared::u)
   Rng rng;
   // tauint2 locals
   double tau, taurun, d;
-  V3 startPos, ssp;
-  double minabs, minv;  // reductions of the last EVAL at pos
+  V3 ssp;              // startPos: LDS (LaneShared::start)
+  double minabs;       // minval(abs(ds)) of the last EVAL at pos
   int32_t old_layer, new_layer, Ls;
-  uint32_t hop, loopc, inter;  // hop / march-or-glance / interaction loop guards
+  uint32_t hop, loopc;  // hop / march-or-glance loop guards (interactions: LDS)
   // state machine
   uint32_t st;
   bool pend;  // an EVAL was requested for the current state
@@ -273,17 +272,22 @@ struct Lane {
   double sd, slen;
   int32_t ci, cj, ck;
   uint32_t dda_it;
-  // hot counters (the rest are in LDS)
-  uint32_t c_sdf, c_dep, c_upd;
 };
 
 // LDS-resident per-lane values, [field][threadIdx] so lanes never share a bank.
+// Everything here is touched at most a few times per photon, so it lives in LDS instead of
+// costing a register for the whole kernel.
 enum : int { LC_PHOTONS = 0, LC_RETRIES, LC_SCATTERS, LC_ABSORBED, LC_TAU, LC_FRES, LC_REFL, LC_BABORT,
-             LC_FAULTS, LC_DRAWS, LC_HITS, LC_ESCAPED, LC_N };
+             LC_FAULTS, LC_DRAWS, LC_HITS, LC_ESCAPED, LC_UPD, LC_N };
+enum : int { LU_INTER = 0, LU_BOUNCES, LU_NSCATT, LU_STATUS, LU_N };  // per-photon fields
 struct LaneShared {
   uint32_t ctr[LC_N][256];
+  uint32_t u[LU_N][256];
   double entry[6][256];  // tauint2 entry pos/dir, restored on a bounce abort (inttau2.f90:313-315)
+  double start[3][256];  // startPos of the detector segment (inttau2.f90:59,125-131)
 };
+#define LCTR(c) (sh->ctr[(c)][threadIdx.x])
+#define LU(f) (sh->u[(f)][threadIdx.x])
 
 __device__ __forceinline__ bool is_eval_state(uint32_t s) {
   return s == ST_LAYER || s == ST_H0 || s == ST_H1 || s == ST_H3 || s == ST_M1 || s == ST_G0 || s == ST_F0 ||
@@ -333,7 +337,6 @@ __device__ __forceinline__ void emit(const KParams& K, Lane& L) {
     L.dir = v3(s.dir[0], s.dir[1], s.dir[2]);
   }
   L.tflag = false;
-  L.bounces = 0;
   L.weight = 1.0;
   L.xcell = vox_of(L.pos.x, K.nx, K.xmax, K.inv2x);
   L.ycell = vox_of(L.pos.y, K.ny, K.ymax, K.inv2y);
@@ -378,8 +381,8 @@ __device__ __forceinline__ void scatter(const KParams& K, Lane& L, double hgg) {
 // update_grids entry (inttau2.f90:401-415): start a deposit segment from `p` (centred) of
 // length `dlen` along L.dir; the segment itself runs in the DDA phase. Returns true if the
 // lane must wait for the DDA.
-__device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, V3 p, double dlen) {
-  L.c_upd++;
+__device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneShared* sh, V3 p, double dlen) {
+  LCTR(LC_UPD)++;
   V3 old = v3(p.x + K.xmax, p.y + K.ymax, p.z + K.zmax);
   int32_t ci = cell_of(old.x, K.nx, K.xmax, K.inv2x), cj = cell_of(old.y, K.ny, K.ymax, K.inv2y),
           ck = cell_of(old.z, K.nz, K.zmax, K.inv2z);
