@@ -35,30 +35,78 @@ def workload(grid_n):
     return sc, g, scene.point_source()
 
 
-def cpu_baseline(sc, g, src, seconds, eng):
-    """The CPU restatement (oracle/, 1 core) on a bounded sample of the same workload,
-    plus jmean agreement of the GPU on exactly the same photons."""
+def cpu_threads():
+    """Host cores to use for the CPU leg: this process's CPU share, at most 16 (the GPU
+    box's per-GPU share; nproc there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, min(16, n))
+
+
+def cpu_baseline(sc, g, src, seconds, eng, threads):
+    """The CPU restatement (oracle/, C, one photon stream per photon like the GPU) timed on
+    `threads` host cores for about `seconds` of wall time: threads pull 2000-photon chunks
+    of the same workload (ctypes releases the GIL), so the sample is photons [0, n).
+    Then the GPU runs exactly those photons and its fluence is compared with the CPU's."""
+    import threading
     import numpy as np
     from oracle import pyoracle as O
-    res = None
-    n = 0
+    from rsmcrt_amd.tallies import Result
     chunk = 2000
+    nxt = [0]
+    lock = threading.Lock()
+    results = [Result(g) for _ in range(threads)]
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        res = O.run(sc, g, src, chunk, first_photon=n, result=res)
-        n += chunk
+
+    def worker(i):
+        while time.perf_counter() - t0 < seconds:
+            with lock:
+                first = nxt[0]
+                nxt[0] += chunk
+            O.run(sc, g, src, chunk, first_photon=first, result=results[i])
+
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(threads)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
     dt = time.perf_counter() - t0
+    n = nxt[0]
+    res = results[0]
+    for r in results[1:]:
+        res.merge(r)
+    assert res.n_photons == n
     gpu = eng.run(src, n)
     fc, fg = res.normalised_fluence(), gpu.normalised_fluence()
     rmse = float(np.sqrt(np.mean((fg - fc) ** 2)))
     rel = float(np.max(np.abs(fg - fc)) / max(1e-300, float(np.max(np.abs(fc)))))
     same_counters = gpu.counters_dict() == res.counters_dict()
-    return {"value": n / dt, "unit": "photon packets/s", "cores": 1, "kind": "port",
-            "sample": f"photons [0,{n}) of the same workload on 1 host core (oracle/ C restatement, gcc -O2)",
+    return {"value": n / dt, "unit": "photon packets/s", "cores": threads, "kind": "port",
+            "sample": f"photons [0,{n}) of the same workload, oracle/ C restatement (gcc -O2) on {threads} host "
+                      f"threads for {dt:.1f} s",
             "seconds": round(dt, 2)}, {"jmean_rmse_vs_cpu_same_photons": rmse,
                                       "jmean_max_rel_diff_vs_cpu": rel,
                                       "counters_bit_exact_vs_cpu": same_counters,
                                       "photons_compared": n}
+
+
+def pmc_traffic(batch, grid, steps_kernel="transport_kernel<true>"):
+    """HBM bytes per transport launch from the committed rocprofv3 PMC summary of this
+    exact configuration (tools/profile.sh -> profiles/transport_traffic.json), else None."""
+    p = os.path.join(ROOT, "profiles", "transport_traffic.json")
+    try:
+        with open(p) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("batch") != batch or t.get("grid") != grid:
+        return None, None
+    return t.get("hbm_bytes_per_launch"), t.get("source")
 
 
 def main():
@@ -70,6 +118,7 @@ def main():
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--seed", type=int, default=123456789)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share, <= 16")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
     ap.add_argument("--source", default="point", choices=["point", "uniform"],
@@ -117,18 +166,17 @@ def main():
     for s in range(args.warmup):
         step(s)
     torch.cuda.synchronize()
+    eng.set_timing(True)
+    eng.kernel_times()  # reset
     c0 = counters.clone()
     if world > 1:
         dist.all_reduce(c0)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev0.record(stream)
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
-    ev1.record(stream)
     if world > 1:
         for t in (jmean, absorb, nscatt, counters):
             dist.all_reduce(t)
@@ -140,17 +188,23 @@ def main():
     if world > 1:
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     elapsed = float(elapsed.item())
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # launches are back to back on `stream`
+    kt = eng.kernel_times()  # HIP events around each kernel group, on the launch stream
+    eng.set_timing(False)
+    launches = max(1, kt["launches"])
+    kern_ms = kt["transport_ms"] / launches
+    dep_ms = kt["deposit_ms"] / launches
     cdelta = (counters - c0).cpu().numpy()  # all ranks, timed steps only
     photons = world * args.steps * B
 
     out = None
     if rank == 0:
         deposits = float(cdelta[abi.CTR["deposits"]]) / world  # per rank, over the timed steps
-        dep_per_launch = deposits / args.steps
-        # algorithmic bytes of the deposition: one fp32 jmean read + write per deposit (8 B),
-        # SURVEY.md §8(d)
-        achieved = 8.0 * dep_per_launch / (kern_ms * 1e-3) / 1e9
+        dep_per_launch = deposits / launches
+        # algorithmic HBM bytes of the transport kernel: 8 B per jmean deposit (SURVEY.md
+        # §8(d): the reference's fp32 read+write per atomic; here one 8-B deposit record)
+        alg_bytes = 8.0 * dep_per_launch
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(B, args.grid)
         out = {
             "metric": "photon packets/sec (128^3 jmean grid, path-length deposition)",
             "value": photons / elapsed,
@@ -169,15 +223,19 @@ def main():
                        "grid": [g.nx, g.ny, g.nz], "photons_per_step_per_gpu": B, "photons_timed": photons,
                        "parallelism": f"photon-index shards x{world} + RCCL all-reduce of tallies"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": achieved / 8000.0, "traffic": None,
+                         "frac": achieved / 8000.0, "traffic": traffic,
                          "kernel": "transport_kernel", "avg_launch_ms": kern_ms,
-                         "algorithmic_bytes_per_launch": 8.0 * dep_per_launch,
+                         "launches_timed": kt["launches"],
+                         "algorithmic_bytes_per_launch": alg_bytes,
+                         "traffic_source": traffic_src,
                          "deposits_per_photon": deposits / (args.steps * B),
-                         "deposits_per_s": dep_per_launch / (kern_ms * 1e-3)},
+                         "deposit_fold_ms_per_launch": dep_ms,
+                         "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) / world / launches,
+                         "binding_resource": "fp64 VALU issue + divergence (see DESIGN.md), not HBM"},
             "cpu_baseline": None,
         }
     if rank == 0 and world == 1 and not args.no_cpu:
-        base, agree = cpu_baseline(sc, g, src, args.cpu_seconds, eng)
+        base, agree = cpu_baseline(sc, g, src, args.cpu_seconds, eng, args.cpu_threads or cpu_threads())
         out["cpu_baseline"] = base
         out["parity"] = agree
     if rank == 0:

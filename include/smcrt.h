@@ -182,6 +182,8 @@ enum {
   SMCRT_CTR_RNG_DRAWS,        /* ran2() calls */
   SMCRT_CTR_DETECTOR_HITS,    /* detector bin increments */
   SMCRT_CTR_ESCAPED,          /* photons terminated by leaving the grid/geometry */
+  SMCRT_CTR_WAVE_ITERS,       /* engine diagnostic: scheduler iterations summed over waves
+                                 (no reference counterpart; launch-geometry dependent) */
   SMCRT_NCOUNTERS = 16
 };
 
@@ -265,6 +267,20 @@ typedef struct smcrt_device_tallies {
 
 int smcrt_run_device(smcrt_scene* scene, const smcrt_source* src, const smcrt_run_config* cfg,
                      smcrt_device_tallies* dev, void* stream);
+
+/* Per-kernel device time (ms) of the launches made since the previous query, from HIP
+ * events recorded on the launch stream around each kernel group while timing is enabled
+ * (off by default; no reference counterpart: it is the measurement hook of bench.py).
+ * smcrt_scene_kernel_times waits for those launches to finish, then resets the sums. */
+typedef struct smcrt_kernel_times {
+  double transport_ms;  /* transport_kernel */
+  double deposit_ms;    /* binned jmean fold: bin_hist .. bin_reduce */
+  int64_t launches;     /* transport launches timed */
+  int64_t reserved;
+} smcrt_kernel_times;
+
+int smcrt_scene_set_timing(smcrt_scene* scene, int32_t enable);
+int smcrt_scene_kernel_times(smcrt_scene* scene, smcrt_kernel_times* out);
 
 /* Normalisation of writer.f90:25-52 (normalise_fluence): grid *= nx*ny*nz / nphotons,
  * i.e. (8*xmax*ymax*zmax)/(nphotons*dx*dy*dz). Host-side helper on an fp32 grid. */

@@ -48,10 +48,12 @@ FLAG_RECORD_PHOTONS = 1 << 5
 COUNTER_NAMES = [
     "photons", "emit_retries", "scatters", "absorbed", "sdf_evals", "deposits",
     "grid_updates", "tauint", "fresnel", "reflections", "bounce_aborts", "faults",
-    "rng_draws", "detector_hits", "escaped", "reserved15",
+    "rng_draws", "detector_hits", "escaped", "wave_iters",
 ]
 NCOUNTERS = 16
 CTR = {name: i for i, name in enumerate(COUNTER_NAMES)}
+# counters that describe the engine, not the photons: excluded from parity comparisons
+ENGINE_COUNTERS = ("wave_iters",)
 
 
 class SdfNode(C.Structure):
@@ -123,8 +125,13 @@ def record_dtype():
                      ("status", "<u4")])
 
 
+class KernelTimes(C.Structure):
+    _fields_ = [("transport_ms", C.c_double), ("deposit_ms", C.c_double), ("launches", C.c_int64),
+                ("reserved", C.c_int64)]
+
+
 EXPORTED_SYMBOLS = [
     "smcrt_abi_version", "smcrt_device_count", "smcrt_last_error", "smcrt_scene_create",
     "smcrt_scene_destroy", "smcrt_scene_det_bins", "smcrt_scene_set_optprops", "smcrt_run",
-    "smcrt_run_device", "smcrt_normalise_fluence",
+    "smcrt_run_device", "smcrt_normalise_fluence", "smcrt_scene_set_timing", "smcrt_scene_kernel_times",
 ]

@@ -6,10 +6,11 @@
 // profiles/r01_atomic_microbench.txt), and a wave cannot overlap them with its own
 // compute. So the transport kernel instead appends 8-byte deposit records
 // (voxel << 32 | f32 value) with wave-compacted stores into 128-KiB chunks of a record
-// pool, and four small kernels fold them in:
-//   bin_hist     records -> per-tile counts (tile = TILE_VOXELS consecutive voxels)
-//   bin_scan     counts  -> tile offsets and the list of reduce pieces
-//   bin_scatter  records -> tile-sorted order (one returning atomic per tile per chunk)
+// pool, and five small kernels fold them in:
+//   bin_hist     records -> counts per (tile, bin block) (tile = TILE_VOXELS voxels)
+//   bin_rowscan  counts  -> each bin block's offset inside each tile; tile totals
+//   bin_scan     totals  -> tile offsets and the list of reduce pieces
+//   bin_scatter  records -> tile-sorted order (LDS-staged, no global atomics)
 //   bin_reduce   one piece of one tile per block: fp64 LDS accumulation, then the
 //                tile's non-zero sums are added to the fp64 jmean
 // Every record is read three times and written twice (40 B of HBM traffic per deposit,
@@ -89,56 +90,92 @@ __device__ __forceinline__ void close_log(const KParams& K, RecLog& W, uint32_t 
   }
 }
 
-// ---- bin_hist: per-tile record counts -------------------------------------------------
-__global__ __launch_bounds__(1024) void bin_hist(const unsigned long long* __restrict__ pool,
-                                                 const uint32_t* __restrict__ chunk_fill,
-                                                 const uint32_t* __restrict__ dep_ctl, uint32_t n_chunks,
-                                                 uint32_t n_tiles, uint32_t* __restrict__ tile_count) {
+// Chunk c of the pool belongs to bin block c % BIN_BLOCKS in both bin_hist and bin_scatter,
+// so every (tile, block) pair owns one contiguous run of the sorted array and the scatter
+// needs no global atomics.
+constexpr uint32_t BIN_BLOCKS = 1024;
+constexpr int BIN_THREADS = 1024;
+constexpr uint32_t STAGE_RECORDS = 8192;                        // records per LDS pass of bin_scatter
+constexpr int STAGE_PER_THREAD = STAGE_RECORDS / BIN_THREADS;  // 8
+
+__device__ __forceinline__ uint32_t rec_tile(unsigned long long x) { return (uint32_t)(x >> 32) >> TILE_SHIFT; }
+
+// Exclusive scan of one value per thread over a 1024-thread block; *total gets the sum.
+// `wsum` is 16 words of LDS. Ends with the block synchronised.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) {
+    const uint32_t t = wsum[i];
+    before += i < w ? t : 0u;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
+// ---- bin_hist: record counts per (tile, bin block) -------------------------------------
+__global__ __launch_bounds__(BIN_THREADS) void bin_hist(const unsigned long long* __restrict__ pool,
+                                                        const uint32_t* __restrict__ chunk_fill,
+                                                        const uint32_t* __restrict__ dep_ctl, uint32_t n_chunks,
+                                                        uint32_t n_tiles, uint32_t* __restrict__ counts) {
   __shared__ uint32_t hist[MAX_TILES];
   for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) hist[t] = 0;
   __syncthreads();
   const uint32_t used = dep_ctl[0] < n_chunks ? dep_ctl[0] : n_chunks;
-  for (uint32_t c = blockIdx.x; c < used; c += gridDim.x) {
+  for (uint32_t c = blockIdx.x; c < used; c += BIN_BLOCKS) {
     const uint32_t fill = chunk_fill[c];
     const unsigned long long* r = pool + (uint64_t)c * CHUNK_RECORDS;
-    for (uint32_t i = threadIdx.x; i < fill; i += blockDim.x)
-      atomicAdd(&hist[(uint32_t)(r[i] >> 32) >> TILE_SHIFT], 1u);
+    for (uint32_t i = threadIdx.x; i < fill; i += blockDim.x) atomicAdd(&hist[rec_tile(r[i])], 1u);
   }
   __syncthreads();
-  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x)
-    if (hist[t]) atomicAdd(tile_count + t, hist[t]);
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) counts[(uint64_t)t * BIN_BLOCKS + blockIdx.x] = hist[t];
+}
+
+// ---- bin_rowscan: per tile, exclusive scan over the bin blocks; tile totals ---------------
+__global__ __launch_bounds__(BIN_BLOCKS) void bin_rowscan(uint32_t* __restrict__ counts,
+                                                          uint32_t* __restrict__ tile_count) {
+  __shared__ uint32_t wsum[16];
+  uint32_t* row = counts + (uint64_t)blockIdx.x * BIN_BLOCKS;
+  uint32_t total;
+  const uint32_t ex = block_exscan(row[threadIdx.x], wsum, &total);
+  row[threadIdx.x] = ex;
+  if (threadIdx.x == 0) tile_count[blockIdx.x] = total;
 }
 
 // ---- bin_scan: tile offsets and reduce pieces (one block) ----------------------------------
 __global__ __launch_bounds__(1024) void bin_scan(const uint32_t* __restrict__ tile_count, uint32_t n_tiles,
-                                                 uint32_t* __restrict__ tile_cursor, Piece* __restrict__ pieces,
+                                                 uint32_t* __restrict__ tile_start, Piece* __restrict__ pieces,
                                                  uint32_t* __restrict__ dep_ctl) {
-  __shared__ uint32_t part[1024][2];
+  __shared__ uint32_t wsum[16];
   const uint32_t per = (n_tiles + blockDim.x - 1) / blockDim.x;
-  const uint32_t t0 = threadIdx.x * per, t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
+  const uint32_t t0 = threadIdx.x * per < n_tiles ? threadIdx.x * per : n_tiles;
+  const uint32_t t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
   uint32_t s = 0, np = 0;
   for (uint32_t t = t0; t < t1; ++t) {
     s += tile_count[t];
     np += (tile_count[t] + PIECE_RECORDS - 1) / PIECE_RECORDS;
   }
-  part[threadIdx.x][0] = s;
-  part[threadIdx.x][1] = np;
-  __syncthreads();
-  if (threadIdx.x == 0) {  // n_tiles <= 8192: a serial scan over 1024 partials is short
-    uint32_t a = 0, b = 0;
-    for (uint32_t i = 0; i < blockDim.x; ++i) {
-      const uint32_t x = part[i][0], y = part[i][1];
-      part[i][0] = a; part[i][1] = b;
-      a += x; b += y;
-    }
-    dep_ctl[2] = b;  // number of pieces
-    dep_ctl[3] = a;  // number of records
+  uint32_t all_s, all_np;
+  uint32_t off = block_exscan(s, wsum, &all_s);
+  uint32_t pc = block_exscan(np, wsum, &all_np);
+  if (threadIdx.x == 0) {
+    dep_ctl[2] = all_np;  // number of pieces
+    dep_ctl[3] = all_s;   // number of records
   }
-  __syncthreads();
-  uint32_t off = part[threadIdx.x][0], pc = part[threadIdx.x][1];
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t c = tile_count[t];
-    tile_cursor[t] = off;
+    tile_start[t] = off;
     for (uint32_t k = 0; k < c; k += PIECE_RECORDS) {
       Piece p;
       p.tile = t; p.start = off + k; p.count = (c - k) < PIECE_RECORDS ? (c - k) : PIECE_RECORDS; p.pad = 0;
@@ -148,46 +185,83 @@ __global__ __launch_bounds__(1024) void bin_scan(const uint32_t* __restrict__ ti
   }
 }
 
-// ---- bin_scatter: records into tile order ----------------------------------------------
-constexpr int SCATTER_THREADS = 1024;
-constexpr int SCATTER_PER_THREAD = CHUNK_RECORDS / SCATTER_THREADS;  // 16
+// ---- bin_scatter: records into tile order --------------------------------------------------
+// Per pass of STAGE_RECORDS records: count per tile in LDS (the returned count is the
+// record's rank), scan, place the records tile-ordered in LDS, then write them out with
+// consecutive threads on consecutive addresses of each tile's run.
+// Dynamic LDS: stage[STAGE_RECORDS] u64 | cnt[n_tiles + 1] | base[n_tiles] | wsum[16].
+inline size_t scatter_lds_bytes(uint32_t n_tiles) {
+  return STAGE_RECORDS * 8 + ((size_t)2 * n_tiles + 1 + 16) * 4;
+}
 
-__global__ __launch_bounds__(SCATTER_THREADS) void bin_scatter(const unsigned long long* __restrict__ pool,
-                                                               const uint32_t* __restrict__ chunk_fill,
-                                                               const uint32_t* __restrict__ dep_ctl,
-                                                               uint32_t n_chunks, uint32_t n_tiles,
-                                                               uint32_t* __restrict__ tile_cursor,
-                                                               unsigned long long* __restrict__ sorted) {
-  __shared__ uint32_t cnt[MAX_TILES];
-  __shared__ uint32_t base[MAX_TILES];
+__global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long long* __restrict__ pool,
+                                                           const uint32_t* __restrict__ chunk_fill,
+                                                           const uint32_t* __restrict__ dep_ctl, uint32_t n_chunks,
+                                                           uint32_t n_tiles, const uint32_t* __restrict__ tile_start,
+                                                           const uint32_t* __restrict__ counts,
+                                                           unsigned long long* __restrict__ sorted) {
+  extern __shared__ unsigned long long stage[];
+  uint32_t* cnt = (uint32_t*)(stage + STAGE_RECORDS);
+  uint32_t* base = cnt + n_tiles + 1;
+  uint32_t* wsum = base + n_tiles;
   const uint32_t used = dep_ctl[0] < n_chunks ? dep_ctl[0] : n_chunks;
-  for (uint32_t c = blockIdx.x; c < used; c += gridDim.x) {
-    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) cnt[t] = 0;
-    __syncthreads();
+  if (blockIdx.x >= used) return;  // block-uniform
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x)
+    base[t] = tile_start[t] + counts[(uint64_t)t * BIN_BLOCKS + blockIdx.x];
+  const uint32_t per = (n_tiles + blockDim.x - 1) / blockDim.x;
+  const uint32_t t0 = threadIdx.x * per < n_tiles ? threadIdx.x * per : n_tiles;
+  const uint32_t t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
+  for (uint32_t c = blockIdx.x; c < used; c += BIN_BLOCKS) {
     const uint32_t fill = chunk_fill[c];
     const unsigned long long* r = pool + (uint64_t)c * CHUNK_RECORDS;
-    unsigned long long v[SCATTER_PER_THREAD];
+    for (uint32_t h = 0; h < fill; h += STAGE_RECORDS) {
+      const uint32_t n = fill - h < STAGE_RECORDS ? fill - h : STAGE_RECORDS;
+      for (uint32_t t = threadIdx.x; t <= n_tiles; t += blockDim.x) cnt[t] = 0;
+      __syncthreads();
+      unsigned long long v[STAGE_PER_THREAD];
+      uint32_t rank[STAGE_PER_THREAD];
 #pragma unroll
-    for (int k = 0; k < SCATTER_PER_THREAD; ++k) {
-      const uint32_t i = threadIdx.x + k * SCATTER_THREADS;
-      v[k] = i < fill ? r[i] : ~0ull;
-      if (i < fill) atomicAdd(&cnt[(uint32_t)(v[k] >> 32) >> TILE_SHIFT], 1u);
-    }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
-      const uint32_t n = cnt[t];
-      if (n) base[t] = atomicAdd(tile_cursor + t, n);
-      cnt[t] = 0;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SCATTER_PER_THREAD; ++k) {
-      if (v[k] != ~0ull) {
-        const uint32_t t = (uint32_t)(v[k] >> 32) >> TILE_SHIFT;
-        sorted[base[t] + atomicAdd(&cnt[t], 1u)] = v[k];
+      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+        const uint32_t i = threadIdx.x + k * BIN_THREADS;
+        v[k] = i < n ? r[h + i] : 0ull;
       }
+#pragma unroll
+      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+        const uint32_t i = threadIdx.x + k * BIN_THREADS;
+        rank[k] = i < n ? atomicAdd(&cnt[rec_tile(v[k])], 1u) : 0u;
+      }
+      __syncthreads();
+      // exclusive scan of cnt[0..n_tiles) in place; cnt[n_tiles] = n
+      uint32_t s = 0;
+      for (uint32_t t = t0; t < t1; ++t) s += cnt[t];
+      uint32_t all;
+      uint32_t off = block_exscan(s, wsum, &all);
+      for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t x = cnt[t];
+        cnt[t] = off;
+        off += x;
+      }
+      if (threadIdx.x == 0) cnt[n_tiles] = n;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+        const uint32_t i = threadIdx.x + k * BIN_THREADS;
+        if (i < n) stage[cnt[rec_tile(v[k])] + rank[k]] = v[k];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+        const uint32_t j = threadIdx.x + k * BIN_THREADS;
+        if (j < n) {
+          const unsigned long long x = stage[j];
+          const uint32_t t = rec_tile(x);
+          sorted[base[t] + (j - cnt[t])] = x;
+        }
+      }
+      __syncthreads();
+      for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) base[t] += cnt[t + 1] - cnt[t];
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 

@@ -97,11 +97,11 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   RecLog W;
   W.chunk = LOG_NONE; W.fill = 0;
   uint32_t overflow = 0;
-  uint32_t w_dep = 0, w_sdf = 0;  // wave totals (scalar registers)
+  uint32_t w_dep = 0, w_sdf = 0, w_iters = 0;  // wave totals (scalar registers)
   uint64_t chunk_base = 0;  // wave-uniform photon chunk
   uint32_t chunk_left = 0;
 
-  for (;;) {
+  for (;; ++w_iters) {
     // ---- photon fetch (wave-aggregated work queue) ------------------------------------
     // A wave takes FETCH_CHUNK photon indices per (returning) queue atomic and hands them
     // to its lanes as they free up: a returning atomic waits for all of the wave's
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     c[SMCRT_CTR_RNG_DRAWS] = LCTR(LC_DRAWS);
     c[SMCRT_CTR_DETECTOR_HITS] = LCTR(LC_HITS);
     c[SMCRT_CTR_ESCAPED] = LCTR(LC_ESCAPED);
-    c[15] = 0;
+    c[SMCRT_CTR_WAVE_ITERS] = lane_id == 0 ? w_iters : 0u;
 #pragma unroll
     for (int i = 0; i < SMCRT_NCOUNTERS; ++i) {
       const uint32_t s = wave_sum_u32(c[i]);
@@ -567,8 +567,10 @@ struct smcrt_scene {
   unsigned long long* d_sorted = nullptr;  // tile-sorted records
   uint32_t* d_chunk_fill = nullptr;
   uint32_t* d_dep_ctl = nullptr;      // [0] chunks taken [1] overflow [2] pieces [3] records
-  uint32_t* d_tile_count = nullptr;   // n_tiles
-  uint32_t* d_tile_cursor = nullptr;  // n_tiles
+  uint32_t* d_tile_count = nullptr;  // n_tiles
+  uint32_t* d_tile_start = nullptr;  // n_tiles
+  uint32_t* d_bin_counts = nullptr;  // [n_tiles][BIN_BLOCKS]
+  size_t scatter_lds = 0;
   Piece* d_pieces = nullptr;
   uint64_t pool_chunks = 0, max_pieces = 0;
   double rpp_est = 1024.0;           // deposit records per photon, refined from past launches
@@ -576,8 +578,32 @@ struct smcrt_scene {
   hipEvent_t ctl_ev = nullptr;
   bool ctl_pending = false;
   bool force_atomic = false;  // SMCRT_DEPOSIT=atomic
+  // smcrt_scene_kernel_times: event triples (before transport, after transport, after
+  // the deposit fold) of the launches since the last harvest
+  bool timing = false;
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  double t_transport = 0.0, t_deposit = 0.0;
+  int64_t t_launches = 0;
   std::mutex mu;
 };
+
+constexpr size_t MAX_TIMED = 256;  // launches kept before the events are harvested
+
+// Fold the recorded event triples into the sums (waits for them).
+static hipError_t harvest_times(smcrt_scene* s) {
+  for (size_t i = 0; i < s->tev_used; ++i) {
+    hipEvent_t* e = &s->tev[3 * i];
+    hipError_t err = hipEventSynchronize(e[2]);
+    if (err != hipSuccess) return err;
+    float a = 0.f, b = 0.f;
+    if ((err = hipEventElapsedTime(&a, e[0], e[1])) != hipSuccess) return err;
+    if ((err = hipEventElapsedTime(&b, e[1], e[2])) != hipSuccess) return err;
+    s->t_transport += a; s->t_deposit += b; s->t_launches += 1;
+  }
+  s->tev_used = 0;
+  return hipSuccess;
+}
 
 static TopProps make_props(const smcrt_sdf_node& nd) {
   TopProps p;  // init_mono, opticalProperties.f90:107-125
@@ -611,8 +637,9 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off,
                   s->d_queue, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_dep_ctl, s->d_tile_count,
-                  s->d_tile_cursor, s->d_pieces};
+                  s->d_tile_start, s->d_bin_counts, s->d_pieces};
   if (s->ctl_ev) (void)hipEventDestroy(s->ctl_ev);
+  for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
   if (s->h_ctl) (void)hipHostFree(s->h_ctl);
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -731,8 +758,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     s->force_atomic = fa && std::string(fa) == "atomic";
     if (s->n_tiles) {
       if ((st = dalloc(&s->d_dep_ctl, 4)) || (st = dalloc(&s->d_tile_count, s->n_tiles)) ||
-          (st = dalloc(&s->d_tile_cursor, s->n_tiles)))
+          (st = dalloc(&s->d_tile_start, s->n_tiles)) ||
+          (st = dalloc(&s->d_bin_counts, (size_t)s->n_tiles * BIN_BLOCKS)))
         return cleanup_fail(st);
+      s->scatter_lds = scatter_lds_bytes(s->n_tiles);
+      if (hipFuncSetAttribute((const void*)bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)s->scatter_lds) != hipSuccess)
+        return cleanup_fail(fail(SMCRT_ERR_HIP, "bin_scatter LDS attribute"));
       if (hipHostMalloc((void**)&s->h_ctl, 8 * sizeof(uint32_t)) != hipSuccess ||
           hipEventCreateWithFlags(&s->ctl_ev, hipEventDisableTiming) != hipSuccess)
         return cleanup_fail(fail(SMCRT_ERR_HIP, "pinned/event allocation failed"));
@@ -806,7 +838,18 @@ static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
   const bool binned = K.rec_pool != nullptr;
   if (binned) {
     HIPCHK(hipMemsetAsync(s->d_dep_ctl, 0, 4 * sizeof(uint32_t), stream));
-    HIPCHK(hipMemsetAsync(s->d_tile_count, 0, s->n_tiles * sizeof(uint32_t), stream));
+  }
+  hipEvent_t* ev = nullptr;
+  if (s->timing) {
+    if (s->tev_used == MAX_TIMED) HIPCHK(harvest_times(s));
+    if (3 * (s->tev_used + 1) > s->tev.size())
+      for (int i = 0; i < 3; ++i) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        s->tev.push_back(e);
+      }
+    ev = &s->tev[3 * s->tev_used++];
+    HIPCHK(hipEventRecord(ev[0], stream));
   }
   const uint64_t waves_needed = (K.n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
@@ -818,15 +861,19 @@ static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
     hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K, K.nodes, K.prog, K.dets,
                        K.det_off);
   HIPCHK(hipGetLastError());
+  if (ev) HIPCHK(hipEventRecord(ev[1], stream));
   if (binned) {
     const uint32_t nch = (uint32_t)s->pool_chunks;
     const uint64_t nv = (uint64_t)s->grid.nx * s->grid.ny * s->grid.nz;
-    hipLaunchKernelGGL(bin_hist, dim3(1024), dim3(1024), 0, stream, s->d_pool, s->d_chunk_fill, s->d_dep_ctl, nch,
-                       s->n_tiles, s->d_tile_count);
-    hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, stream, s->d_tile_count, s->n_tiles, s->d_tile_cursor,
+    hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, stream, s->d_pool, s->d_chunk_fill,
+                       s->d_dep_ctl, nch, s->n_tiles, s->d_bin_counts);
+    hipLaunchKernelGGL(bin_rowscan, dim3(s->n_tiles), dim3(BIN_BLOCKS), 0, stream, s->d_bin_counts,
+                       s->d_tile_count);
+    hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, stream, s->d_tile_count, s->n_tiles, s->d_tile_start,
                        s->d_pieces, s->d_dep_ctl);
-    hipLaunchKernelGGL(bin_scatter, dim3(1024), dim3(SCATTER_THREADS), 0, stream, s->d_pool, s->d_chunk_fill,
-                       s->d_dep_ctl, nch, s->n_tiles, s->d_tile_cursor, s->d_sorted);
+    hipLaunchKernelGGL(bin_scatter, dim3(BIN_BLOCKS), dim3(BIN_THREADS), s->scatter_lds, stream, s->d_pool,
+                       s->d_chunk_fill, s->d_dep_ctl, nch, s->n_tiles, s->d_tile_start, s->d_bin_counts,
+                       s->d_sorted);
     hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, stream, s->d_sorted, s->d_pieces, s->d_dep_ctl, nv,
                        K.jmean);
     HIPCHK(hipGetLastError());
@@ -835,6 +882,7 @@ static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
     HIPCHK(hipEventRecord(s->ctl_ev, stream));
     s->ctl_pending = true;
   }
+  if (ev) HIPCHK(hipEventRecord(ev[2], stream));
   return SMCRT_OK;
 }
 
@@ -983,6 +1031,27 @@ int smcrt_run(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* c
   }
   if (rec)
     HIPCHK(hipMemcpy(io->records, s->d_records, sizeof(smcrt_photon_record) * cfg->n_photons, hipMemcpyDeviceToHost));
+  return SMCRT_OK;
+}
+
+int smcrt_scene_set_timing(smcrt_scene* s, int32_t enable) {
+  if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
+  std::lock_guard<std::mutex> g(s->mu);
+  s->timing = enable != 0;
+  return SMCRT_OK;
+}
+
+int smcrt_scene_kernel_times(smcrt_scene* s, smcrt_kernel_times* out) {
+  if (!s || !out) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(harvest_times(s));
+  out->transport_ms = s->t_transport;
+  out->deposit_ms = s->t_deposit;
+  out->launches = s->t_launches;
+  out->reserved = 0;
+  s->t_transport = s->t_deposit = 0.0;
+  s->t_launches = 0;
   return SMCRT_OK;
 }
 

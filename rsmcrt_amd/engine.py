@@ -50,6 +50,8 @@ def load_library(path: str = LIB_PATH):
         L.smcrt_run.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.RunConfig), C.POINTER(abi.Tallies)]
         L.smcrt_run_device.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.RunConfig),
                                        C.POINTER(abi.DeviceTallies), C.c_void_p]
+        L.smcrt_scene_set_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.smcrt_scene_kernel_times.argtypes = [C.c_void_p, C.POINTER(abi.KernelTimes)]
         L.smcrt_normalise_fluence.argtypes = [C.POINTER(C.c_float), C.POINTER(abi.Grid), C.c_uint64]
         if L.smcrt_abi_version() != abi.SMCRT_ABI_VERSION:
             raise SmcrtError("libsmcrt.so ABI version mismatch")
@@ -123,3 +125,13 @@ class Engine:
         """Asynchronous launch into caller-owned device buffers on `stream` (hipStream_t)."""
         _check(load_library().smcrt_run_device(self._h, C.byref(source), C.byref(cfg), C.byref(dev),
                                                C.c_void_p(stream)))
+
+    def set_timing(self, enable: bool = True):
+        """Record HIP events around each kernel group of later launches."""
+        _check(load_library().smcrt_scene_set_timing(self._h, 1 if enable else 0))
+
+    def kernel_times(self) -> dict:
+        """Device ms per kernel group since the previous call (waits for those launches)."""
+        t = abi.KernelTimes()
+        _check(load_library().smcrt_scene_kernel_times(self._h, C.byref(t)))
+        return {"transport_ms": t.transport_ms, "deposit_ms": t.deposit_ms, "launches": t.launches}

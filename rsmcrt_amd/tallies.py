@@ -49,8 +49,17 @@ class Result:
     def counter(self, name: str) -> int:
         return int(self.counters[abi.CTR[name]])
 
-    def counters_dict(self):
-        return {n: int(v) for n, v in zip(abi.COUNTER_NAMES, self.counters)}
+    def counters_dict(self, engine: bool = False):
+        """Counter name -> value; engine diagnostics (abi.ENGINE_COUNTERS) only if `engine`."""
+        return {n: int(v) for n, v in zip(abi.COUNTER_NAMES, self.counters)
+                if engine or n not in abi.ENGINE_COUNTERS}
+
+    def merge(self, other: "Result") -> "Result":
+        """Add another Result of the same grid/detectors (disjoint photon ranges)."""
+        for f in ("jmean", "absorb", "emission", "det_bins", "nscatt", "moments", "counters"):
+            getattr(self, f)[...] += getattr(other, f)
+        self.n_photons += other.n_photons
+        return self
 
     def detector(self, i: int) -> np.ndarray:
         off = sum(self.det_sizes[:i])

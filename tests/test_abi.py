@@ -65,6 +65,7 @@ STRUCTS = {
     "smcrt_photon_record": (abi.PhotonRecord, ["pos", "weight", "cell", "draws", "status"]),
     "smcrt_tallies": (abi.Tallies, ["jmean", "jmean_f64", "det_bins", "counters", "records"]),
     "smcrt_device_tallies": (abi.DeviceTallies, ["jmean", "det_bins", "records"]),
+    "smcrt_kernel_times": (abi.KernelTimes, ["transport_ms", "deposit_ms", "launches"]),
 }
 
 

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
-ARGS=${PROF_ARGS:-"--no-cpu --steps 3 --warmup 1"}
+ARGS=${PROF_ARGS:-"--no-cpu --steps 3 --warmup 2"}
 fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 134 ] || [ "$1" -eq 139 ]; }
 run() {  # name, rocprof args...
   local name=$1; shift
