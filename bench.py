@@ -139,7 +139,7 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
-    from rsmcrt_amd import abi
+    from rsmcrt_amd import abi, shard
     from rsmcrt_amd.engine import Engine
 
     sc, g, src = workload(args.grid)
@@ -160,7 +160,7 @@ def main():
     B = args.batch
 
     def step(s):
-        cfg = Engine.config(B, seed=args.seed, flags=run_flags, first_photon=(s * world + rank) * B)
+        cfg = Engine.config(B, seed=args.seed, flags=run_flags, first_photon=shard.first_photon(s, rank, world, B))
         eng.run_device(src, cfg, dt_, stream.cuda_stream)
 
     for s in range(args.warmup):
@@ -178,8 +178,7 @@ def main():
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
     if world > 1:
-        for t in (jmean, absorb, nscatt, counters):
-            dist.all_reduce(t)
+        shard.reduce_tallies((jmean, absorb, nscatt, counters), dist)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:

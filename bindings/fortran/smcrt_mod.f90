@@ -69,6 +69,17 @@ module smcrt_mod
         type(c_ptr) :: counters = c_null_ptr, records = c_null_ptr
     end type smcrt_tallies
 
+    type, bind(C) :: smcrt_device_tallies
+        type(c_ptr) :: jmean = c_null_ptr, absorb = c_null_ptr, emission = c_null_ptr
+        type(c_ptr) :: det_bins = c_null_ptr, nscatt = c_null_ptr, moments = c_null_ptr
+        type(c_ptr) :: counters = c_null_ptr, records = c_null_ptr
+    end type smcrt_device_tallies
+
+    type, bind(C) :: smcrt_kernel_times
+        real(c_double)     :: transport_ms = 0._c_double, deposit_ms = 0._c_double
+        integer(c_int64_t) :: launches = 0, reserved = 0
+    end type smcrt_kernel_times
+
     interface
         integer(c_int) function smcrt_abi_version() bind(C, name="smcrt_abi_version")
             import :: c_int
@@ -122,6 +133,27 @@ module smcrt_mod
             type(smcrt_run_config), intent(in) :: cfg
             type(smcrt_tallies), intent(inout) :: io
         end function smcrt_run
+
+        integer(c_int) function smcrt_run_device(scene, src, cfg, dev, stream) bind(C, name="smcrt_run_device")
+            import :: c_int, c_ptr, smcrt_source, smcrt_run_config, smcrt_device_tallies
+            type(c_ptr), value                 :: scene
+            type(smcrt_source), intent(in)     :: src
+            type(smcrt_run_config), intent(in) :: cfg
+            type(smcrt_device_tallies), intent(inout) :: dev
+            type(c_ptr), value                 :: stream
+        end function smcrt_run_device
+
+        integer(c_int) function smcrt_scene_set_timing(scene, enable) bind(C, name="smcrt_scene_set_timing")
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value        :: scene
+            integer(c_int32_t), value :: enable
+        end function smcrt_scene_set_timing
+
+        integer(c_int) function smcrt_scene_kernel_times(scene, times) bind(C, name="smcrt_scene_kernel_times")
+            import :: c_int, c_ptr, smcrt_kernel_times
+            type(c_ptr), value                    :: scene
+            type(smcrt_kernel_times), intent(out) :: times
+        end function smcrt_scene_kernel_times
 
         integer(c_int) function smcrt_normalise_fluence(grid_data, grid, nphotons) &
                 bind(C, name="smcrt_normalise_fluence")

@@ -18,3 +18,10 @@ def kats():
     import json
     with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def lib_path():
+    """Path of the in-tree HIP engine library, built for gfx950 if stale (no GPU needed)."""
+    from rsmcrt_amd import build as B
+    return B.build()

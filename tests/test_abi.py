@@ -16,11 +16,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "smcrt.h")
 
 
-@pytest.fixture(scope="module")
-def lib_path():
-    return B.build()
-
-
 def header_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
