@@ -114,7 +114,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=4_000_000, help="photons per step per GPU")
+    ap.add_argument("--batch", type=int, default=16_000_000, help="photons per step per GPU")
     ap.add_argument("--grid", type=int, default=128)
     ap.add_argument("--seed", type=int, default=123456789)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

@@ -47,17 +47,24 @@ __device__ __forceinline__ V3 eval_query(const Lane& L) {
   }
 }
 
+#ifdef SMCRT_DIAG
+// Diagnostic build only (-DSMCRT_DIAG): lane-state occupancy per scheduler trip.
+// [0..31] lane-trips by state at the trip head (+32 if a segment is active), [64] trips,
+// [65] trips running the DDA phase, [66] EVAL, [67] P7 events.
+__device__ unsigned long long g_diag[72];
+#endif
+
 template <bool LDS_FACES>
 __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
                                                         const ProgOp* __restrict__ prog,
                                                         const smcrt_detector* __restrict__ dets,
-                                                        const int64_t* __restrict__ det_off) {
+                                                        const int64_t* __restrict__ det_off,
+                                                        const KCold* __restrict__ C) {
   __shared__ LaneShared shm;
   LaneShared* sh = &shm;
   const double eps = 1e-8;  // inttau2.f90:56
   const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
   const bool survival = (K.flags & SMCRT_FLAG_SURVIVAL_BIAS) != 0;
-  const bool rec_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) && K.records;
   const int lane_id = threadIdx.x & 63;
 
   extern __shared__ double sh_dyn[];  // [props (4 doubles per top-level SDF) | faces]
@@ -111,10 +118,11 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
       while (need) {
         if (chunk_left == 0) {
           unsigned long long base = 0;
-          if (lane_id == 0) base = atomicAdd(K.queue, (unsigned long long)SMCRT_FETCH_CHUNK);
+          if (lane_id == 0) base = atomicAdd(C->queue, (unsigned long long)SMCRT_FETCH_CHUNK);
           chunk_base = __shfl(base, 0, 64);
-          chunk_left = (chunk_base < K.n_photons)
-                           ? (uint32_t)((K.n_photons - chunk_base) < SMCRT_FETCH_CHUNK ? (K.n_photons - chunk_base)
+          const uint64_t n_photons = C->n_photons;
+          chunk_left = (chunk_base < n_photons)
+                           ? (uint32_t)((n_photons - chunk_base) < SMCRT_FETCH_CHUNK ? (n_photons - chunk_base)
                                                                                        : SMCRT_FETCH_CHUNK)
                            : 0u;
           if (chunk_left == 0) {  // queue exhausted
@@ -126,7 +134,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         const uint32_t take = n < chunk_left ? n : chunk_left;
         const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
         if (L.st == ST_FETCH && rank < take) {
-          L.rng.init(K.first_photon + chunk_base + rank);
+          L.rng.init(C->first_photon + chunk_base + rank);
           L.st = ST_EMIT;
         }
         chunk_base += take;
@@ -136,20 +144,20 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
       if (__ballot(L.st != ST_IDLE) == 0) break;
     }
 
-    // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
-    if (__ballot(L.seg)) {  // wave-uniform, so deposit records can be wave-compacted
-#pragma unroll
-      for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {
-        bool dep = false;
-        uint32_t vox = 0;
-        double val = 0.0;
-        if (L.seg) dda_step(K, L, xf, yf, zf, dep, vox, val);
-        w_dep += __popcll(__ballot(dep));
-        if (binned) emit_deposits(K, W, dep, vox, val, overflow);
-        else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
+#ifdef SMCRT_DIAG
+    {
+      const uint32_t cls = (L.seg ? 32u : 0u) + (L.st & 31u);
+      for (uint32_t c = 0; c < 64; ++c) {  // wave-uniform loop: count lanes per class
+        const uint32_t n = __popcll(__ballot(cls == c));
+        if (n && lane_id == 0) atomicAdd(&g_diag[c], (unsigned long long)n);
+      }
+      if (lane_id == 0) {
+        atomicAdd(&g_diag[64], 1ull);
+        if (__ballot(L.seg)) atomicAdd(&g_diag[65], 1ull);
+        if (__ballot(!L.seg && L.pend)) atomicAdd(&g_diag[66], 1ull);
       }
     }
-
+#endif
     // ---- EVAL phase: the SDF array at the lane's query point ----------------------------
     const bool have = !L.seg && L.pend;
     EvalOut R;
@@ -315,6 +323,22 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
       }
     }
 
+    // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
+    // Placed after the program points that start segments (P3, P4) and before the ones that
+    // consume them (P5), so a short segment is started, walked and finished in one trip.
+    if (__ballot(L.seg)) {  // wave-uniform, so deposit records can be wave-compacted
+#pragma unroll
+      for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {
+        bool dep = false;
+        uint32_t vox = 0;
+        double val = 0.0;
+        if (L.seg) dda_step(K, L, xf, yf, zf, dep, vox, val);
+        w_dep += __popcll(__ballot(dep));
+        if (binned) emit_deposits(K, W, dep, vox, val, overflow);
+        else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
+      }
+    }
+
     // ---- P5: after a deposit segment: detectors and the next program point -------------
     bool rec = false;
     V3 rec_start = v3(0.0, 0.0, 0.0);
@@ -342,7 +366,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         L.st = ST_G0; L.pend = true;
       }
     }
-    if (K.n_dets && rec) LCTR(LC_HITS) += record_hits(K, dets, det_off, rec_start, L.dir, rec_sep, L.layer, L.weight);
+    if (K.n_dets && rec) LCTR(LC_HITS) += record_hits(K, C->det_bins, dets, det_off, rec_start, L.dir, rec_sep, L.layer, L.weight);
 
     // ---- P6: tauint2 write-back checks, :341-362 -----------------------------------------
     if (!L.seg && L.st == ST_T2END) {
@@ -361,6 +385,9 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
       const uint64_t busy = __ballot(L.st != ST_IDLE && L.st != ST_FETCH);
       const uint32_t nev = __popcll(evm);
       if (nev && (nev >= SMCRT_EVENT_LANES || evm == busy)) {
+#ifdef SMCRT_DIAG
+        if (lane_id == 0) atomicAdd(&g_diag[67], 1ull);
+#endif
         if (L.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2036-2065 / 2126-2170
           if (L.tflag || L.fault) {
             L.st = ST_DONE;
@@ -373,7 +400,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             if (survival) {
               const double w_abs = L.weight * (1.0 - pr.albedo);
               L.weight = L.weight - w_abs;
-              add_cell(K, K.absorb, L, w_abs);
+              add_cell(K, C->absorb, L, w_abs);
               sc = true;
               if (L.weight < 0.01) {
                 if (ran < 0.1) L.weight = L.weight / 0.1;
@@ -383,7 +410,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
               sc = true;
             } else {
               L.tflag = true; LU(LU_STATUS) = 1; LCTR(LC_ABSORBED)++;
-              if (!test_kernel) add_cell(K, K.absorb, L, 1.0);  // recordWeight(packet, 1.0)
+              if (!test_kernel) add_cell(K, C->absorb, L, 1.0);  // recordWeight(packet, 1.0)
             }
             if (sc) {
               scatter(K, L, pr.hgg);
@@ -391,9 +418,10 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
               LCTR(LC_SCATTERS)++;
               if (test_kernel && !survival) {
                 if (st >= 1 && st <= 4) {
-                  if (K.moments) {
-                    double* m = K.moments + 3 * (st - 1);
-                    double* m2 = K.moments + 12 + 3 * (st - 1);
+                  double* const moments = C->moments;
+                  if (moments) {
+                    double* m = moments + 3 * (st - 1);
+                    double* m2 = moments + 12 + 3 * (st - 1);
                     atomic_add_nr(m + 0, L.pos.x); atomic_add_nr(m + 1, L.pos.y); atomic_add_nr(m + 2, L.pos.z);
                     atomic_add_nr(m2 + 0, L.pos.x * L.pos.x);
                     atomic_add_nr(m2 + 1, L.pos.y * L.pos.y);
@@ -426,15 +454,15 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           L.fault = false; L.layer = 0;
           LU(LU_STATUS) = 0; LU(LU_NSCATT) = 0; LU(LU_INTER) = 0; LU(LU_BOUNCES) = 0;
           L.xcell = L.ycell = L.zcell = 0;
-          emit(K, L);
+          emit(K, C, L);
           if (!test_kernel) {
             int64_t tries = 0;
             while (cell_out(K, L)) {
               if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
               LCTR(LC_RETRIES)++;
-              emit(K, L);
+              emit(K, C, L);
             }
-            if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, K.emission, L, 1.0);
+            if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, C->emission, L, 1.0);
           }
           if (L.fault) L.st = ST_DONE;
           else { L.st = ST_LAYER; L.pend = true; }
@@ -444,9 +472,10 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           else if (LU(LU_STATUS) == 0) { LU(LU_STATUS) = 2; LCTR(LC_ESCAPED)++; }
           LCTR(LC_PHOTONS)++;
           LCTR(LC_DRAWS) += L.rng.draws;
-          if (rec_on) {
+          smcrt_photon_record* const records = C->records;
+          if ((K.flags & SMCRT_FLAG_RECORD_PHOTONS) && records) {
             const uint64_t pid = ((uint64_t)L.rng.pid_hi << 32) | L.rng.pid_lo;
-            smcrt_photon_record* r = K.records + (pid - K.first_photon);
+            smcrt_photon_record* r = records + (pid - C->first_photon);
             r->pos[0] = L.pos.x; r->pos[1] = L.pos.y; r->pos[2] = L.pos.z;
             r->dir[0] = L.dir.x; r->dir[1] = L.dir.y; r->dir[2] = L.dir.z;
             r->weight = L.weight;
@@ -474,7 +503,8 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   if (binned) close_log(K, W, overflow);
 
   // ---- per-wave counter reduction ------------------------------------------------------
-  if (K.counters) {
+  unsigned long long* const counters = C->counters;
+  if (counters) {
     uint32_t c[SMCRT_NCOUNTERS];
     c[SMCRT_CTR_PHOTONS] = LCTR(LC_PHOTONS);
     c[SMCRT_CTR_EMIT_RETRIES] = LCTR(LC_RETRIES);
@@ -495,12 +525,13 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
 #pragma unroll
     for (int i = 0; i < SMCRT_NCOUNTERS; ++i) {
       const uint32_t s = wave_sum_u32(c[i]);
-      if (lane_id == 0 && s) atomicAdd(K.counters + i, (unsigned long long)s);
+      if (lane_id == 0 && s) atomicAdd(counters + i, (unsigned long long)s);
     }
   }
-  if (K.nscatt) {  // nscatt = number of scatters (kernelsMod.f90:1966)
+  double* const nscatt = C->nscatt;
+  if (nscatt) {  // nscatt = number of scatters (kernelsMod.f90:1966)
     const uint32_t s = wave_sum_u32(LCTR(LC_SCATTERS));
-    if (lane_id == 0 && s) atomic_add_nr(K.nscatt, (double)s);
+    if (lane_id == 0 && s) atomic_add_nr(nscatt, (double)s);
   }
 }
 
@@ -551,6 +582,8 @@ struct smcrt_scene {
   smcrt_detector* d_dets = nullptr;
   int64_t* d_det_off = nullptr;
   unsigned long long* d_queue = nullptr;
+  KCold* d_cold = nullptr;  // COLD_SLOTS launch slots (ring, stream-ordered writes)
+  uint64_t cold_seq = 0;
   // tallies owned by the scene for the synchronous smcrt_run
   double* d_grids = nullptr;  // jmean | absorb | emission
   double* d_small = nullptr;  // det bins | nscatt | moments(24)
@@ -574,6 +607,7 @@ struct smcrt_scene {
   Piece* d_pieces = nullptr;
   uint64_t pool_chunks = 0, max_pieces = 0;
   double rpp_est = 1024.0;           // deposit records per photon, refined from past launches
+  bool rpp_measured = false;
   uint32_t* h_ctl = nullptr;         // pinned copy of dep_ctl of the last launch
   hipEvent_t ctl_ev = nullptr;
   bool ctl_pending = false;
@@ -588,7 +622,15 @@ struct smcrt_scene {
   std::mutex mu;
 };
 
-constexpr size_t MAX_TIMED = 256;  // launches kept before the events are harvested
+constexpr size_t MAX_TIMED = 256;
+constexpr uint64_t COLD_SLOTS = 64;
+// Record pool: record indices in the bin kernels are 32-bit, so at most 2^32 - 2^28 records
+// (30 GiB, plus the same again for the sorted copy) per launch; a launch that would need more
+// is split into sub-batches. POOL_SLACK covers the spread of records per photon between
+// batches; a launch that still overflows folds the excess with atomics (exact, slower).
+constexpr uint64_t MAX_POOL_RECORDS = (1ull << 32) - (1ull << 28);
+constexpr double POOL_SLACK = 1.15;
+constexpr uint64_t CALIB_PHOTONS = 1ull << 18;  // first binned launch of a scene above this size  // in-flight launches per scene before a KCold slot is reused  // launches kept before the events are harvested
 
 // Fold the recorded event triples into the sums (waits for them).
 static hipError_t harvest_times(smcrt_scene* s) {
@@ -635,7 +677,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off,
-                  s->d_queue, s->d_grids, s->d_small, s->d_counters, s->d_records,
+                  s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_dep_ctl, s->d_tile_count,
                   s->d_tile_start, s->d_bin_counts, s->d_pieces};
   if (s->ctl_ev) (void)hipEventDestroy(s->ctl_ev);
@@ -736,6 +778,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
       (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, 1)) ||
+      (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
     return cleanup_fail(st);
@@ -802,10 +845,22 @@ int smcrt_scene_set_optprops(smcrt_scene* s, int32_t i, double mus, double mua, 
   return SMCRT_OK;
 }
 
+// Refine the records-per-photon estimate from the last binned launch, if it has landed.
+static void refine_rpp(smcrt_scene* s) {
+  if (s->ctl_pending && hipEventQuery(s->ctl_ev) == hipSuccess) {
+    s->ctl_pending = false;
+    if (s->h_ctl[4] > 0) {
+      const double rpp = (double)(s->h_ctl[3] + s->h_ctl[1]) / (double)s->h_ctl[4];
+      s->rpp_est = std::max(1.0, rpp);
+      s->rpp_measured = true;
+    }
+  }
+}
+
 // Records the record pool must hold for one launch of n photons.
 static uint64_t pool_records_for(const smcrt_scene* s, uint64_t n) {
-  const double want = (double)n * s->rpp_est * 1.25 + (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
-  return (uint64_t)std::min(want, 2147483648.0);
+  const double want = (double)n * s->rpp_est * POOL_SLACK + (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
+  return (uint64_t)std::min(want, (double)MAX_POOL_RECORDS);
 }
 
 // Make sure the record pool holds `records` (grow only). Returns false if it cannot.
@@ -833,8 +888,11 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   return true;
 }
 
-static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
+static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t stream) {
   HIPCHK(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), stream));
+  // this launch's cold parameters: a ring slot, written in stream order before the kernel
+  KCold* C = s->d_cold + (s->cold_seq++ % COLD_SLOTS);
+  HIPCHK(hipMemcpyAsync(C, &Ch, sizeof(KCold), hipMemcpyHostToDevice, stream));
   const bool binned = K.rec_pool != nullptr;
   if (binned) {
     HIPCHK(hipMemsetAsync(s->d_dep_ctl, 0, 4 * sizeof(uint32_t), stream));
@@ -851,15 +909,15 @@ static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
     ev = &s->tev[3 * s->tev_used++];
     HIPCHK(hipEventRecord(ev[0], stream));
   }
-  const uint64_t waves_needed = (K.n_photons + 63) / 64;
+  const uint64_t waves_needed = (Ch.n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
   const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
   if (s->lds_faces)
     hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K, K.nodes, K.prog,
-                       K.dets, K.det_off);
+                       K.dets, K.det_off, (const KCold*)C);
   else
     hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K, K.nodes, K.prog, K.dets,
-                       K.det_off);
+                       K.det_off, (const KCold*)C);
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
   if (binned) {
@@ -883,6 +941,22 @@ static int launch_one(smcrt_scene* s, KParams K, hipStream_t stream) {
     s->ctl_pending = true;
   }
   if (ev) HIPCHK(hipEventRecord(ev[2], stream));
+#ifdef SMCRT_DIAG
+  {
+    unsigned long long h[72];
+    HIPCHK(hipStreamSynchronize(stream));
+    HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)));
+    unsigned long long lt = 0;
+    for (int i = 0; i < 64; ++i) lt += h[i];
+    std::fprintf(stderr, "[diag] trips %llu dda %llu eval %llu p7 %llu | lane-trips %llu:", h[64], h[65], h[66],
+                 h[67], lt);
+    for (int i = 0; i < 64; ++i)
+      if (h[i]) std::fprintf(stderr, " %s%d=%.3f", i >= 32 ? "seg:" : "", i & 31, (double)h[i] / (double)lt);
+    std::fprintf(stderr, "\n");
+    std::memset(h, 0, sizeof(h));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), h, sizeof(h)));
+  }
+#endif
   return SMCRT_OK;
 }
 
@@ -906,53 +980,53 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.nx = s->grid.nx; K.ny = s->grid.ny; K.nz = s->grid.nz;
   K.xmax = s->grid.xmax; K.ymax = s->grid.ymax; K.zmax = s->grid.zmax;
   K.flags = cfg->flags;
-  K.src = *src;
-  K.seed = cfg->seed;
+  KCold Ch;
+  Ch.src = *src;
   K.key0 = (uint32_t)cfg->seed;
   K.key1 = (uint32_t)(cfg->seed >> 32);
-  K.jmean = dt.jmean; K.absorb = dt.absorb; K.emission = dt.emission;
-  K.det_bins = dt.det_bins; K.nscatt = dt.nscatt; K.moments = dt.moments;
-  K.counters = (unsigned long long*)dt.counters;
-  K.queue = s->d_queue;
+  K.jmean = dt.jmean; Ch.absorb = dt.absorb; Ch.emission = dt.emission;
+  Ch.det_bins = dt.det_bins; Ch.nscatt = dt.nscatt; Ch.moments = dt.moments;
+  Ch.counters = (unsigned long long*)dt.counters;
+  Ch.queue = s->d_queue;
   K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
 
-  // refine the records-per-photon estimate from the last binned launch, if it has landed
-  if (s->ctl_pending && hipEventQuery(s->ctl_ev) == hipSuccess) {
-    s->ctl_pending = false;
-    if (s->h_ctl[4] > 0) {
-      const double rpp = (double)(s->h_ctl[3] + s->h_ctl[1]) / (double)s->h_ctl[4];
-      s->rpp_est = std::max(1.0, rpp);
-    }
-  }
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
   const bool binned = dt.jmean && (cfg->flags & SMCRT_FLAG_PATHLENGTH) && !(cfg->flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
                       s->n_tiles > 0 && !s->force_atomic;
-  uint64_t batch = cfg->n_photons;
-  if (binned) {
-    uint64_t want = pool_records_for(s, cfg->n_photons);
-    if (!ensure_pool(s, want)) {
-      (void)ensure_pool(s, want / 4);  // smaller pool, more batches
+  for (uint64_t done = 0; done < cfg->n_photons;) {
+    refine_rpp(s);
+    uint64_t n = cfg->n_photons - done;
+    K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
+    bool calibrate = false;
+    if (binned) {
+      // records per photon are scene-dependent: the scene's first large launch starts with a
+      // small calibration batch whose count is waited for once, then batches are sized to it
+      if (!s->rpp_measured && n > CALIB_PHOTONS) { n = CALIB_PHOTONS; calibrate = true; }
+      const uint64_t want = pool_records_for(s, n);
+      if (!ensure_pool(s, want)) (void)ensure_pool(s, want / 4);  // smaller pool, more batches
+      if (s->pool_chunks) {
+        const double usable = (double)(s->pool_chunks * CHUNK_RECORDS) - (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
+        n = std::min<uint64_t>(n, (uint64_t)std::max(65536.0, usable / (s->rpp_est * POOL_SLACK)));
+        // (taken after ensure_pool: it may have reallocated the pool)
+        K.rec_pool = s->d_pool;
+        K.chunk_fill = s->d_chunk_fill;
+        K.dep_ctl = s->d_dep_ctl;
+        K.n_chunks = (uint32_t)s->pool_chunks;
+      }
     }
-    if (s->pool_chunks) {
-      const double usable = (double)(s->pool_chunks * CHUNK_RECORDS) - (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
-      batch = (uint64_t)std::max(65536.0, usable / (s->rpp_est * 1.25));
-      // (taken after ensure_pool: it may have reallocated the pool)
-      K.rec_pool = s->d_pool;
-      K.chunk_fill = s->d_chunk_fill;
-      K.dep_ctl = s->d_dep_ctl;
-      K.n_chunks = (uint32_t)s->pool_chunks;
-    }
-  }
-  for (uint64_t done = 0; done < cfg->n_photons; done += batch) {
-    const uint64_t n = std::min<uint64_t>(batch, cfg->n_photons - done);
-    K.n_photons = n;
-    K.first_photon = cfg->first_photon + done;
-    K.records = dt.records ? dt.records + done : nullptr;
+    Ch.n_photons = n;
+    Ch.first_photon = cfg->first_photon + done;
+    Ch.records = dt.records ? dt.records + done : nullptr;
     if (K.rec_pool) s->h_ctl[4] = 0;
-    int st = launch_one(s, K, stream);
+    int st = launch_one(s, K, Ch, stream);
     if (st) return st;
     if (K.rec_pool) s->h_ctl[4] = (uint32_t)std::min<uint64_t>(n, 0xFFFFFFFFull);
+    if (calibrate && K.rec_pool) {
+      HIPCHK(hipEventSynchronize(s->ctl_ev));
+      refine_rpp(s);
+    }
+    done += n;
   }
   return SMCRT_OK;
 }

@@ -53,6 +53,22 @@ struct TopProps {
   double kappa, albedo, hgg, n;
 };
 
+// Launch parameters read only at rare program points (fetch of a new photon chunk,
+// emission, interactions, completion). They live in device memory behind a pointer and are
+// loaded where used, so they do not occupy scalar registers for the whole kernel.
+struct KCold {
+  smcrt_source src;
+  uint64_t n_photons, first_photon;
+  double* absorb;
+  double* emission;
+  double* det_bins;
+  double* nscatt;
+  double* moments;
+  unsigned long long* counters;
+  smcrt_photon_record* records;
+  unsigned long long* queue;  // photon work-queue head (zeroed before launch)
+};
+
 struct KParams {
   const smcrt_sdf_node* __restrict__ nodes;
   const ProgOp* __restrict__ prog;
@@ -68,18 +84,8 @@ struct KParams {
   double xmax, ymax, zmax;
   // exact reciprocal of 2*max when that is a power of two (else 0): n*p/(2*max) == n*p*inv
   double inv2x, inv2y, inv2z;
-  smcrt_source src;
-  uint64_t n_photons, first_photon, seed;
   uint32_t key0, key1;  // Philox key = seed words
   double* jmean;
-  double* absorb;
-  double* emission;
-  double* det_bins;
-  double* nscatt;
-  double* moments;
-  unsigned long long* counters;
-  smcrt_photon_record* records;
-  unsigned long long* queue;  // photon work-queue head (zeroed before launch)
   // binned jmean deposition (deposit.h): record log in chunks
   unsigned long long* rec_pool;  // CHUNK_RECORDS records per chunk; NULL -> fp64 atomics into jmean
   uint32_t* chunk_fill;          // records in each used chunk
@@ -138,7 +144,8 @@ __device__ __forceinline__ int64_t f_int(double x) {
 
 // record_hit on every detector for one path segment (detector_base.f90:137-235,
 // detectors.f90:147-469). Returns the number of bin increments.
-__device__ __forceinline__ uint32_t record_hits(const KParams& K, const smcrt_detector* __restrict__ dets,
+__device__ __forceinline__ uint32_t record_hits(const KParams& K, double* det_bins,
+                                                const smcrt_detector* __restrict__ dets,
                                                 const int64_t* __restrict__ det_off, V3 start, V3 dir,
                                                 double pointSep, int32_t layer, double weight) {
   uint32_t hits = 0;
@@ -147,7 +154,7 @@ __device__ __forceinline__ uint32_t record_hits(const KParams& K, const smcrt_de
     const smcrt_detector* D = dets + di;
     const V3 dpos = v3(D->pos[0], D->pos[1], D->pos[2]);
     const V3 ddir = v3(D->dir[0], D->dir[1], D->dir[2]);
-    double* data = K.det_bins ? K.det_bins + det_off[di] : nullptr;
+    double* data = det_bins ? det_bins + det_off[di] : nullptr;
     double t;
     int64_t bin = -1;
     double w = weight;
@@ -308,8 +315,8 @@ __device__ __forceinline__ void add_cell(const KParams& K, double* g, Lane& L, d
 }
 
 // emit: point photon.f90:311-359 / uniform :566-649 / pencil :652-710
-__device__ __forceinline__ void emit(const KParams& K, Lane& L) {
-  const smcrt_source& s = K.src;
+__device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__ C, Lane& L) {
+  const smcrt_source& s = C->src;
   if (s.kind == SMCRT_SRC_POINT) {
     L.pos = v3(s.pos[0], s.pos[1], s.pos[2]);
     const double phi = L.rng.next(K.key0, K.key1) * 6.283185307179586;
