@@ -54,7 +54,7 @@ __device__ __forceinline__ V3 eval_query(const Lane& L) {
 __device__ unsigned long long g_diag[72];
 #endif
 
-template <bool LDS_FACES>
+template <bool LDS_FACES, bool P2>
 __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
                                                         const ProgOp* __restrict__ prog,
                                                         const smcrt_detector* __restrict__ dets,
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             else { L.d = (L.tau - L.taurun) / kap; L.pos = L.pos - smul(L.d, L.dir); }
           }
           L.st = ST_H2;
-          start_segment(K, L, sh, oldpos, L.d);
+          start_segment<P2>(K, L, sh, oldpos, L.d);
           break;
         }
         case ST_H3:  // :133-152
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           if (n1 != n2) { L.st = ST_F0; L.pend = true; break; }
           L.layer = L.new_layer;  // equal n: cross, :318-328
           L.st = ST_X1;
-          start_segment(K, L, sh, L.pos, L.d);
+          start_segment<P2>(K, L, sh, L.pos, L.d);
           break;
         }
         case ST_F0:  // ds(new), ds(old) at pos (kept in sd/slen: no segment is active)
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             L.dir = smul(eta, L.dir) + smul(eta * c1 - c2, Nt);
             L.layer = L.new_layer;
             L.st = ST_X1;
-            start_segment(K, L, sh, L.pos, L.d);
+            start_segment<P2>(K, L, sh, L.pos, L.d);
           }
           break;
         }
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           L.pos = L.pos + smul(L.d, L.dir);
           L.st = ST_B0;
         }
-        start_segment(K, L, sh, oldpos, L.d);
+        start_segment<P2>(K, L, sh, oldpos, L.d);
       }
     }
 
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         bool dep = false;
         uint32_t vox = 0;
         double val = 0.0;
-        if (L.seg) dda_step(K, L, xf, yf, zf, dep, vox, val);
+        if (L.seg) dda_step<P2>(K, L, xf, yf, zf, dep, vox, val);
         w_dep += __popcll(__ballot(dep));
         if (binned) emit_deposits(K, W, dep, vox, val, overflow);
         else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
@@ -454,13 +454,13 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           L.fault = false; L.layer = 0;
           LU(LU_STATUS) = 0; LU(LU_NSCATT) = 0; LU(LU_INTER) = 0; LU(LU_BOUNCES) = 0;
           L.xcell = L.ycell = L.zcell = 0;
-          emit(K, C, L);
+          emit<P2>(K, C, L);
           if (!test_kernel) {
             int64_t tries = 0;
             while (cell_out(K, L)) {
               if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
               LCTR(LC_RETRIES)++;
-              emit(K, C, L);
+              emit<P2>(K, C, L);
             }
             if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, C->emission, L, 1.0);
           }
@@ -577,6 +577,7 @@ struct smcrt_scene {
   ProgOp* d_prog = nullptr;
   int n_prog = 0;
   double inv2[3] = {0.0, 0.0, 0.0};
+  bool pow2 = false;  // all three inv2 exact: transport_kernel<*, true>
   TopProps* d_props = nullptr;
   double* d_faces = nullptr;
   smcrt_detector* d_dets = nullptr;
@@ -647,6 +648,12 @@ static hipError_t harvest_times(smcrt_scene* s) {
   return hipSuccess;
 }
 
+// The transport kernel instantiation for this scene (LDS faces? power-of-two grid?).
+static const void* transport_fn(const smcrt_scene* s) {
+  if (s->lds_faces) return s->pow2 ? (const void*)transport_kernel<true, true> : (const void*)transport_kernel<true, false>;
+  return s->pow2 ? (const void*)transport_kernel<false, true> : (const void*)transport_kernel<false, false>;
+}
+
 static TopProps make_props(const smcrt_sdf_node& nd) {
   TopProps p;  // init_mono, opticalProperties.f90:107-125
   p.kappa = nd.mus + nd.mua;
@@ -700,6 +707,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (grid->nx < 1 || grid->ny < 1 || grid->nz < 1 || !(grid->xmax > 0) || !(grid->ymax > 0) ||
       !(grid->zmax > 0))
     return fail(SMCRT_ERR_INVALID_ARG, "grid dimensions must be positive");
+  if ((uint64_t)grid->nx * (uint64_t)grid->ny * (uint64_t)grid->nz >= (1ull << 32))
+    return fail(SMCRT_ERR_UNSUPPORTED, "grids of 2^32 or more voxels are not supported");
   for (int32_t i = 0; i < n_nodes; ++i) {
     const smcrt_sdf_node& nd = nodes[i];
     if (nd.kind < SMCRT_SDF_SPHERE || nd.kind > SMCRT_SDF_MODEL)
@@ -817,9 +826,9 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   int per_cu = 0, cus = 0;
   s->face_bytes = faces.size() * sizeof(double) + sizeof(TopProps) * (size_t)n_top;
   s->lds_faces = s->face_bytes <= 40960;  // stage props + voxel faces in LDS when they fit
-  hipError_t oe = s->lds_faces
-      ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel<true>, 256, s->face_bytes)
-      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, transport_kernel<false>, 256, 0);
+  s->pow2 = s->inv2[0] != 0.0 && s->inv2[1] != 0.0 && s->inv2[2] != 0.0;
+  const void* kfn = transport_fn(s);
+  hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, s->lds_faces ? s->face_bytes : 0);
   if (oe != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   s->grid_blocks = cus * per_cu;
@@ -912,12 +921,15 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
   const uint64_t waves_needed = (Ch.n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
   const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
-  if (s->lds_faces)
-    hipLaunchKernelGGL(transport_kernel<true>, dim3(blocks), dim3(256), s->face_bytes, stream, K, K.nodes, K.prog,
-                       K.dets, K.det_off, (const KCold*)C);
-  else
-    hipLaunchKernelGGL(transport_kernel<false>, dim3(blocks), dim3(256), 0, stream, K, K.nodes, K.prog, K.dets,
-                       K.det_off, (const KCold*)C);
+  {
+    const KCold* Cc = C;
+    const smcrt_sdf_node* a_nodes = K.nodes;
+    const ProgOp* a_prog = K.prog;
+    const smcrt_detector* a_dets = K.dets;
+    const int64_t* a_off = K.det_off;
+    void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&a_dets, (void*)&a_off, (void*)&Cc};
+    HIPCHK(hipLaunchKernel(transport_fn(s), dim3(blocks), dim3(256), args, s->lds_faces ? s->face_bytes : 0, stream));
+  }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
   if (binned) {

@@ -95,16 +95,20 @@ struct KParams {
 
 // ------------------------------------------------------------------ voxels -------
 // update_voxels, inttau2.f90:587-614 (corner coordinates): floor(n*p/(2*max))+1, -1 outside
+// P2: every axis has 2*max a power of two, so the division is an exact multiply (the kernel
+// is instantiated for it; the general case keeps a per-axis uniform branch).
+template <bool P2>
 __device__ __forceinline__ int32_t cell_of(double p, int32_t n, double max, double inv) {
   const double a = (double)n * p;
-  const double f = floor(inv != 0.0 ? a * inv : a / (2.0 * max));
+  const double f = floor(P2 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
   if (!(f >= 0.0 && f < (double)n)) return -1;
   return (int32_t)f + 1;
 }
 // get_voxel_cart, grid.f90:51-78 (centred coordinates)
+template <bool P2>
 __device__ __forceinline__ int32_t vox_of(double p, int32_t n, double max, double inv) {
   const double a = (double)n * (p + max);
-  const double f = floor(inv != 0.0 ? a * inv : a / (2.0 * max));
+  const double f = floor(P2 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
   if (!(f >= 0.0 && f < (double)n)) return -1;
   return (int32_t)f + 1;
 }
@@ -305,8 +309,9 @@ __device__ __forceinline__ bool cell_out(const KParams& K, const Lane& L) {
   return L.xcell < 1 || L.xcell > K.nx || L.ycell < 1 || L.ycell > K.ny || L.zcell < 1 || L.zcell > K.nz;
 }
 
-__device__ __forceinline__ int64_t lin(const KParams& K, int32_t i, int32_t j, int32_t k) {
-  return (int64_t)(i - 1) + (int64_t)K.nx * ((int64_t)(j - 1) + (int64_t)K.ny * (int64_t)(k - 1));
+// Voxel index, x fastest (Fortran order). Grids are limited to < 2^32 voxels (scene_create).
+__device__ __forceinline__ uint32_t lin(const KParams& K, int32_t i, int32_t j, int32_t k) {
+  return (uint32_t)(i - 1) + (uint32_t)K.nx * ((uint32_t)(j - 1) + (uint32_t)K.ny * (uint32_t)(k - 1));
 }
 
 __device__ __forceinline__ void add_cell(const KParams& K, double* g, Lane& L, double w) {
@@ -315,6 +320,7 @@ __device__ __forceinline__ void add_cell(const KParams& K, double* g, Lane& L, d
 }
 
 // emit: point photon.f90:311-359 / uniform :566-649 / pencil :652-710
+template <bool P2>
 __device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__ C, Lane& L) {
   const smcrt_source& s = C->src;
   if (s.kind == SMCRT_SRC_POINT) {
@@ -345,9 +351,9 @@ __device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__
   }
   L.tflag = false;
   L.weight = 1.0;
-  L.xcell = vox_of(L.pos.x, K.nx, K.xmax, K.inv2x);
-  L.ycell = vox_of(L.pos.y, K.ny, K.ymax, K.inv2y);
-  L.zcell = vox_of(L.pos.z, K.nz, K.zmax, K.inv2z);
+  L.xcell = vox_of<P2>(L.pos.x, K.nx, K.xmax, K.inv2x);
+  L.ycell = vox_of<P2>(L.pos.y, K.ny, K.ymax, K.inv2y);
+  L.zcell = vox_of<P2>(L.pos.z, K.nz, K.zmax, K.inv2z);
 }
 
 // scatter, photon.f90:1045-1103
@@ -388,18 +394,19 @@ __device__ __forceinline__ void scatter(const KParams& K, Lane& L, double hgg) {
 // update_grids entry (inttau2.f90:401-415): start a deposit segment from `p` (centred) of
 // length `dlen` along L.dir; the segment itself runs in the DDA phase. Returns true if the
 // lane must wait for the DDA.
+template <bool P2>
 __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneShared* sh, V3 p, double dlen) {
   LCTR(LC_UPD)++;
   V3 old = v3(p.x + K.xmax, p.y + K.ymax, p.z + K.zmax);
-  int32_t ci = cell_of(old.x, K.nx, K.xmax, K.inv2x), cj = cell_of(old.y, K.ny, K.ymax, K.inv2y),
-          ck = cell_of(old.z, K.nz, K.zmax, K.inv2z);
+  int32_t ci = cell_of<P2>(old.x, K.nx, K.xmax, K.inv2x), cj = cell_of<P2>(old.y, K.ny, K.ymax, K.inv2y),
+          ck = cell_of<P2>(old.z, K.nz, K.zmax, K.inv2z);
   L.xcell = ci; L.ycell = cj; L.zcell = ck;
   if (!(K.flags & SMCRT_FLAG_PATHLENGTH)) {  // :446-463
     old.x = old.x + L.dir.x * dlen;
     old.y = old.y + L.dir.y * dlen;
     old.z = old.z + L.dir.z * dlen;
-    ci = cell_of(old.x, K.nx, K.xmax, K.inv2x); cj = cell_of(old.y, K.ny, K.ymax, K.inv2y);
-    ck = cell_of(old.z, K.nz, K.zmax, K.inv2z);
+    ci = cell_of<P2>(old.x, K.nx, K.xmax, K.inv2x); cj = cell_of<P2>(old.y, K.ny, K.ymax, K.inv2y);
+    ck = cell_of<P2>(old.z, K.nz, K.zmax, K.inv2z);
     if (ci == -1 || cj == -1 || ck == -1) L.tflag = true;
     L.xcell = ci; L.ycell = cj; L.zcell = ck;
     return false;
@@ -412,6 +419,7 @@ __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneSha
 
 // One voxel crossing of the pending segment: wall_dist + deposit + update_pos
 // (inttau2.f90:417-441, 467-584). Clears L.seg when the segment ends.
+template <bool P2>
 __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double* __restrict__ xf,
                                          const double* __restrict__ yf, const double* __restrict__ zf,
                                          bool& dep, uint32_t& dep_vox, double& dep_val) {
@@ -419,21 +427,46 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   bool done = false;
   if (++L.dda_it > (uint32_t)MAX_DDA_ITERS) { L.fault = true; L.tflag = true; done = true; }
   if (!done) {
-    double dx = -999.0, dy = -999.0, dz = -999.0;
-    if (dir.x > 0.0) dx = (xf[L.ci] - L.old.x) / dir.x;
-    else if (dir.x < 0.0) dx = (xf[L.ci - 1] - L.old.x) / dir.x;
-    else if (dir.x == 0.0) dx = 100000.0;
-    if (dir.y > 0.0) dy = (yf[L.cj] - L.old.y) / dir.y;
-    else if (dir.y < 0.0) dy = (yf[L.cj - 1] - L.old.y) / dir.y;
-    else if (dir.y == 0.0) dy = 100000.0;
-    if (dir.z > 0.0) dz = (zf[L.ck] - L.old.z) / dir.z;
-    else if (dir.z < 0.0) dz = (zf[L.ck - 1] - L.old.z) / dir.z;
-    else if (dir.z == 0.0) dz = 100000.0;
-    double dcell = dmin(dmin(dx, dy), dz);
+    // wall_dist, :467-521: d_a = (face_a - old_a)/dir_a, dcell = min, ldir_a = (dcell == d_a).
+    // Only the smallest quotient is needed exactly: the three are ranked with hardware
+    // reciprocals (relative error far below the 2^-16 margin required), and the one winner
+    // is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
+    // or negative distances, NaN), all three are divided exactly as the reference does.
+    // Both paths give the reference's dcell and ldir bit for bit.
+    const double nx = (dir.x > 0.0 ? xf[L.ci] : xf[L.ci - 1]) - L.old.x;
+    const double ny = (dir.y > 0.0 ? yf[L.cj] : yf[L.cj - 1]) - L.old.y;
+    const double nz = (dir.z > 0.0 ? zf[L.ck] : zf[L.ck - 1]) - L.old.z;
+    const double ax = dir.x == 0.0 ? 100000.0 : nx * __builtin_amdgcn_rcp(dir.x);
+    const double ay = dir.y == 0.0 ? 100000.0 : ny * __builtin_amdgcn_rcp(dir.y);
+    const double az = dir.z == 0.0 ? 100000.0 : nz * __builtin_amdgcn_rcp(dir.z);
+    const bool mx = ax <= ay && ax <= az, my = !mx && ay <= az;
+    const double amin = mx ? ax : (my ? ay : az);
+    const double arest = mx ? dmin(ay, az) : (my ? dmin(ax, az) : dmin(ax, ay));
+    const bool fast = amin > 0.0 && arest > amin * (1.0 + 0x1.0p-16) && !(dir.x != dir.x) && !(dir.y != dir.y) &&
+                      !(dir.z != dir.z);
+    double dcell;
+    bool lx, ly, lz;
+    if (fast) {
+      const double num = mx ? nx : (my ? ny : nz), den = mx ? dir.x : (my ? dir.y : dir.z);
+      dcell = den == 0.0 ? 100000.0 : num / den;
+      lx = mx; ly = my; lz = !mx && !my;
+    } else {
+      double dx = -999.0, dy = -999.0, dz = -999.0;
+      if (dir.x > 0.0) dx = (xf[L.ci] - L.old.x) / dir.x;
+      else if (dir.x < 0.0) dx = (xf[L.ci - 1] - L.old.x) / dir.x;
+      else if (dir.x == 0.0) dx = 100000.0;
+      if (dir.y > 0.0) dy = (yf[L.cj] - L.old.y) / dir.y;
+      else if (dir.y < 0.0) dy = (yf[L.cj - 1] - L.old.y) / dir.y;
+      else if (dir.y == 0.0) dy = 100000.0;
+      if (dir.z > 0.0) dz = (zf[L.ck] - L.old.z) / dir.z;
+      else if (dir.z < 0.0) dz = (zf[L.ck - 1] - L.old.z) / dir.z;
+      else if (dir.z == 0.0) dz = 100000.0;
+      dcell = dmin(dmin(dx, dy), dz);
+      lx = (dcell == dx); ly = (dcell == dy); lz = (dcell == dz);
+    }
     if (dcell < 0.0) {  // error stop :510-516
       L.fault = true; L.tflag = true; done = true;
     } else {
-      const bool lx = (dcell == dx), ly = (dcell == dy), lz = (dcell == dz);
       const bool last = L.sd + dcell > L.slen;
       if (last) { dcell = L.slen - L.sd; L.sd = L.slen; }
       else L.sd = L.sd + dcell;
@@ -462,9 +495,9 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
         L.old.x = snx ? sx : ax;
         L.old.y = sny ? sy : ay;
         L.old.z = snz ? sz : az;
-        L.ci = cell_of(L.old.x, K.nx, K.xmax, K.inv2x);
-        L.cj = cell_of(L.old.y, K.ny, K.ymax, K.inv2y);
-        L.ck = cell_of(L.old.z, K.nz, K.zmax, K.inv2z);
+        L.ci = cell_of<P2>(L.old.x, K.nx, K.xmax, K.inv2x);
+        L.cj = cell_of<P2>(L.old.y, K.ny, K.ymax, K.inv2y);
+        L.ck = cell_of<P2>(L.old.z, K.nz, K.zmax, K.inv2z);
         if (L.ci == -1 || L.cj == -1 || L.ck == -1) { L.tflag = true; done = true; }
       }
     }
