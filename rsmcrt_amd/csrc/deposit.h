@@ -28,7 +28,11 @@ constexpr uint32_t CHUNK_RECORDS = 16384;  // 128 KiB per chunk
 constexpr uint32_t TILE_SHIFT = 13;        // 8192 voxels per tile: 64 KiB of fp64 in LDS
 constexpr uint32_t TILE_VOXELS = 1u << TILE_SHIFT;
 constexpr uint32_t MAX_TILES = 8192;       // grids up to 2^26 voxels use the binned path
-constexpr uint32_t PIECE_RECORDS = 1u << 18;
+// A reduce piece is one block's share of one tile. Each piece ends with one fp64 atomic per
+// touched voxel of its tile (up to TILE_VOXELS), so pieces are made as large as load balance
+// allows: about REDUCE_PIECES pieces in total, and never smaller than MIN_PIECE_RECORDS.
+constexpr uint32_t MIN_PIECE_RECORDS = 1u << 16;
+constexpr uint32_t REDUCE_PIECES = 2048;
 
 struct Piece {
   uint32_t tile, start, count, pad;
@@ -50,20 +54,40 @@ __device__ __forceinline__ unsigned long long pack_record(uint32_t vox, double v
   return ((unsigned long long)vox << 32) | (unsigned long long)__float_as_uint((float)val);
 }
 
+constexpr uint32_t BIN_BLOCKS_ = 1024;  // == BIN_BLOCKS below
+
+// Add the wave's LDS tile histogram of chunk `chunk` into counts[tile][chunk % BIN_BLOCKS]
+// and clear it (wave-uniform call; LDS ops of one wave complete in order).
+__device__ __forceinline__ void flush_hist(const KParams& K, uint32_t* whist, uint32_t chunk) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t t = lane; t < K.hist_tiles; t += 64) {
+    const uint32_t v = whist[t];
+    if (v) {
+      atomicAdd(K.bin_counts + (uint64_t)t * BIN_BLOCKS_ + (chunk % BIN_BLOCKS_), v);
+      whist[t] = 0;
+    }
+  }
+}
+
 __device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool dep, uint32_t vox, double val,
-                                              uint32_t& overflow) {
+                                              uint32_t& overflow, uint32_t* whist) {
   const uint64_t m = __ballot(dep);
   if (!m) return;
   const uint32_t n = __popcll(m);
   const int lane = threadIdx.x & 63;
   const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+  const bool fused = K.hist_tiles != 0;
   uint32_t before = 0;  // lanes that still fit in the current chunk
   if (W.chunk < K.n_chunks) before = (CHUNK_RECORDS - W.fill) < n ? (CHUNK_RECORDS - W.fill) : n;
-  if (dep && rank < before) K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + W.fill + rank] = pack_record(vox, val);
+  if (dep && rank < before) {
+    K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + W.fill + rank] = pack_record(vox, val);
+    if (fused) atomicAdd(whist + (vox >> TILE_SHIFT), 1u);
+  }
   W.fill += before;
   if (before < n) {  // chunk full or none yet: retire it, take the next one
     const uint32_t rest = n - before;
     if (W.chunk != LOG_EXHAUSTED) {
+      if (W.chunk < K.n_chunks && fused) flush_hist(K, whist, W.chunk);
       if (W.chunk < K.n_chunks && lane == 0) K.chunk_fill[W.chunk] = W.fill;
       uint32_t c = 0;
       if (lane == 0) c = atomicAdd(K.dep_ctl, 1u);
@@ -72,8 +96,10 @@ __device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool 
       W.fill = 0;
     }
     if (W.chunk < K.n_chunks) {  // rest <= 64 < CHUNK_RECORDS
-      if (dep && rank >= before)
+      if (dep && rank >= before) {
         K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + (rank - before)] = pack_record(vox, val);
+        if (fused) atomicAdd(whist + (vox >> TILE_SHIFT), 1u);
+      }
       W.fill = rest;
     } else {  // pool exhausted: stay correct with fp64 atomics
       if (dep && rank >= before) atomic_add_nr(K.jmean + vox, val);
@@ -82,8 +108,9 @@ __device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool 
   }
 }
 
-__device__ __forceinline__ void close_log(const KParams& K, RecLog& W, uint32_t overflow) {
+__device__ __forceinline__ void close_log(const KParams& K, RecLog& W, uint32_t overflow, uint32_t* whist) {
   const int lane = threadIdx.x & 63;
+  if (W.chunk < K.n_chunks && K.hist_tiles) flush_hist(K, whist, W.chunk);
   if (lane == 0) {
     if (W.chunk < K.n_chunks) K.chunk_fill[W.chunk] = W.fill;
     if (overflow) atomicAdd(K.dep_ctl + 1, overflow);
@@ -93,9 +120,12 @@ __device__ __forceinline__ void close_log(const KParams& K, RecLog& W, uint32_t 
 // Chunk c of the pool belongs to bin block c % BIN_BLOCKS in both bin_hist and bin_scatter,
 // so every (tile, block) pair owns one contiguous run of the sorted array and the scatter
 // needs no global atomics.
-constexpr uint32_t BIN_BLOCKS = 1024;
+constexpr uint32_t BIN_BLOCKS = BIN_BLOCKS_;
 constexpr int BIN_THREADS = 1024;
-constexpr uint32_t STAGE_RECORDS = 8192;                        // records per LDS pass of bin_scatter
+#ifndef SMCRT_STAGE_RECORDS
+#define SMCRT_STAGE_RECORDS 8192
+#endif
+constexpr uint32_t STAGE_RECORDS = SMCRT_STAGE_RECORDS;        // records per LDS pass of bin_scatter
 constexpr int STAGE_PER_THREAD = STAGE_RECORDS / BIN_THREADS;  // 8
 
 __device__ __forceinline__ uint32_t rec_tile(unsigned long long x) { return (uint32_t)(x >> 32) >> TILE_SHIFT; }
@@ -161,13 +191,14 @@ __global__ __launch_bounds__(1024) void bin_scan(const uint32_t* __restrict__ ti
   const uint32_t per = (n_tiles + blockDim.x - 1) / blockDim.x;
   const uint32_t t0 = threadIdx.x * per < n_tiles ? threadIdx.x * per : n_tiles;
   const uint32_t t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
-  uint32_t s = 0, np = 0;
-  for (uint32_t t = t0; t < t1; ++t) {
-    s += tile_count[t];
-    np += (tile_count[t] + PIECE_RECORDS - 1) / PIECE_RECORDS;
-  }
+  uint32_t s = 0;
+  for (uint32_t t = t0; t < t1; ++t) s += tile_count[t];
   uint32_t all_s, all_np;
   uint32_t off = block_exscan(s, wsum, &all_s);
+  const uint32_t want = all_s / REDUCE_PIECES + 1;
+  const uint32_t piece = want > MIN_PIECE_RECORDS ? want : MIN_PIECE_RECORDS;
+  uint32_t np = 0;
+  for (uint32_t t = t0; t < t1; ++t) np += (tile_count[t] + piece - 1) / piece;
   uint32_t pc = block_exscan(np, wsum, &all_np);
   if (threadIdx.x == 0) {
     dep_ctl[2] = all_np;  // number of pieces
@@ -176,9 +207,9 @@ __global__ __launch_bounds__(1024) void bin_scan(const uint32_t* __restrict__ ti
   for (uint32_t t = t0; t < t1; ++t) {
     const uint32_t c = tile_count[t];
     tile_start[t] = off;
-    for (uint32_t k = 0; k < c; k += PIECE_RECORDS) {
+    for (uint32_t k = 0; k < c; k += piece) {
       Piece p;
-      p.tile = t; p.start = off + k; p.count = (c - k) < PIECE_RECORDS ? (c - k) : PIECE_RECORDS; p.pad = 0;
+      p.tile = t; p.start = off + k; p.count = (c - k) < piece ? (c - k) : piece; p.pad = 0;
       pieces[pc++] = p;
     }
     off += c;
@@ -199,7 +230,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
                                                            const uint32_t* __restrict__ dep_ctl, uint32_t n_chunks,
                                                            uint32_t n_tiles, const uint32_t* __restrict__ tile_start,
                                                            const uint32_t* __restrict__ counts,
-                                                           unsigned long long* __restrict__ sorted) {
+                                                           unsigned long long* __restrict__ sorted, uint64_t cap) {
   extern __shared__ unsigned long long stage[];
   uint32_t* cnt = (uint32_t*)(stage + STAGE_RECORDS);
   uint32_t* base = cnt + n_tiles + 1;
@@ -231,6 +262,17 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
         rank[k] = i < n ? atomicAdd(&cnt[rec_tile(v[k])], 1u) : 0u;
       }
       __syncthreads();
+#ifdef SMCRT_SCATTER_DIRECT
+#pragma unroll
+      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+        const uint32_t i = threadIdx.x + k * BIN_THREADS;
+        if (i < n && (uint64_t)base[rec_tile(v[k])] + rank[k] < cap) sorted[base[rec_tile(v[k])] + rank[k]] = v[k];
+      }
+      __syncthreads();
+      for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) base[t] += cnt[t];
+      __syncthreads();
+      continue;
+#endif
       // exclusive scan of cnt[0..n_tiles) in place; cnt[n_tiles] = n
       uint32_t s = 0;
       for (uint32_t t = t0; t < t1; ++t) s += cnt[t];
@@ -255,7 +297,8 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
         if (j < n) {
           const unsigned long long x = stage[j];
           const uint32_t t = rec_tile(x);
-          sorted[base[t] + (j - cnt[t])] = x;
+          const uint64_t at = (uint64_t)base[t] + (j - cnt[t]);
+          if (at < cap) sorted[at] = x;  // (guard: counts and records always agree)
         }
       }
       __syncthreads();
@@ -266,6 +309,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 }
 
 // ---- bin_reduce: one tile piece per block, fp64 LDS sums added into jmean ----------------
+// (blockDim.x must be 1024)
 __global__ __launch_bounds__(1024) void bin_reduce(const unsigned long long* __restrict__ sorted,
                                                    const Piece* __restrict__ pieces,
                                                    const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
@@ -277,7 +321,16 @@ __global__ __launch_bounds__(1024) void bin_reduce(const unsigned long long* __r
     for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) acc[i] = 0.0;
     __syncthreads();
     const unsigned long long* r = sorted + p.start;
-    for (uint32_t i = threadIdx.x; i < p.count; i += blockDim.x) {
+    uint32_t i = threadIdx.x;
+    for (; i + 7 * 1024 < p.count; i += 8 * 1024) {  // 8 loads in flight per thread
+      unsigned long long x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = r[i + k * 1024];
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        atomicAdd(&acc[(uint32_t)(x[k] >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x[k]));
+    }
+    for (; i < p.count; i += 1024) {
       const unsigned long long x = r[i];
       atomicAdd(&acc[(uint32_t)(x >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x));
     }

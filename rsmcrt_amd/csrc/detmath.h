@@ -46,7 +46,15 @@ struct Rng {
   __device__ __forceinline__ double next(uint32_t key0, uint32_t key1) {
     const uint32_t d = draws++;
     if (d & 1u) return cached;
+#ifdef SMCRT_ABL_CHEAP_RNG  // timing ablation only: not the engine's stream
+    Philox4 o;
+    {
+      uint32_t a = (d >> 1) * 0x9E3779B9u ^ pid_lo, b = pid_hi ^ key0 ^ (a * 0x85EBCA6Bu);
+      o.v[0] = a ^ (b >> 13); o.v[1] = b * 0xC2B2AE35u; o.v[2] = a * 0x27D4EB2Fu ^ b; o.v[3] = (a + b) * 0x165667B1u;
+    }
+#else
     const Philox4 o = philox4x32_10(d >> 1, 0u, pid_lo, pid_hi, key0, key1);
+#endif
     const uint64_t u0 = ((uint64_t)o.v[1] << 32) | o.v[0];
     const uint64_t u1 = ((uint64_t)o.v[3] << 32) | o.v[2];
     cached = (double)(u1 >> 11) * 0x1.0p-53;

@@ -44,11 +44,17 @@ __device__ __forceinline__ double csg(int32_t op, double d1, double d2, double k
   }
 }
 
-// One primitive, sdfs.f90:494-735. `nd` is wave-uniform: its fields arrive by scalar loads
-// and the switch never diverges.
-__device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos) {
+// One primitive, sdfs.f90:494-735, at p = pos .dot. transform. `nd` is wave-uniform: its
+// fields arrive by scalar loads and the switch never diverges.
+//
+// translate_only: the transform's 3x3 part is the identity (every builder's
+// invert(translate(c)), setupGeometry.f90:64,289), so ((x*1 + y*0) + z*0) + t = x + t.
+// This is exact for every finite input; at most the sign of a zero result differs, which
+// no SDF below can observe (they use squares, abs, min/max and comparisons with 0).
+__device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos, bool translate_only) {
   const double* P = nd->param;
-  const V3 p = dotmat(pos, nd->transform);
+  const double* t = nd->transform;
+  const V3 p = translate_only ? v3(pos.x + t[3], pos.y + t[7], pos.z + t[11]) : dotmat(pos, t);
   switch (nd->kind) {
     case SMCRT_SDF_SPHERE:  // :494-508
       return sqrt(p.x * p.x + p.y * p.y + p.z * p.z) - P[0];
@@ -139,6 +145,8 @@ struct ProgOp {
   int32_t top;    // 1-based top-level index completed by this op (0 if none)
   int32_t op;     // CSG op for PROG_CHILD
   double k;       // CSG parameter
+  int32_t translate_only;  // the node's transform is a pure translation (see sdf_prim)
+  int32_t pad;
 };
 
 }  // namespace smcrt

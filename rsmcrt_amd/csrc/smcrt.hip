@@ -67,11 +67,12 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   const bool survival = (K.flags & SMCRT_FLAG_SURVIVAL_BIAS) != 0;
   const int lane_id = threadIdx.x & 63;
 
-  extern __shared__ double sh_dyn[];  // [props (4 doubles per top-level SDF) | faces]
+  extern __shared__ double sh_dyn[];  // [props (4 doubles per top-level SDF) | faces] | wave tile histograms
   const TopProps* props = K.props;
   const double* xf = K.xface;
   const double* yf = K.yface;
   const double* zf = K.zface;
+  int hist_off = 0;  // doubles of sh_dyn before the wave histograms
   if constexpr (LDS_FACES) {
     // per-lane (divergent) lookups go to LDS, never to vector memory: a vector load would
     // make the wave wait for all of its outstanding deposit atomics
@@ -85,7 +86,10 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     xf = sh_faces;
     yf = sh_faces + (K.nx + 1);
     zf = yf + (K.ny + 1);
+    hist_off = np + nf;
   }
+  uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * K.hist_tiles;
+  for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
 #pragma unroll
   for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
 #pragma unroll
@@ -334,7 +338,11 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         double val = 0.0;
         if (L.seg) dda_step<P2>(K, L, xf, yf, zf, dep, vox, val);
         w_dep += __popcll(__ballot(dep));
-        if (binned) emit_deposits(K, W, dep, vox, val, overflow);
+#ifdef SMCRT_ABL_NO_EMIT  // timing ablation only: deposits are computed but dropped
+        if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, W, dep, vox, val, overflow, whist); }
+#else
+        if (binned) emit_deposits(K, W, dep, vox, val, overflow, whist);
+#endif
         else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
       }
     }
@@ -500,7 +508,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     }
   }
 
-  if (binned) close_log(K, W, overflow);
+  if (binned) close_log(K, W, overflow, whist);
 
   // ---- per-wave counter reduction ------------------------------------------------------
   unsigned long long* const counters = C->counters;
@@ -595,6 +603,7 @@ struct smcrt_scene {
   int grid_blocks = 0;
   bool lds_faces = false;
   size_t face_bytes = 0;
+  uint32_t hist_tiles = 0;  // fused tile histogram in the transport kernel (0: bin_hist kernel)
   // binned jmean deposition (deposit.h)
   uint32_t n_tiles = 0;
   unsigned long long* d_pool = nullptr;    // record log, cap records
@@ -625,6 +634,7 @@ struct smcrt_scene {
 
 constexpr size_t MAX_TIMED = 256;
 constexpr uint64_t COLD_SLOTS = 64;
+constexpr uint32_t MAX_FUSED_HIST_TILES = 512;  // 8 KiB of LDS per block for the wave histograms
 // Record pool: record indices in the bin kernels are 32-bit, so at most 2^32 - 2^28 records
 // (30 GiB, plus the same again for the sorted copy) per launch; a launch that would need more
 // is split into sub-batches. POOL_SLACK covers the spread of records per photon between
@@ -652,6 +662,11 @@ static hipError_t harvest_times(smcrt_scene* s) {
 static const void* transport_fn(const smcrt_scene* s) {
   if (s->lds_faces) return s->pow2 ? (const void*)transport_kernel<true, true> : (const void*)transport_kernel<true, false>;
   return s->pow2 ? (const void*)transport_kernel<false, true> : (const void*)transport_kernel<false, false>;
+}
+
+// Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
+static size_t transport_lds(const smcrt_scene* s, uint32_t hist_tiles) {
+  return (s->lds_faces ? s->face_bytes : 0) + (size_t)4 * hist_tiles * sizeof(uint32_t);
 }
 
 static TopProps make_props(const smcrt_sdf_node& nd) {
@@ -766,14 +781,20 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   int st;
   // flatten the SDF array into one evaluation program (eval_model fold order)
   std::vector<ProgOp> prog;
+  auto translate_only = [&](int32_t idx) -> int32_t {  // 3x3 part of the column-major transform is I
+    const double* t = nodes[idx].transform;
+    return t[0] == 1.0 && t[1] == 0.0 && t[2] == 0.0 && t[4] == 0.0 && t[5] == 1.0 && t[6] == 0.0 &&
+           t[8] == 0.0 && t[9] == 0.0 && t[10] == 1.0;
+  };
   for (int32_t i = 0; i < n_top; ++i) {
     const smcrt_sdf_node& nd = nodes[top[i]];
     if (nd.kind != SMCRT_SDF_MODEL) {
-      prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0});
+      prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0, translate_only(top[i]), 0});
     } else {
       for (int32_t c = 0; c < nd.n_children; ++c)
         prog.push_back(ProgOp{nd.first_child + c, c == 0 ? PROG_CHILD_FIRST : PROG_CHILD,
-                              c == nd.n_children - 1 ? i + 1 : 0, nd.op, nd.k});
+                              c == nd.n_children - 1 ? i + 1 : 0, nd.op, nd.k,
+                              translate_only(nd.first_child + c), 0});
     }
   }
   s->n_prog = (int)prog.size();
@@ -826,9 +847,14 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   int per_cu = 0, cus = 0;
   s->face_bytes = faces.size() * sizeof(double) + sizeof(TopProps) * (size_t)n_top;
   s->lds_faces = s->face_bytes <= 40960;  // stage props + voxel faces in LDS when they fit
+  {
+    const char* fh = std::getenv("SMCRT_FUSED_HIST");
+    const bool fuse = !(fh && std::string(fh) == "0");
+    s->hist_tiles = (fuse && s->n_tiles > 0 && s->n_tiles <= MAX_FUSED_HIST_TILES) ? s->n_tiles : 0;
+  }
   s->pow2 = s->inv2[0] != 0.0 && s->inv2[1] != 0.0 && s->inv2[2] != 0.0;
   const void* kfn = transport_fn(s);
-  hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, s->lds_faces ? s->face_bytes : 0);
+  hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, s->hist_tiles));
   if (oe != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   s->grid_blocks = cus * per_cu;
@@ -874,14 +900,18 @@ static uint64_t pool_records_for(const smcrt_scene* s, uint64_t n) {
 
 // Make sure the record pool holds `records` (grow only). Returns false if it cannot.
 static bool ensure_pool(smcrt_scene* s, uint64_t records) {
-  const uint64_t chunks = (records + CHUNK_RECORDS - 1) / CHUNK_RECORDS;
+  uint64_t chunks = (records + CHUNK_RECORDS - 1) / CHUNK_RECORDS;
   if (chunks <= s->pool_chunks) return true;
+  // grow with 25% headroom so launch-to-launch jitter of the estimate never reallocates
+  // (a reallocation synchronises the device)
+  chunks = std::min<uint64_t>(chunks + chunks / 4, MAX_POOL_RECORDS / CHUNK_RECORDS);
   const void* old[] = {s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_pieces};
   for (const void* p : old)
     if (p) (void)hipFree((void*)p);
   s->d_pool = s->d_sorted = nullptr; s->d_chunk_fill = nullptr; s->d_pieces = nullptr; s->pool_chunks = 0;
   const uint64_t cap = chunks * CHUNK_RECORDS;
-  const uint64_t pieces = cap / PIECE_RECORDS + s->n_tiles + 1;
+  // pieces <= records / piece size + one partial piece per tile (deposit.h bin_scan)
+  const uint64_t pieces = std::min<uint64_t>(cap / MIN_PIECE_RECORDS, REDUCE_PIECES + 1) + s->n_tiles + 1;
   if (hipMalloc((void**)&s->d_pool, cap * 8) != hipSuccess || hipMalloc((void**)&s->d_sorted, cap * 8) != hipSuccess ||
       hipMalloc((void**)&s->d_chunk_fill, chunks * 4) != hipSuccess ||
       hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) != hipSuccess) {
@@ -905,6 +935,8 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
   const bool binned = K.rec_pool != nullptr;
   if (binned) {
     HIPCHK(hipMemsetAsync(s->d_dep_ctl, 0, 4 * sizeof(uint32_t), stream));
+    if (K.hist_tiles)
+      HIPCHK(hipMemsetAsync(s->d_bin_counts, 0, (size_t)s->n_tiles * BIN_BLOCKS * sizeof(uint32_t), stream));
   }
   hipEvent_t* ev = nullptr;
   if (s->timing) {
@@ -928,22 +960,23 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
     const smcrt_detector* a_dets = K.dets;
     const int64_t* a_off = K.det_off;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&a_dets, (void*)&a_off, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(transport_fn(s), dim3(blocks), dim3(256), args, s->lds_faces ? s->face_bytes : 0, stream));
+    HIPCHK(hipLaunchKernel(transport_fn(s), dim3(blocks), dim3(256), args, transport_lds(s, K.hist_tiles), stream));
   }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
   if (binned) {
     const uint32_t nch = (uint32_t)s->pool_chunks;
     const uint64_t nv = (uint64_t)s->grid.nx * s->grid.ny * s->grid.nz;
-    hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, stream, s->d_pool, s->d_chunk_fill,
-                       s->d_dep_ctl, nch, s->n_tiles, s->d_bin_counts);
+    if (!K.hist_tiles)  // else the transport kernel built the counts
+      hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, stream, s->d_pool, s->d_chunk_fill,
+                         s->d_dep_ctl, nch, s->n_tiles, s->d_bin_counts);
     hipLaunchKernelGGL(bin_rowscan, dim3(s->n_tiles), dim3(BIN_BLOCKS), 0, stream, s->d_bin_counts,
                        s->d_tile_count);
     hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, stream, s->d_tile_count, s->n_tiles, s->d_tile_start,
                        s->d_pieces, s->d_dep_ctl);
     hipLaunchKernelGGL(bin_scatter, dim3(BIN_BLOCKS), dim3(BIN_THREADS), s->scatter_lds, stream, s->d_pool,
                        s->d_chunk_fill, s->d_dep_ctl, nch, s->n_tiles, s->d_tile_start, s->d_bin_counts,
-                       s->d_sorted);
+                       s->d_sorted, (uint64_t)s->pool_chunks * CHUNK_RECORDS);
     hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, stream, s->d_sorted, s->d_pieces, s->d_dep_ctl, nv,
                        K.jmean);
     HIPCHK(hipGetLastError());
@@ -1001,6 +1034,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = s->d_queue;
   K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
+  K.bin_counts = s->d_bin_counts; K.hist_tiles = 0;
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
@@ -1010,6 +1044,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
     refine_rpp(s);
     uint64_t n = cfg->n_photons - done;
     K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
+  K.bin_counts = s->d_bin_counts; K.hist_tiles = 0;
     bool calibrate = false;
     if (binned) {
       // records per photon are scene-dependent: the scene's first large launch starts with a
@@ -1025,6 +1060,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
         K.chunk_fill = s->d_chunk_fill;
         K.dep_ctl = s->d_dep_ctl;
         K.n_chunks = (uint32_t)s->pool_chunks;
+        K.hist_tiles = s->hist_tiles;
       }
     }
     Ch.n_photons = n;

@@ -91,6 +91,10 @@ struct KParams {
   uint32_t* chunk_fill;          // records in each used chunk
   uint32_t* dep_ctl;             // [0] next chunk, [1] overflowed deposits
   uint32_t n_chunks;
+  // fused tile histogram (deposit.h): counts[tile][chunk % BIN_BLOCKS] built by the
+  // transport kernel from a per-wave LDS histogram; hist_tiles == 0 -> bin_hist does it
+  uint32_t* bin_counts;
+  uint32_t hist_tiles;
 };
 
 // ------------------------------------------------------------------ voxels -------
@@ -531,7 +535,7 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
     const ProgOp op = prog[ip];
     // the program is wave-uniform: keep node parameters on the scalar path
     const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-    const double v = sdf_prim(nodes + node, q);
+    const double v = sdf_prim(nodes + node, q, op.translate_only != 0);
     if (op.action == PROG_TOP) acc = v;
     else if (op.action == PROG_CHILD_FIRST) acc = v;
     else acc = csg(op.op, acc, v, op.k);

@@ -171,3 +171,57 @@ def test_point_source_symmetry():
     octs = np.array(octs)
     assert np.all(np.abs(octs / octs.mean() - 1.0) < 0.01)
     assert abs(j.sum() / n - 6.0) < 0.1  # ~6 cm path per photon (Survey §6 probe: 6.01-6.05)
+
+
+@pytest.mark.parametrize("env", [{}, {"SMCRT_FUSED_HIST": "0"}, {"SMCRT_DEPOSIT": "atomic"}],
+                         ids=["fused-hist", "hist-kernel", "atomics"])
+def test_deposit_paths(monkeypatch, env):
+    """Every jmean deposition path (binned with the tile histogram fused into the transport
+    kernel, binned with the separate bin_hist kernel, fp64 atomics) gives the oracle's
+    result. The paths are chosen when the scene is created."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    gpu, cpu = both(sc, scene.grid(96, 96, 96, 1, 1, 1), scene.point_source(), 20000)
+    compare(gpu, cpu)
+    assert cpu.counter("deposits") > 1_000_000
+
+
+def test_multi_launch_pool_reuse():
+    """A scene reused for batches of very different size (calibration launch, pool growth,
+    sub-batching) accumulates exactly the single-run result."""
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(64, 64, 64, 1, 1, 1)
+    src = scene.point_source()
+    with Engine(sc, g) as eng:
+        res = eng.run(src, 300, seed=SEED)
+        for first, n in ((300, 700_000), (700_300, 50), (700_350, 2_000)):
+            eng.run(src, n, seed=SEED, first_photon=first, result=res)
+    cpu = O.run(sc, g, src, 702_350, seed=SEED)
+    assert res.counters_dict() == cpu.counters_dict()
+    np.testing.assert_allclose(res.jmean, cpu.jmean, rtol=RTOL, atol=1e-300)
+    assert np.array_equal(res.absorb, cpu.absorb)
+
+
+def test_vessels_capsule_net():
+    """M4 (build-defined): a capsule tree as separate top-level SDFs in a
+    dermis box, uniform source over the top face: a deep SDF array (49 SDFs per EVAL)."""
+    sc = builders.synthetic_vessels(n_capsules=48)
+    g = scene.grid(48, 40, 44, 0.16, 0.09, 0.13)
+    src = scene.uniform_source((-0.16, -0.09, 0.1299), (0.32, 0.0, 0.0), (0.0, 0.18, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, g, src, 1500)
+    compare(gpu, cpu)
+    assert cpu.counter("sdf_evals") > 1500 * 49 * 10
+
+
+def test_skin_layers_with_detectors():
+    """M5 (build-defined): layered boxes with different n (Fresnel at every interface), a
+    pencil beam and reflectance detectors on the top surface."""
+    sc = builders.skin_layers()
+    g = scene.grid(50, 50, 50, 0.05, 0.05, 0.05)
+    src = scene.pencil_source((0.0, 0.0, 0.0499), (0.0, 0.0, -1.0))
+    dets = [scene.circle_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.05, 50),
+            scene.annulus_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.005, 0.02, 25)]
+    gpu, cpu = both(sc, g, src, 3000, dets=dets)
+    compare(gpu, cpu)
+    assert cpu.counter("fresnel") > 0

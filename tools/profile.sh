@@ -13,9 +13,15 @@ run() {  # name, rocprof args...
     > $OUT/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc"; if fatal $rc; then exit $rc; fi
 }
-run trace --kernel-trace --stats
-run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE
-run pmc_fetch --pmc FETCH_SIZE
-run pmc_write --pmc WRITE_SIZE
-run pmc_tcc --pmc TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum
+PASSES=${PASSES:-"trace sq fetch write tcc"}
+for p in $PASSES; do
+  case $p in
+    trace) run trace --kernel-trace --stats ;;
+    sq) run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE ;;
+    fetch) run pmc_fetch --pmc FETCH_SIZE ;;
+    write) run pmc_write --pmc WRITE_SIZE ;;
+    tcc) run pmc_tcc --pmc TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum ;;
+    valu) run pmc_valu --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_LDS SQ_INSTS_SMEM ;;
+  esac
+done
 find $OUT -name "*.csv" | head -50
