@@ -27,7 +27,7 @@ namespace smcrt {
 constexpr uint32_t CHUNK_RECORDS = 16384;  // 128 KiB per chunk
 constexpr uint32_t TILE_SHIFT = 13;        // 8192 voxels per tile: 64 KiB of fp64 in LDS
 constexpr uint32_t TILE_VOXELS = 1u << TILE_SHIFT;
-constexpr uint32_t MAX_TILES = 8192;       // grids up to 2^26 voxels use the binned path
+constexpr uint32_t MAX_TILES = 4096;       // grids up to 2^25 voxels use the binned path
 // A reduce piece is one block's share of one tile. Each piece ends with one fp64 atomic per
 // touched voxel of its tile (up to TILE_VOXELS), so pieces are made as large as load balance
 // allows: about REDUCE_PIECES pieces in total, and never smaller than MIN_PIECE_RECORDS.
@@ -217,12 +217,28 @@ __global__ __launch_bounds__(1024) void bin_scan(const uint32_t* __restrict__ ti
 }
 
 // ---- bin_scatter: records into tile order --------------------------------------------------
-// Per pass of STAGE_RECORDS records: count per tile in LDS (the returned count is the
-// record's rank), scan, place the records tile-ordered in LDS, then write them out with
-// consecutive threads on consecutive addresses of each tile's run.
-// Dynamic LDS: stage[STAGE_RECORDS] u64 | cnt[n_tiles + 1] | base[n_tiles] | wsum[16].
+// Block b walks the chunks c = b, b + BIN_BLOCKS, ... in passes of STAGE_RECORDS records:
+//   A  rank: LDS atomic count per tile (the returned count is the record's rank)
+//   B  wave 0: scan the counts -> off[t]; dest[t] = base[t] - off[t]; base[t] += count;
+//      counts cleared for the next pass
+//   C  place the records tile-ordered in LDS (stage[off[t] + rank])
+//   D  write stage[j] to sorted[dest[t] + j]: consecutive threads, consecutive addresses
+// The next pass's records are loaded during B-D. Three barriers per pass.
+// Dynamic LDS: stage[STAGE_RECORDS] u64 | cnt[n_tiles] | off[n_tiles + 1] | dest[n_tiles] | base[n_tiles].
 inline size_t scatter_lds_bytes(uint32_t n_tiles) {
-  return STAGE_RECORDS * 8 + ((size_t)2 * n_tiles + 1 + 16) * 4;
+  return STAGE_RECORDS * 8 + ((size_t)4 * n_tiles + 1) * 4;
+}
+
+__device__ __forceinline__ void load_stage(unsigned long long (&v)[STAGE_PER_THREAD],
+                                           const unsigned long long* __restrict__ pool, uint32_t c, uint32_t h,
+                                           uint32_t fill) {
+  const unsigned long long* r = pool + (uint64_t)c * CHUNK_RECORDS + h;
+  const uint32_t n = fill - h < STAGE_RECORDS ? fill - h : STAGE_RECORDS;
+#pragma unroll
+  for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+    const uint32_t i = threadIdx.x + k * BIN_THREADS;
+    v[k] = i < n ? r[i] : 0ull;
+  }
 }
 
 __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long long* __restrict__ pool,
@@ -233,78 +249,80 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
                                                            unsigned long long* __restrict__ sorted, uint64_t cap) {
   extern __shared__ unsigned long long stage[];
   uint32_t* cnt = (uint32_t*)(stage + STAGE_RECORDS);
-  uint32_t* base = cnt + n_tiles + 1;
-  uint32_t* wsum = base + n_tiles;
+  uint32_t* off = cnt + n_tiles;
+  uint32_t* dest = off + n_tiles + 1;
+  uint32_t* base = dest + n_tiles;
   const uint32_t used = dep_ctl[0] < n_chunks ? dep_ctl[0] : n_chunks;
   if (blockIdx.x >= used) return;  // block-uniform
-  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x)
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
     base[t] = tile_start[t] + counts[(uint64_t)t * BIN_BLOCKS + blockIdx.x];
-  const uint32_t per = (n_tiles + blockDim.x - 1) / blockDim.x;
-  const uint32_t t0 = threadIdx.x * per < n_tiles ? threadIdx.x * per : n_tiles;
+    cnt[t] = 0;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint32_t per = (n_tiles + 63) / 64;  // wave-0 scan: consecutive tiles per lane
+  const uint32_t t0 = lane * per < n_tiles ? lane * per : n_tiles;
   const uint32_t t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
-  for (uint32_t c = blockIdx.x; c < used; c += BIN_BLOCKS) {
-    const uint32_t fill = chunk_fill[c];
-    const unsigned long long* r = pool + (uint64_t)c * CHUNK_RECORDS;
-    for (uint32_t h = 0; h < fill; h += STAGE_RECORDS) {
-      const uint32_t n = fill - h < STAGE_RECORDS ? fill - h : STAGE_RECORDS;
-      for (uint32_t t = threadIdx.x; t <= n_tiles; t += blockDim.x) cnt[t] = 0;
-      __syncthreads();
-      unsigned long long v[STAGE_PER_THREAD];
-      uint32_t rank[STAGE_PER_THREAD];
+
+  uint32_t c = blockIdx.x, h = 0, fill = chunk_fill[c];
+  unsigned long long v[STAGE_PER_THREAD];
+  load_stage(v, pool, c, h, fill);
+  __syncthreads();
+  for (;;) {
+    const uint32_t n = fill - h < STAGE_RECORDS ? fill - h : STAGE_RECORDS;
+    uint32_t rank[STAGE_PER_THREAD];  // A
 #pragma unroll
-      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-        const uint32_t i = threadIdx.x + k * BIN_THREADS;
-        v[k] = i < n ? r[h + i] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-        const uint32_t i = threadIdx.x + k * BIN_THREADS;
-        rank[k] = i < n ? atomicAdd(&cnt[rec_tile(v[k])], 1u) : 0u;
-      }
-      __syncthreads();
-#ifdef SMCRT_SCATTER_DIRECT
-#pragma unroll
-      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-        const uint32_t i = threadIdx.x + k * BIN_THREADS;
-        if (i < n && (uint64_t)base[rec_tile(v[k])] + rank[k] < cap) sorted[base[rec_tile(v[k])] + rank[k]] = v[k];
-      }
-      __syncthreads();
-      for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) base[t] += cnt[t];
-      __syncthreads();
-      continue;
-#endif
-      // exclusive scan of cnt[0..n_tiles) in place; cnt[n_tiles] = n
-      uint32_t s = 0;
-      for (uint32_t t = t0; t < t1; ++t) s += cnt[t];
-      uint32_t all;
-      uint32_t off = block_exscan(s, wsum, &all);
-      for (uint32_t t = t0; t < t1; ++t) {
-        const uint32_t x = cnt[t];
-        cnt[t] = off;
-        off += x;
-      }
-      if (threadIdx.x == 0) cnt[n_tiles] = n;
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-        const uint32_t i = threadIdx.x + k * BIN_THREADS;
-        if (i < n) stage[cnt[rec_tile(v[k])] + rank[k]] = v[k];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < STAGE_PER_THREAD; ++k) {
-        const uint32_t j = threadIdx.x + k * BIN_THREADS;
-        if (j < n) {
-          const unsigned long long x = stage[j];
-          const uint32_t t = rec_tile(x);
-          const uint64_t at = (uint64_t)base[t] + (j - cnt[t]);
-          if (at < cap) sorted[at] = x;  // (guard: counts and records always agree)
-        }
-      }
-      __syncthreads();
-      for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) base[t] += cnt[t + 1] - cnt[t];
-      __syncthreads();
+    for (int k = 0; k < STAGE_PER_THREAD; ++k) {
+      const uint32_t i = threadIdx.x + k * BIN_THREADS;
+      rank[k] = i < n ? atomicAdd(&cnt[rec_tile(v[k])], 1u) : 0u;
     }
+    uint32_t cn = c, hn = h + STAGE_RECORDS, filln = fill;  // next pass, loaded during B-D
+    if (hn >= fill) {
+      cn = c + BIN_BLOCKS; hn = 0;
+      filln = cn < used ? chunk_fill[cn] : 0u;
+    }
+    unsigned long long vn[STAGE_PER_THREAD];
+    if (cn < used) load_stage(vn, pool, cn, hn, filln);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // B
+      uint32_t sum = 0;
+      for (uint32_t t = t0; t < t1; ++t) sum += cnt[t];
+      uint32_t x = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      uint32_t o = x - sum;
+      for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t k = cnt[t];
+        off[t] = o;
+        dest[t] = base[t] - o;
+        base[t] += k;
+        cnt[t] = 0;
+        o += k;
+      }
+      if (lane == 63) off[n_tiles] = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < STAGE_PER_THREAD; ++k) {  // C
+      const uint32_t i = threadIdx.x + k * BIN_THREADS;
+      if (i < n) stage[off[rec_tile(v[k])] + rank[k]] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < STAGE_PER_THREAD; ++k) {  // D
+      const uint32_t j = threadIdx.x + k * BIN_THREADS;
+      if (j < n) {
+        const unsigned long long x = stage[j];
+        const uint64_t at = (uint64_t)dest[rec_tile(x)] + j;
+        if (at < cap) sorted[at] = x;  // (guard: counts and records always agree)
+      }
+    }
+    if (cn >= used) break;
+    c = cn; h = hn; fill = filln;
+#pragma unroll
+    for (int k = 0; k < STAGE_PER_THREAD; ++k) v[k] = vn[k];
   }
 }
 
