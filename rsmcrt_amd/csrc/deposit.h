@@ -58,19 +58,20 @@ constexpr uint32_t BIN_BLOCKS_ = 1024;  // == BIN_BLOCKS below
 
 // Add the wave's LDS tile histogram of chunk `chunk` into counts[tile][chunk % BIN_BLOCKS]
 // and clear it (wave-uniform call; LDS ops of one wave complete in order).
-__device__ __forceinline__ void flush_hist(const KParams& K, uint32_t* whist, uint32_t chunk) {
+__device__ __forceinline__ void flush_hist(const KParams& K, const KCold* __restrict__ C, uint32_t* whist,
+                                           uint32_t chunk) {
   const int lane = threadIdx.x & 63;
   for (uint32_t t = lane; t < K.hist_tiles; t += 64) {
     const uint32_t v = whist[t];
     if (v) {
-      atomicAdd(K.bin_counts + (uint64_t)t * BIN_BLOCKS_ + (chunk % BIN_BLOCKS_), v);
+      atomicAdd(C->bin_counts + (uint64_t)t * BIN_BLOCKS_ + (chunk % BIN_BLOCKS_), v);
       whist[t] = 0;
     }
   }
 }
 
-__device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool dep, uint32_t vox, double val,
-                                              uint32_t& overflow, uint32_t* whist) {
+__device__ __forceinline__ void emit_deposits(const KParams& K, const KCold* __restrict__ C, RecLog& W, bool dep,
+                                              uint32_t vox, double val, uint32_t& overflow, uint32_t* whist) {
   const uint64_t m = __ballot(dep);
   if (!m) return;
   const uint32_t n = __popcll(m);
@@ -87,10 +88,10 @@ __device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool 
   if (before < n) {  // chunk full or none yet: retire it, take the next one
     const uint32_t rest = n - before;
     if (W.chunk != LOG_EXHAUSTED) {
-      if (W.chunk < K.n_chunks && fused) flush_hist(K, whist, W.chunk);
-      if (W.chunk < K.n_chunks && lane == 0) K.chunk_fill[W.chunk] = W.fill;
+      if (W.chunk < K.n_chunks && fused) flush_hist(K, C, whist, W.chunk);
+      if (W.chunk < K.n_chunks && lane == 0) C->chunk_fill[W.chunk] = W.fill;
       uint32_t c = 0;
-      if (lane == 0) c = atomicAdd(K.dep_ctl, 1u);
+      if (lane == 0) c = atomicAdd(C->dep_ctl, 1u);
       c = __shfl(c, 0, 64);
       W.chunk = c < K.n_chunks ? c : LOG_EXHAUSTED;
       W.fill = 0;
@@ -102,18 +103,19 @@ __device__ __forceinline__ void emit_deposits(const KParams& K, RecLog& W, bool 
       }
       W.fill = rest;
     } else {  // pool exhausted: stay correct with fp64 atomics
-      if (dep && rank >= before) atomic_add_nr(K.jmean + vox, val);
+      if (dep && rank >= before) atomic_add_nr(C->jmean + vox, val);
       overflow += rest;
     }
   }
 }
 
-__device__ __forceinline__ void close_log(const KParams& K, RecLog& W, uint32_t overflow, uint32_t* whist) {
+__device__ __forceinline__ void close_log(const KParams& K, const KCold* __restrict__ C, RecLog& W,
+                                          uint32_t overflow, uint32_t* whist) {
   const int lane = threadIdx.x & 63;
-  if (W.chunk < K.n_chunks && K.hist_tiles) flush_hist(K, whist, W.chunk);
+  if (W.chunk < K.n_chunks && K.hist_tiles) flush_hist(K, C, whist, W.chunk);
   if (lane == 0) {
-    if (W.chunk < K.n_chunks) K.chunk_fill[W.chunk] = W.fill;
-    if (overflow) atomicAdd(K.dep_ctl + 1, overflow);
+    if (W.chunk < K.n_chunks) C->chunk_fill[W.chunk] = W.fill;
+    if (overflow) atomicAdd(C->dep_ctl + 1, overflow);
   }
 }
 

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   L.hop = L.loopc = L.dda_it = 0;
   L.sd = L.slen = 0.0; L.ci = L.cj = L.ck = 0;
   L.rng.init(0);
-  const bool binned = K.rec_pool != nullptr && K.jmean != nullptr;
+  const bool binned = K.rec_pool != nullptr;  // (set only when jmean is tallied)
   RecLog W;
   W.chunk = LOG_NONE; W.fill = 0;
   uint32_t overflow = 0;
@@ -339,11 +339,14 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         if (L.seg) dda_step<P2>(K, L, xf, yf, zf, dep, vox, val);
         w_dep += __popcll(__ballot(dep));
 #ifdef SMCRT_ABL_NO_EMIT  // timing ablation only: deposits are computed but dropped
-        if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, W, dep, vox, val, overflow, whist); }
+        if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, C, W, dep, vox, val, overflow, whist); }
 #else
-        if (binned) emit_deposits(K, W, dep, vox, val, overflow, whist);
+        if (binned) emit_deposits(K, C, W, dep, vox, val, overflow, whist);
 #endif
-        else if (dep && K.jmean) atomic_add_nr(K.jmean + vox, val);
+        else if (dep) {
+          double* const jm = C->jmean;
+          if (jm) atomic_add_nr(jm + vox, val);
+        }
       }
     }
 
@@ -508,7 +511,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     }
   }
 
-  if (binned) close_log(K, W, overflow, whist);
+  if (binned) close_log(K, C, W, overflow, whist);
 
   // ---- per-wave counter reduction ------------------------------------------------------
   unsigned long long* const counters = C->counters;
@@ -978,7 +981,7 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
                        s->d_chunk_fill, s->d_dep_ctl, nch, s->n_tiles, s->d_tile_start, s->d_bin_counts,
                        s->d_sorted, (uint64_t)s->pool_chunks * CHUNK_RECORDS);
     hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, stream, s->d_sorted, s->d_pieces, s->d_dep_ctl, nv,
-                       K.jmean);
+                       Ch.jmean);
     HIPCHK(hipGetLastError());
     // remember how many records this launch produced (read back lazily, never waited for)
     HIPCHK(hipMemcpyAsync(s->h_ctl, s->d_dep_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1029,12 +1032,12 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.src = *src;
   K.key0 = (uint32_t)cfg->seed;
   K.key1 = (uint32_t)(cfg->seed >> 32);
-  K.jmean = dt.jmean; Ch.absorb = dt.absorb; Ch.emission = dt.emission;
+  Ch.jmean = dt.jmean; Ch.absorb = dt.absorb; Ch.emission = dt.emission;
+  Ch.chunk_fill = s->d_chunk_fill; Ch.dep_ctl = s->d_dep_ctl; Ch.bin_counts = s->d_bin_counts;
   Ch.det_bins = dt.det_bins; Ch.nscatt = dt.nscatt; Ch.moments = dt.moments;
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = s->d_queue;
-  K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
-  K.bin_counts = s->d_bin_counts; K.hist_tiles = 0;
+  K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0;
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
@@ -1043,8 +1046,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   for (uint64_t done = 0; done < cfg->n_photons;) {
     refine_rpp(s);
     uint64_t n = cfg->n_photons - done;
-    K.rec_pool = nullptr; K.chunk_fill = nullptr; K.dep_ctl = nullptr; K.n_chunks = 0;
-  K.bin_counts = s->d_bin_counts; K.hist_tiles = 0;
+    K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0;
     bool calibrate = false;
     if (binned) {
       // records per photon are scene-dependent: the scene's first large launch starts with a
@@ -1057,8 +1059,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
         n = std::min<uint64_t>(n, (uint64_t)std::max(65536.0, usable / (s->rpp_est * POOL_SLACK)));
         // (taken after ensure_pool: it may have reallocated the pool)
         K.rec_pool = s->d_pool;
-        K.chunk_fill = s->d_chunk_fill;
-        K.dep_ctl = s->d_dep_ctl;
+        Ch.chunk_fill = s->d_chunk_fill;  // (ensure_pool may have reallocated them)
         K.n_chunks = (uint32_t)s->pool_chunks;
         K.hist_tiles = s->hist_tiles;
       }

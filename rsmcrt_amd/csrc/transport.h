@@ -67,6 +67,10 @@ struct KCold {
   unsigned long long* counters;
   smcrt_photon_record* records;
   unsigned long long* queue;  // photon work-queue head (zeroed before launch)
+  double* jmean;              // fp64 atomics: the unbinned path and pool overflow
+  uint32_t* chunk_fill;       // records in each used chunk (deposit.h)
+  uint32_t* dep_ctl;          // [0] next chunk, [1] overflowed deposits
+  uint32_t* bin_counts;       // fused tile histogram, counts[tile][chunk % BIN_BLOCKS]
 };
 
 struct KParams {
@@ -85,15 +89,11 @@ struct KParams {
   // exact reciprocal of 2*max when that is a power of two (else 0): n*p/(2*max) == n*p*inv
   double inv2x, inv2y, inv2z;
   uint32_t key0, key1;  // Philox key = seed words
-  double* jmean;
   // binned jmean deposition (deposit.h): record log in chunks
   unsigned long long* rec_pool;  // CHUNK_RECORDS records per chunk; NULL -> fp64 atomics into jmean
-  uint32_t* chunk_fill;          // records in each used chunk
-  uint32_t* dep_ctl;             // [0] next chunk, [1] overflowed deposits
   uint32_t n_chunks;
   // fused tile histogram (deposit.h): counts[tile][chunk % BIN_BLOCKS] built by the
   // transport kernel from a per-wave LDS histogram; hist_tiles == 0 -> bin_hist does it
-  uint32_t* bin_counts;
   uint32_t hist_tiles;
 };
 
