@@ -25,9 +25,12 @@
 namespace smcrt {
 
 constexpr uint32_t CHUNK_RECORDS = 16384;  // 128 KiB per chunk
-constexpr uint32_t TILE_SHIFT = 13;        // 8192 voxels per tile: 64 KiB of fp64 in LDS
+#ifndef SMCRT_TILE_SHIFT
+#define SMCRT_TILE_SHIFT 14
+#endif
+constexpr uint32_t TILE_SHIFT = SMCRT_TILE_SHIFT;  // 16384 voxels per tile: 128 KiB of fp64 in LDS
 constexpr uint32_t TILE_VOXELS = 1u << TILE_SHIFT;
-constexpr uint32_t MAX_TILES = 4096;       // grids up to 2^25 voxels use the binned path
+constexpr uint32_t MAX_TILES = 4096;       // grids up to 2^26 voxels use the binned path
 // A reduce piece is one block's share of one tile. Each piece ends with one fp64 atomic per
 // touched voxel of its tile (up to TILE_VOXELS), so pieces are made as large as load balance
 // allows: about REDUCE_PIECES pieces in total, and never smaller than MIN_PIECE_RECORDS.
