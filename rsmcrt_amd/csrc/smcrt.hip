@@ -55,7 +55,10 @@ __device__ unsigned long long g_diag[72];
 #endif
 
 template <bool LDS_FACES, bool P2>
-__global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
+#ifndef SMCRT_WAVES_PER_EU
+#define SMCRT_WAVES_PER_EU 3
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES_PER_EU))) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
                                                         const ProgOp* __restrict__ prog,
                                                         const smcrt_detector* __restrict__ dets,
                                                         const int64_t* __restrict__ det_off,
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
   const bool survival = (K.flags & SMCRT_FLAG_SURVIVAL_BIAS) != 0;
   const int lane_id = threadIdx.x & 63;
 
-  extern __shared__ double sh_dyn[];  // [props (4 doubles per top-level SDF) | faces] | wave tile histograms
+  extern __shared__ double sh_dyn[];  // [props | faces] | [startPos if detectors] | wave tile histograms
   const TopProps* props = K.props;
   const double* xf = K.xface;
   const double* yf = K.yface;
@@ -88,6 +91,8 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
     zf = yf + (K.ny + 1);
     hist_off = np + nf;
   }
+  double* const startp = sh_dyn + hist_off + threadIdx.x;  // [3][256] when n_dets > 0
+  if (K.n_dets) hist_off += 3 * 256;
   uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * K.hist_tiles;
   for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
 #pragma unroll
@@ -274,8 +279,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
             const double s2 = 2.0 * dot(N, L.dir);
             L.dir = L.dir - smul(s2, N);
             LCTR(LC_REFL)++;
-            sh->start[0][threadIdx.x] = L.pos.x; sh->start[1][threadIdx.x] = L.pos.y;
-            sh->start[2][threadIdx.x] = L.pos.z;
+            if (K.n_dets) { startp[0] = L.pos.x; startp[256] = L.pos.y; startp[512] = L.pos.z; }
             if (++LU(LU_BOUNCES) > 1000) {  // :313-315: return without write-back
               LCTR(LC_BABORT)++;
               L.pos = v3(sh->entry[0][threadIdx.x], sh->entry[1][threadIdx.x], sh->entry[2][threadIdx.x]);
@@ -360,9 +364,11 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
         L.pos = L.ssp;
       }
       rec = true;  // :125-131, 195-201
-      rec_start = v3(sh->start[0][threadIdx.x], sh->start[1][threadIdx.x], sh->start[2][threadIdx.x]);
-      rec_sep = pointsep(L.pos, rec_start);
-      sh->start[0][threadIdx.x] = L.pos.x; sh->start[1][threadIdx.x] = L.pos.y; sh->start[2][threadIdx.x] = L.pos.z;
+      if (K.n_dets) {
+        rec_start = v3(startp[0], startp[256], startp[512]);
+        rec_sep = pointsep(L.pos, rec_start);
+        startp[0] = L.pos.x; startp[256] = L.pos.y; startp[512] = L.pos.z;
+      }
       if (L.st == ST_H2) {
         L.st = ST_H3; L.pend = true;
       } else if (L.st == ST_X1) {
@@ -450,8 +456,7 @@ __global__ __launch_bounds__(256) void transport_kernel(KParams K, const smcrt_s
           }
         }
         if (L.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
-          sh->start[0][threadIdx.x] = L.pos.x; sh->start[1][threadIdx.x] = L.pos.y;
-          sh->start[2][threadIdx.x] = L.pos.z;
+          if (K.n_dets) { startp[0] = L.pos.x; startp[256] = L.pos.y; startp[512] = L.pos.z; }
           sh->entry[0][threadIdx.x] = L.pos.x; sh->entry[1][threadIdx.x] = L.pos.y;
           sh->entry[2][threadIdx.x] = L.pos.z; sh->entry[3][threadIdx.x] = L.dir.x;
           sh->entry[4][threadIdx.x] = L.dir.y; sh->entry[5][threadIdx.x] = L.dir.z;
@@ -669,7 +674,8 @@ static const void* transport_fn(const smcrt_scene* s) {
 
 // Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
 static size_t transport_lds(const smcrt_scene* s, uint32_t hist_tiles) {
-  return (s->lds_faces ? s->face_bytes : 0) + (size_t)4 * hist_tiles * sizeof(uint32_t);
+  return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
+         (size_t)4 * hist_tiles * sizeof(uint32_t);
 }
 
 static TopProps make_props(const smcrt_sdf_node& nd) {

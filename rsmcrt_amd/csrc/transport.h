@@ -299,7 +299,8 @@ struct LaneShared {
   uint32_t ctr[LC_N][256];
   uint32_t u[LU_N][256];
   double entry[6][256];  // tauint2 entry pos/dir, restored on a bounce abort (inttau2.f90:313-315)
-  double start[3][256];  // startPos of the detector segment (inttau2.f90:59,125-131)
+  // (startPos of the detector segments, inttau2.f90:59,125-131, is in dynamic LDS and only
+  // allocated when the scene has detectors)
 };
 #define LCTR(c) (sh->ctr[(c)][threadIdx.x])
 #define LU(f) (sh->u[(f)][threadIdx.x])
