@@ -18,6 +18,10 @@ struct Philox4 {
 
 __device__ __forceinline__ Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                  uint32_t k0, uint32_t k1) {
+  // The key is wave-uniform. Make it opaque here so the ten round keys are derived at each
+  // call (two scalar adds per round) instead of being hoisted into twenty long-lived scalar
+  // registers, which the kernel cannot afford and would spill.
+  asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }

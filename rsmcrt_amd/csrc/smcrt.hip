@@ -52,6 +52,9 @@ __device__ __forceinline__ V3 eval_query(const Lane& L) {
 // [0..31] lane-trips by state at the trip head (+32 if a segment is active), [64] trips,
 // [65] trips running the DDA phase, [66] EVAL, [67] P7 events.
 __device__ unsigned long long g_diag[72];
+// wave-time (s_memtime ticks) per phase: [1] fetch [2] EVAL [3] P3 [4] P4 [5] DDA [6] P5-P6
+// [7] P7 [8] P8 + loop
+__device__ unsigned long long g_diag_t[9];
 #endif
 
 template <bool LDS_FACES, bool P2>
@@ -117,7 +120,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   uint64_t chunk_base = 0;  // wave-uniform photon chunk
   uint32_t chunk_left = 0;
 
+#ifdef SMCRT_DIAG
+  unsigned long long t_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#define DIAG_T(i)                                                   \
+  do {                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    t_acc[(i)] += t_ - t_last;                                      \
+    t_last = t_;                                                    \
+  } while (0)
+#elif defined(SMCRT_ASM_MARKERS)  // analysis builds: phase boundaries visible in the ISA
+#define DIAG_T(i) asm volatile("; @@PHASE " #i)
+#else
+#define DIAG_T(i) do {} while (0)
+#endif
   for (;; ++w_iters) {
+    DIAG_T(8);
     // ---- photon fetch (wave-aggregated work queue) ------------------------------------
     // A wave takes FETCH_CHUNK photon indices per (returning) queue atomic and hands them
     // to its lanes as they free up: a returning atomic waits for all of the wave's
@@ -153,7 +171,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if (__ballot(L.st != ST_IDLE) == 0) break;
     }
 
-#ifdef SMCRT_DIAG
+#ifdef SMCRT_DIAG_STATES
     {
       const uint32_t cls = (L.seg ? 32u : 0u) + (L.st & 31u);
       for (uint32_t c = 0; c < 64; ++c) {  // wave-uniform loop: count lanes per class
@@ -167,6 +185,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 #endif
+    DIAG_T(1);
     // ---- EVAL phase: the SDF array at the lane's query point ----------------------------
     const bool have = !L.seg && L.pend;
     EvalOut R;
@@ -184,6 +203,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if (have) L.pend = false;
     }
 
+    DIAG_T(2);
     // ---- P3: consume the EVAL result ----------------------------------------------------
     if (have) {
       switch (L.st) {
@@ -307,6 +327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    DIAG_T(3);
     // ---- P4: a march step starts its deposit segment, :155-176 -------------------------
     if (!L.seg && L.st == ST_M0) {
       if (!(L.d >= eps)) {
@@ -331,6 +352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    DIAG_T(4);
     // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
     // Placed after the program points that start segments (P3, P4) and before the ones that
     // consume them (P5), so a short segment is started, walked and finished in one trip.
@@ -354,6 +376,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    DIAG_T(5);
     // ---- P5: after a deposit segment: detectors and the next program point -------------
     bool rec = false;
     V3 rec_start = v3(0.0, 0.0, 0.0);
@@ -393,6 +416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       L.st = ST_INTERACT;
     }
 
+    DIAG_T(6);
     // ---- P7: photon events (interaction, tauint2 entry, emission, completion) ----------
     // These are the expensive, rare program points; a wave runs them together once enough
     // lanes wait for one (or nothing else is left), instead of paying for them every trip.
@@ -508,6 +532,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    DIAG_T(7);
     // ---- P8: arrive at the hop-loop head, :61 ---------------------------------------------
     if (!L.seg && L.st == ST_H0 && !L.pend) {
       if (!(L.taurun <= L.tau)) L.st = ST_T2END;
@@ -518,6 +543,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 
   if (binned) close_log(K, C, W, overflow, whist);
 
+#ifdef SMCRT_DIAG
+  if (lane_id == 0)
+    for (int i = 0; i < 9; ++i) atomicAdd(&g_diag_t[i], t_acc[i]);
+#endif
   // ---- per-wave counter reduction ------------------------------------------------------
   unsigned long long* const counters = C->counters;
   if (counters) {
@@ -1009,6 +1038,16 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
     std::fprintf(stderr, "\n");
     std::memset(h, 0, sizeof(h));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), h, sizeof(h)));
+    unsigned long long ht[9];
+    HIPCHK(hipMemcpyFromSymbol(ht, HIP_SYMBOL(g_diag_t), sizeof(ht)));
+    double tt = 0;
+    for (int i = 1; i < 9; ++i) tt += (double)ht[i];
+    const char* nm[9] = {"", "fetch", "eval", "p3", "p4", "dda", "p5p6", "p7", "p8"};
+    std::fprintf(stderr, "[diag-time]");
+    for (int i = 1; i < 9; ++i) std::fprintf(stderr, " %s=%.3f", nm[i], (double)ht[i] / tt);
+    std::fprintf(stderr, "\n");
+    std::memset(ht, 0, sizeof(ht));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_t), ht, sizeof(ht)));
   }
 #endif
   return SMCRT_OK;
