@@ -57,7 +57,7 @@ __device__ unsigned long long g_diag[72];
 __device__ unsigned long long g_diag_t[9];
 #endif
 
-template <bool LDS_FACES, bool P2>
+template <bool LDS_FACES, int GM>
 #ifndef SMCRT_WAVES_PER_EU
 #define SMCRT_WAVES_PER_EU 3
 #endif
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
             else { L.d = (L.tau - L.taurun) / kap; L.pos = L.pos - smul(L.d, L.dir); }
           }
           L.st = ST_H2;
-          start_segment<P2>(K, L, sh, oldpos, L.d);
+          start_segment<GM>(K, L, sh, oldpos, L.d);
           break;
         }
         case ST_H3:  // :133-152
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           if (n1 != n2) { L.st = ST_F0; L.pend = true; break; }
           L.layer = L.new_layer;  // equal n: cross, :318-328
           L.st = ST_X1;
-          start_segment<P2>(K, L, sh, L.pos, L.d);
+          start_segment<GM>(K, L, sh, L.pos, L.d);
           break;
         }
         case ST_F0:  // ds(new), ds(old) at pos (kept in sd/slen: no segment is active)
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
             L.dir = smul(eta, L.dir) + smul(eta * c1 - c2, Nt);
             L.layer = L.new_layer;
             L.st = ST_X1;
-            start_segment<P2>(K, L, sh, L.pos, L.d);
+            start_segment<GM>(K, L, sh, L.pos, L.d);
           }
           break;
         }
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           L.pos = L.pos + smul(L.d, L.dir);
           L.st = ST_B0;
         }
-        start_segment<P2>(K, L, sh, oldpos, L.d);
+        start_segment<GM>(K, L, sh, oldpos, L.d);
       }
     }
 
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
         bool dep = false;
         uint32_t vox = 0;
         double val = 0.0;
-        if (L.seg) dda_step<P2>(K, L, xf, yf, zf, dep, vox, val);
+        if (L.seg) dda_step<GM>(K, L, xf, yf, zf, dep, vox, val);
         w_dep += __popcll(__ballot(dep));
 #ifdef SMCRT_ABL_NO_EMIT  // timing ablation only: deposits are computed but dropped
         if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, C, W, dep, vox, val, overflow, whist); }
@@ -494,13 +494,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           L.fault = false; L.layer = 0;
           LU(LU_STATUS) = 0; LU(LU_NSCATT) = 0; LU(LU_INTER) = 0; LU(LU_BOUNCES) = 0;
           L.xcell = L.ycell = L.zcell = 0;
-          emit<P2>(K, C, L);
+          emit<GM>(K, C, L);
           if (!test_kernel) {
             int64_t tries = 0;
             while (cell_out(K, L)) {
               if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
               LCTR(LC_RETRIES)++;
-              emit<P2>(K, C, L);
+              emit<GM>(K, C, L);
             }
             if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, C->emission, L, 1.0);
           }
@@ -622,7 +622,8 @@ struct smcrt_scene {
   ProgOp* d_prog = nullptr;
   int n_prog = 0;
   double inv2[3] = {0.0, 0.0, 0.0};
-  bool pow2 = false;  // all three inv2 exact: transport_kernel<*, true>
+  int grid_mode = 0;  // transport_kernel<*, GM>: 1 = every 2*max a power of two, 2 = and every n too
+  int32_t fe[3] = {0, 0, 0};
   TopProps* d_props = nullptr;
   double* d_faces = nullptr;
   smcrt_detector* d_dets = nullptr;
@@ -697,8 +698,12 @@ static hipError_t harvest_times(smcrt_scene* s) {
 
 // The transport kernel instantiation for this scene (LDS faces? power-of-two grid?).
 static const void* transport_fn(const smcrt_scene* s) {
-  if (s->lds_faces) return s->pow2 ? (const void*)transport_kernel<true, true> : (const void*)transport_kernel<true, false>;
-  return s->pow2 ? (const void*)transport_kernel<false, true> : (const void*)transport_kernel<false, false>;
+  static const void* const fns[2][3] = {
+      {(const void*)transport_kernel<false, 0>, (const void*)transport_kernel<false, 1>,
+       (const void*)transport_kernel<false, 2>},
+      {(const void*)transport_kernel<true, 0>, (const void*)transport_kernel<true, 1>,
+       (const void*)transport_kernel<true, 2>}};
+  return fns[s->lds_faces ? 1 : 0][s->grid_mode];
 }
 
 // Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
@@ -890,7 +895,19 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     const bool fuse = !(fh && std::string(fh) == "0");
     s->hist_tiles = (fuse && s->n_tiles > 0 && s->n_tiles <= MAX_FUSED_HIST_TILES) ? s->n_tiles : 0;
   }
-  s->pow2 = s->inv2[0] != 0.0 && s->inv2[1] != 0.0 && s->inv2[2] != 0.0;
+  {
+    const bool p2 = s->inv2[0] != 0.0 && s->inv2[1] != 0.0 && s->inv2[2] != 0.0;
+    const int32_t ns[3] = {grid->nx, grid->ny, grid->nz};
+    bool f2 = p2;
+    for (int a = 0; a < 3; ++a) {
+      if ((ns[a] & (ns[a] - 1)) != 0) { f2 = false; continue; }
+      int e2m = 0, en = 0;  // 2*max = 2^(e2m-1), n = 2^(en-1)
+      (void)std::frexp(2.0 * maxes[a], &e2m);
+      (void)std::frexp((double)ns[a], &en);
+      s->fe[a] = e2m - en;  // face k = k * 2*max/n = k * 2^fe
+    }
+    s->grid_mode = f2 ? 2 : (p2 ? 1 : 0);
+  }
   const void* kfn = transport_fn(s);
   hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, s->hist_tiles));
   if (oe != hipSuccess || per_cu < 1) per_cu = 1;
@@ -1062,6 +1079,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.prog = s->d_prog;
   K.n_prog = s->n_prog;
   K.inv2x = s->inv2[0]; K.inv2y = s->inv2[1]; K.inv2z = s->inv2[2];
+  K.fex = s->fe[0]; K.fey = s->fe[1]; K.fez = s->fe[2];
   K.props = s->d_props;
   K.xface = s->d_faces;
   K.yface = s->d_faces + (s->grid.nx + 1);

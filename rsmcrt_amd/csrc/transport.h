@@ -88,6 +88,7 @@ struct KParams {
   double xmax, ymax, zmax;
   // exact reciprocal of 2*max when that is a power of two (else 0): n*p/(2*max) == n*p*inv
   double inv2x, inv2y, inv2z;
+  int32_t fex, fey, fez;  // GM == 2: face k = k * 2^fe (see face())
   uint32_t key0, key1;  // Philox key = seed words
   // binned jmean deposition (deposit.h): record log in chunks
   unsigned long long* rec_pool;  // CHUNK_RECORDS records per chunk; NULL -> fp64 atomics into jmean
@@ -99,22 +100,30 @@ struct KParams {
 
 // ------------------------------------------------------------------ voxels -------
 // update_voxels, inttau2.f90:587-614 (corner coordinates): floor(n*p/(2*max))+1, -1 outside
-// P2: every axis has 2*max a power of two, so the division is an exact multiply (the kernel
+// GM >= 1: every axis has 2*max a power of two, so the division is an exact multiply (the kernel
 // is instantiated for it; the general case keeps a per-axis uniform branch).
-template <bool P2>
+template <int GM>
 __device__ __forceinline__ int32_t cell_of(double p, int32_t n, double max, double inv) {
   const double a = (double)n * p;
-  const double f = floor(P2 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
+  const double f = floor(GM >= 1 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
   if (!(f >= 0.0 && f < (double)n)) return -1;
   return (int32_t)f + 1;
 }
 // get_voxel_cart, grid.f90:51-78 (centred coordinates)
-template <bool P2>
+template <int GM>
 __device__ __forceinline__ int32_t vox_of(double p, int32_t n, double max, double inv) {
   const double a = (double)n * (p + max);
-  const double f = floor(P2 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
+  const double f = floor(GM >= 1 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
   if (!(f >= 0.0 && f < (double)n)) return -1;
   return (int32_t)f + 1;
+}
+
+// Voxel face k (0-based; xface(k+1) of grid.f90:147-157, = ((k*2)*max)/n). GM == 2: both
+// 2*max and n are powers of two, so the face is exactly k * 2^ex and needs no table lookup.
+template <int GM>
+__device__ __forceinline__ double face(const double* __restrict__ f, int32_t k, int32_t ex) {
+  if constexpr (GM == 2) return ldexp((double)k, ex);
+  else return f[k];
 }
 
 __device__ __forceinline__ void atomic_add_nr(double* p, double v) {
@@ -325,7 +334,7 @@ __device__ __forceinline__ void add_cell(const KParams& K, double* g, Lane& L, d
 }
 
 // emit: point photon.f90:311-359 / uniform :566-649 / pencil :652-710
-template <bool P2>
+template <int GM>
 __device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__ C, Lane& L) {
   const smcrt_source& s = C->src;
   if (s.kind == SMCRT_SRC_POINT) {
@@ -356,9 +365,9 @@ __device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__
   }
   L.tflag = false;
   L.weight = 1.0;
-  L.xcell = vox_of<P2>(L.pos.x, K.nx, K.xmax, K.inv2x);
-  L.ycell = vox_of<P2>(L.pos.y, K.ny, K.ymax, K.inv2y);
-  L.zcell = vox_of<P2>(L.pos.z, K.nz, K.zmax, K.inv2z);
+  L.xcell = vox_of<GM>(L.pos.x, K.nx, K.xmax, K.inv2x);
+  L.ycell = vox_of<GM>(L.pos.y, K.ny, K.ymax, K.inv2y);
+  L.zcell = vox_of<GM>(L.pos.z, K.nz, K.zmax, K.inv2z);
 }
 
 // scatter, photon.f90:1045-1103
@@ -399,19 +408,19 @@ __device__ __forceinline__ void scatter(const KParams& K, Lane& L, double hgg) {
 // update_grids entry (inttau2.f90:401-415): start a deposit segment from `p` (centred) of
 // length `dlen` along L.dir; the segment itself runs in the DDA phase. Returns true if the
 // lane must wait for the DDA.
-template <bool P2>
+template <int GM>
 __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneShared* sh, V3 p, double dlen) {
   LCTR(LC_UPD)++;
   V3 old = v3(p.x + K.xmax, p.y + K.ymax, p.z + K.zmax);
-  int32_t ci = cell_of<P2>(old.x, K.nx, K.xmax, K.inv2x), cj = cell_of<P2>(old.y, K.ny, K.ymax, K.inv2y),
-          ck = cell_of<P2>(old.z, K.nz, K.zmax, K.inv2z);
+  int32_t ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x), cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y),
+          ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z);
   L.xcell = ci; L.ycell = cj; L.zcell = ck;
   if (!(K.flags & SMCRT_FLAG_PATHLENGTH)) {  // :446-463
     old.x = old.x + L.dir.x * dlen;
     old.y = old.y + L.dir.y * dlen;
     old.z = old.z + L.dir.z * dlen;
-    ci = cell_of<P2>(old.x, K.nx, K.xmax, K.inv2x); cj = cell_of<P2>(old.y, K.ny, K.ymax, K.inv2y);
-    ck = cell_of<P2>(old.z, K.nz, K.zmax, K.inv2z);
+    ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x); cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y);
+    ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z);
     if (ci == -1 || cj == -1 || ck == -1) L.tflag = true;
     L.xcell = ci; L.ycell = cj; L.zcell = ck;
     return false;
@@ -424,7 +433,7 @@ __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneSha
 
 // One voxel crossing of the pending segment: wall_dist + deposit + update_pos
 // (inttau2.f90:417-441, 467-584). Clears L.seg when the segment ends.
-template <bool P2>
+template <int GM>
 __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double* __restrict__ xf,
                                          const double* __restrict__ yf, const double* __restrict__ zf,
                                          bool& dep, uint32_t& dep_vox, double& dep_val) {
@@ -438,9 +447,13 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
     // is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
     // or negative distances, NaN), all three are divided exactly as the reference does.
     // Both paths give the reference's dcell and ldir bit for bit.
-    const double nx = (dir.x > 0.0 ? xf[L.ci] : xf[L.ci - 1]) - L.old.x;
-    const double ny = (dir.y > 0.0 ? yf[L.cj] : yf[L.cj - 1]) - L.old.y;
-    const double nz = (dir.z > 0.0 ? zf[L.ck] : zf[L.ck - 1]) - L.old.z;
+    // the wall each axis moves towards: xface(ci+1) going +, xface(ci) going - (0-based here)
+    const double fx = face<GM>(xf, dir.x > 0.0 ? L.ci : L.ci - 1, K.fex);
+    const double fy = face<GM>(yf, dir.y > 0.0 ? L.cj : L.cj - 1, K.fey);
+    const double fz = face<GM>(zf, dir.z > 0.0 ? L.ck : L.ck - 1, K.fez);
+    const double nx = fx - L.old.x;
+    const double ny = fy - L.old.y;
+    const double nz = fz - L.old.z;
     const double ax = dir.x == 0.0 ? 100000.0 : nx * __builtin_amdgcn_rcp(dir.x);
     const double ay = dir.y == 0.0 ? 100000.0 : ny * __builtin_amdgcn_rcp(dir.y);
     const double az = dir.z == 0.0 ? 100000.0 : nz * __builtin_amdgcn_rcp(dir.z);
@@ -457,14 +470,11 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
       lx = mx; ly = my; lz = !mx && !my;
     } else {
       double dx = -999.0, dy = -999.0, dz = -999.0;
-      if (dir.x > 0.0) dx = (xf[L.ci] - L.old.x) / dir.x;
-      else if (dir.x < 0.0) dx = (xf[L.ci - 1] - L.old.x) / dir.x;
+      if (dir.x > 0.0 || dir.x < 0.0) dx = nx / dir.x;
       else if (dir.x == 0.0) dx = 100000.0;
-      if (dir.y > 0.0) dy = (yf[L.cj] - L.old.y) / dir.y;
-      else if (dir.y < 0.0) dy = (yf[L.cj - 1] - L.old.y) / dir.y;
+      if (dir.y > 0.0 || dir.y < 0.0) dy = ny / dir.y;
       else if (dir.y == 0.0) dy = 100000.0;
-      if (dir.z > 0.0) dz = (zf[L.ck] - L.old.z) / dir.z;
-      else if (dir.z < 0.0) dz = (zf[L.ck - 1] - L.old.z) / dir.z;
+      if (dir.z > 0.0 || dir.z < 0.0) dz = nz / dir.z;
       else if (dir.z == 0.0) dz = 100000.0;
       dcell = dmin(dmin(dx, dy), dz);
       lx = (dcell == dx); ly = (dcell == dy); lz = (dcell == dz);
@@ -493,16 +503,16 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
         // as selects over the same expressions, so `old` stays in registers.
         const double delta = 1e-8;  // local delta, :393
         const double ax = L.old.x + dir.x * dcell, ay = L.old.y + dir.y * dcell, az = L.old.z + dir.z * dcell;
-        const double sx = dir.x > 0.0 ? xf[L.ci] + delta : (dir.x < 0.0 ? xf[L.ci - 1] - delta : L.old.x);
-        const double sy = dir.y > 0.0 ? yf[L.cj] + delta : (dir.y < 0.0 ? yf[L.cj - 1] - delta : L.old.y);
-        const double sz = dir.z > 0.0 ? zf[L.ck] + delta : (dir.z < 0.0 ? zf[L.ck - 1] - delta : L.old.z);
+        const double sx = dir.x > 0.0 ? fx + delta : (dir.x < 0.0 ? fx - delta : L.old.x);
+        const double sy = dir.y > 0.0 ? fy + delta : (dir.y < 0.0 ? fy - delta : L.old.y);
+        const double sz = dir.z > 0.0 ? fz + delta : (dir.z < 0.0 ? fz - delta : L.old.z);
         const bool snx = lx, sny = !lx && ly, snz = !lx && !ly;
         L.old.x = snx ? sx : ax;
         L.old.y = sny ? sy : ay;
         L.old.z = snz ? sz : az;
-        L.ci = cell_of<P2>(L.old.x, K.nx, K.xmax, K.inv2x);
-        L.cj = cell_of<P2>(L.old.y, K.ny, K.ymax, K.inv2y);
-        L.ck = cell_of<P2>(L.old.z, K.nz, K.zmax, K.inv2z);
+        L.ci = cell_of<GM>(L.old.x, K.nx, K.xmax, K.inv2x);
+        L.cj = cell_of<GM>(L.old.y, K.ny, K.ymax, K.inv2y);
+        L.ck = cell_of<GM>(L.old.z, K.nz, K.zmax, K.inv2z);
         if (L.ci == -1 || L.cj == -1 || L.ck == -1) { L.tflag = true; done = true; }
       }
     }
