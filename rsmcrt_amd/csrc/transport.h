@@ -36,7 +36,7 @@ constexpr int MAX_RENORM_ITERS = 64;
 constexpr int64_t MAX_INTERACTIONS = 100000000;
 
 #ifndef SMCRT_DDA_PER_ITER
-#define SMCRT_DDA_PER_ITER 2
+#define SMCRT_DDA_PER_ITER 3
 #endif
 // A wave runs the photon-event phase once this many lanes wait for it (or no lane has
 // anything else to do).
