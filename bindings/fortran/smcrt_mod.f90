@@ -155,6 +155,41 @@ module smcrt_mod
             type(smcrt_kernel_times), intent(out) :: times
         end function smcrt_scene_kernel_times
 
+        integer(c_int) function smcrt_write_data_f32(filename, array, nx, ny, nz, metadata, dect_id, overwrite, &
+                                                     written_path, path_cap) bind(C, name="smcrt_write_data_f32")
+            import :: c_int, c_int32_t, c_char, c_float, c_ptr
+            character(kind=c_char), intent(in) :: filename(*)
+            real(c_float), intent(in)          :: array(*)
+            integer(c_int32_t), value          :: nx, ny, nz
+            type(c_ptr), value                 :: metadata, dect_id   ! C strings or c_null_ptr
+            integer(c_int32_t), value          :: overwrite
+            type(c_ptr), value                 :: written_path
+            integer(c_int32_t), value          :: path_cap
+        end function smcrt_write_data_f32
+
+        integer(c_int) function smcrt_write_detector(filename, d, data, id, nphotons) &
+                bind(C, name="smcrt_write_detector")
+            import :: c_int, c_int64_t, c_char, c_double, smcrt_detector
+            character(kind=c_char), intent(in) :: filename(*)
+            type(smcrt_detector), intent(in)   :: d
+            real(c_double), intent(in)         :: data(*)
+            character(kind=c_char), intent(in) :: id(*)
+            integer(c_int64_t), value          :: nphotons
+        end function smcrt_write_detector
+
+        integer(c_int) function smcrt_write_checkpoint(filename, toml_filename, photons_run, jmean, grid, &
+                                                       overwrite, written_path, path_cap) &
+                bind(C, name="smcrt_write_checkpoint")
+            import :: c_int, c_int32_t, c_int64_t, c_char, c_float, c_ptr, smcrt_grid
+            character(kind=c_char), intent(in) :: filename(*), toml_filename(*)
+            integer(c_int64_t), value          :: photons_run
+            real(c_float), intent(in)          :: jmean(*)
+            type(smcrt_grid), intent(in)       :: grid
+            integer(c_int32_t), value          :: overwrite
+            type(c_ptr), value                 :: written_path
+            integer(c_int32_t), value          :: path_cap
+        end function smcrt_write_checkpoint
+
         integer(c_int) function smcrt_normalise_fluence(grid_data, grid, nphotons) &
                 bind(C, name="smcrt_normalise_fluence")
             import :: c_int, c_int64_t, c_float, smcrt_grid

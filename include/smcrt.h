@@ -286,6 +286,40 @@ int smcrt_scene_kernel_times(smcrt_scene* scene, smcrt_kernel_times* out);
  * i.e. (8*xmax*ymax*zmax)/(nphotons*dx*dy*dz). Host-side helper on an fp32 grid. */
 int smcrt_normalise_fluence(float* grid, const smcrt_grid* g, uint64_t nphotons);
 
+/* ---- output formats (src/writer.f90), host-side, no GPU needed ------------------------
+ * Written byte for byte as the reference writes them, so its readers
+ * (tools/read_nrrd_class.py, tools/plotDetectorsClass.py) load them unchanged. If the
+ * target exists and `overwrite` is 0, " (i)" is inserted before the extension
+ * (get_new_file_name, writer.f90:273-291); the name used is copied to `written_path`
+ * (may be NULL) when it fits in `path_cap` bytes. */
+
+/* write_data (writer.f90:162-226) for an fp32 / fp64 volume of nx*ny*nz values in Fortran
+ * order, chosen by extension:
+ *   .nrrd: NRRD0004 header (write_hdr :300-327; "sizes: nz ny nx"), the optional `metadata`
+ *          text (the reference's toml_dump of its dict), a blank line, then the raw data;
+ *   .raw / .dat: the raw data only (write_3d_r4_raw / _r8_raw :228-271);
+ *   anything else: SMCRT_ERR_UNSUPPORTED ("File type not supported!").
+ * `dect_id` (may be NULL) adds the "dector: <ID>" line of the escape-function files. */
+int smcrt_write_data_f32(const char* filename, const float* array, int32_t nx, int32_t ny, int32_t nz,
+                         const char* metadata, const char* dect_id, int32_t overwrite,
+                         char* written_path, int32_t path_cap);
+int smcrt_write_data_f64(const char* filename, const double* array, int32_t nx, int32_t ny, int32_t nz,
+                         const char* metadata, const char* dect_id, int32_t overwrite,
+                         char* written_path, int32_t path_cap);
+
+/* write_detected_photons (writer.f90:55-138) for one detector: an fp64 stream of type
+ * (1 circle, 2 fibre, 3 annulus), len(ID), the ID characters, nphotons, the geometry, then
+ * (bin centre, value) for each of d->nbins bins. A camera gives an empty file, as in the
+ * reference. The file is replaced if it exists (status='REPLACE'). */
+int smcrt_write_detector(const char* filename, const smcrt_detector* d, const double* data,
+                         const char* id, int64_t nphotons);
+
+/* checkpoint (writer.f90:419-455): "tomlfile=<toml_filename>", "photons_run=<n>", then
+ * jmean (fp32, nx*ny*nz, Fortran order) raw. */
+int smcrt_write_checkpoint(const char* filename, const char* toml_filename, int64_t photons_run,
+                           const float* jmean, const smcrt_grid* g, int32_t overwrite,
+                           char* written_path, int32_t path_cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -134,4 +134,5 @@ EXPORTED_SYMBOLS = [
     "smcrt_abi_version", "smcrt_device_count", "smcrt_last_error", "smcrt_scene_create",
     "smcrt_scene_destroy", "smcrt_scene_det_bins", "smcrt_scene_set_optprops", "smcrt_run",
     "smcrt_run_device", "smcrt_normalise_fluence", "smcrt_scene_set_timing", "smcrt_scene_kernel_times",
+    "smcrt_write_data_f32", "smcrt_write_data_f64", "smcrt_write_detector", "smcrt_write_checkpoint",
 ]

@@ -20,6 +20,7 @@
 #include "../../include/smcrt.h"
 #include "transport.h"
 #include "deposit.h"
+#include "hosterr.h"
 
 using namespace smcrt;
 
@@ -581,14 +582,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 }
 
 // ------------------------------------------------------------------ host side ------
+thread_local std::string smcrt::g_last_error;
+
 namespace {
 
-thread_local std::string g_err;
-
-int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
-}
+int fail(int code, const std::string& msg) { return set_error(code, msg); }
 
 #define HIPCHK(expr)                                                                              \
   do {                                                                                            \
@@ -725,7 +723,7 @@ extern "C" {
 
 int smcrt_abi_version(void) { return SMCRT_ABI_VERSION; }
 
-const char* smcrt_last_error(void) { return g_err.c_str(); }
+const char* smcrt_last_error(void) { return g_last_error.c_str(); }
 
 int smcrt_device_count(int32_t* count) {
   if (!count) return fail(SMCRT_ERR_INVALID_ARG, "count is NULL");
@@ -757,7 +755,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
 int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t* top, int32_t n_top,
                        const smcrt_grid* grid, const smcrt_detector* dets, int32_t n_dets, int32_t device,
                        smcrt_scene** out) {
-  g_err.clear();
+  g_last_error.clear();
   if (!out) return fail(SMCRT_ERR_INVALID_ARG, "out is NULL");
   *out = nullptr;
   if (!nodes || n_nodes < 1 || !top || n_top < 1 || !grid || n_dets < 0 || (n_dets > 0 && !dets))
@@ -815,9 +813,9 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   for (int32_t i = 0; i < grid->nz + 2; ++i) faces.push_back((double)i * 2.0 * grid->zmax / (double)grid->nz);
 
   auto cleanup_fail = [&](int code) {
-    std::string msg = g_err;
+    std::string msg = g_last_error;
     smcrt_scene_destroy(s);
-    g_err = msg;
+    g_last_error = msg;
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, "hipSetDevice failed"));
@@ -1145,7 +1143,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
 
 int smcrt_run_device(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg,
                      smcrt_device_tallies* dev, void* stream) {
-  g_err.clear();
+  g_last_error.clear();
   if (!s || !src || !cfg || !dev) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> g(s->mu);
   HIPCHK(hipSetDevice(s->device));
@@ -1153,7 +1151,7 @@ int smcrt_run_device(smcrt_scene* s, const smcrt_source* src, const smcrt_run_co
 }
 
 int smcrt_run(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io) {
-  g_err.clear();
+  g_last_error.clear();
   if (!s || !src || !cfg || !io) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> g(s->mu);
   HIPCHK(hipSetDevice(s->device));
