@@ -320,6 +320,49 @@ int smcrt_write_checkpoint(const char* filename, const char* toml_filename, int6
                            const float* jmean, const smcrt_grid* g, int32_t overwrite,
                            char* written_path, int32_t path_cap);
 
+/* ---- TOML front end (src/parse/parse*.f90, src/setup.f90, src/setupGeometry.f90) --------
+ * smcrt_job_load reads a res/<name>.toml file with the reference's keys, defaults and error
+ * messages. It builds the scene the way setup_simulation does and keeps the output and
+ * simulation settings.
+ *   Geometries: sphere, box, test_box, scat_test, scat_test2, aptran, sphere_scene, exp, omg.
+ *     vessels (needs data files the reference does not ship), egg and logo return
+ *     SMCRT_ERR_UNSUPPORTED.
+ *   Sources: point, uniform, pencil; a constant spectrum.
+ *   Detectors: circle, annulus, camera, grouped by type as parse_detectors does.
+ * Build-defined: sphere_scene's sphere list, which the reference draws from an unseeded
+ * compiler RNG (setupGeometry.f90:285-292). Here draw d is Philox4x32-10 of counter
+ * (d, 0x5350, 0, 0) under key iseed. */
+typedef struct smcrt_job smcrt_job;
+
+typedef struct smcrt_job_desc {
+  int64_t n_photons;  /* [source] nphotons */
+  int64_t seed;       /* [simulation] iseed */
+  int32_t flags;      /* SMCRT_FLAG_PATHLENGTH | RENDER_SOURCE as configured */
+  int32_t n_nodes, n_top, n_dets;
+  int32_t overwrite;  /* [output] overwrite */
+  smcrt_grid grid;
+  smcrt_source source;
+  char experiment[64];  /* geom_name */
+  char source_name[32];
+} smcrt_job_desc;
+
+int smcrt_job_load(const char* toml_path, smcrt_job** out);
+void smcrt_job_destroy(smcrt_job* job);
+int smcrt_job_info(const smcrt_job* job, smcrt_job_desc* desc);
+/* Copies the flattened scene (desc.n_nodes nodes, desc.n_top top-level indices) and the
+ * detectors (desc.n_dets) into caller arrays. */
+int smcrt_job_scene(const smcrt_job* job, smcrt_sdf_node* nodes, int32_t* top, smcrt_detector* dets);
+/* The metadata dict (the values parse_* and finalise set) as TOML text, for NRRD headers. */
+int smcrt_job_metadata(const smcrt_job* job, char* buf, int32_t cap);
+/* default_MCRT (kernelsMod.f90:14-82) without checkpoint loading: run_MCRT on `device`, then
+ * finalise (:2321-2416). Writes, under outdir (the reference's fileplace):
+ *   jmean/<fluence>, normalised;
+ *   emission/<render_source_name>, normalised;
+ *   absorb/absorb.nrrd;
+ *   detectors/detector_<i>.dat.
+ * `nscatt` (may be NULL) receives the total scatter count. */
+int smcrt_job_run(smcrt_job* job, int32_t device, const char* outdir, double* nscatt);
+
 #ifdef __cplusplus
 }
 #endif

@@ -125,6 +125,12 @@ def record_dtype():
                      ("status", "<u4")])
 
 
+class JobDesc(C.Structure):
+    _fields_ = [("n_photons", C.c_int64), ("seed", C.c_int64), ("flags", C.c_int32), ("n_nodes", C.c_int32),
+                ("n_top", C.c_int32), ("n_dets", C.c_int32), ("overwrite", C.c_int32), ("grid", Grid),
+                ("source", Source), ("experiment", C.c_char * 64), ("source_name", C.c_char * 32)]
+
+
 class KernelTimes(C.Structure):
     _fields_ = [("transport_ms", C.c_double), ("deposit_ms", C.c_double), ("launches", C.c_int64),
                 ("reserved", C.c_int64)]
@@ -135,4 +141,5 @@ EXPORTED_SYMBOLS = [
     "smcrt_scene_destroy", "smcrt_scene_det_bins", "smcrt_scene_set_optprops", "smcrt_run",
     "smcrt_run_device", "smcrt_normalise_fluence", "smcrt_scene_set_timing", "smcrt_scene_kernel_times",
     "smcrt_write_data_f32", "smcrt_write_data_f64", "smcrt_write_detector", "smcrt_write_checkpoint",
+    "smcrt_job_load", "smcrt_job_destroy", "smcrt_job_info", "smcrt_job_scene", "smcrt_job_metadata", "smcrt_job_run",
 ]

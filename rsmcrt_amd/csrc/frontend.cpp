@@ -1,0 +1,717 @@
+// frontend.cpp — TOML front end: res/*.toml -> scene, grid, source,
+// detectors and run settings, then default_MCRT's run + finalise through the engine.
+//
+// Restates, with the reference's defaults and error cases:
+//   parse_params / parse_grid / parse_output / parse_simulation   src/parse/parse.f90:20-186
+//   parse_source                                                  src/parse/parse_source.f90:17-264
+//   parse_geometry (values into the metadata dict)                src/parse/parse_geometry.f90:17-292
+//   parse_detectors (grouped circle, annulus, fibre, camera)      src/parse/parse_detectors.f90:17-349
+//   setup_simulation + the geometry builders                      src/setup.f90:14-62, src/setupGeometry.f90
+//   default_MCRT / finalise                                       src/kernelsMod.f90:14-82, 2321-2416
+// Host code only; part of libsmcrt.so's C ABI (include/smcrt.h).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <sys/stat.h>
+#include <vector>
+
+#include "../../include/smcrt.h"
+#include "hosterr.h"
+#include "toml.h"
+
+using smcrt::toml::Table;
+using smcrt::toml::Value;
+namespace T = smcrt::toml;
+
+namespace {
+
+int ffail(int code, const std::string& m) { return smcrt::set_error(code, m); }
+
+// ---------------------------------------------------------------- 4x4 transforms ---
+// m[r][c] = Fortran t(r+1, c+1); stored column-major in smcrt_sdf_node.transform.
+struct M4 {
+  double m[4][4];
+};
+
+M4 identity() {
+  M4 a{};
+  for (int i = 0; i < 4; ++i) a.m[i][i] = 1.0;
+  return a;
+}
+
+M4 translate(double x, double y, double z) {  // sdfHelpers.f90:160-171: row 4 holds o
+  M4 a = identity();
+  a.m[3][0] = x; a.m[3][1] = y; a.m[3][2] = z;
+  return a;
+}
+
+M4 rotate_y(double angle) {  // sdfHelpers.f90:33-50, deg2rad(a) = a*pi/180
+  const double r = angle * M_PI / 180.0, c = std::cos(r), s = std::sin(r);
+  M4 a{};
+  // columns (c,0,s,0) (0,1,0,0) (-s,0,c,0) (0,0,0,1)
+  a.m[0][0] = c;  a.m[1][0] = 0; a.m[2][0] = s;  a.m[3][0] = 0;
+  a.m[0][1] = 0;  a.m[1][1] = 1; a.m[2][1] = 0;  a.m[3][1] = 0;
+  a.m[0][2] = -s; a.m[1][2] = 0; a.m[2][2] = c;  a.m[3][2] = 0;
+  a.m[0][3] = 0;  a.m[1][3] = 0; a.m[2][3] = 0;  a.m[3][3] = 1;
+  return a;
+}
+
+// Direct 4x4 inverse, term for term as mat_class.f90:154-207.
+M4 invert(const M4& A) {
+  auto a = [&](int i, int j) { return A.m[i - 1][j - 1]; };
+  const double detinv =
+      1.0 / (a(1, 1) * (a(2, 2) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(2, 3) * (a(3, 4) * a(4, 2) - a(3, 2) * a(4, 4)) +
+                        a(2, 4) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2))) -
+             a(1, 2) * (a(2, 1) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(2, 3) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) +
+                        a(2, 4) * (a(3, 1) * a(4, 3) - a(3, 3) * a(4, 1))) +
+             a(1, 3) * (a(2, 1) * (a(3, 2) * a(4, 4) - a(3, 4) * a(4, 2)) + a(2, 2) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) +
+                        a(2, 4) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1))) -
+             a(1, 4) * (a(2, 1) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2)) + a(2, 2) * (a(3, 3) * a(4, 1) - a(3, 1) * a(4, 3)) +
+                        a(2, 3) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1))));
+  M4 B{};
+  B.m[0][0] = detinv * (a(2, 2) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(2, 3) * (a(3, 4) * a(4, 2) - a(3, 2) * a(4, 4)) + a(2, 4) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2)));
+  B.m[1][0] = detinv * (a(2, 1) * (a(3, 4) * a(4, 3) - a(3, 3) * a(4, 4)) + a(2, 3) * (a(3, 1) * a(4, 4) - a(3, 4) * a(4, 1)) + a(2, 4) * (a(3, 3) * a(4, 1) - a(3, 1) * a(4, 3)));
+  B.m[2][0] = detinv * (a(2, 1) * (a(3, 2) * a(4, 4) - a(3, 4) * a(4, 2)) + a(2, 2) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) + a(2, 4) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1)));
+  B.m[3][0] = detinv * (a(2, 1) * (a(3, 3) * a(4, 2) - a(3, 2) * a(4, 3)) + a(2, 2) * (a(3, 1) * a(4, 3) - a(3, 3) * a(4, 1)) + a(2, 3) * (a(3, 2) * a(4, 1) - a(3, 1) * a(4, 2)));
+  B.m[0][1] = detinv * (a(1, 2) * (a(3, 4) * a(4, 3) - a(3, 3) * a(4, 4)) + a(1, 3) * (a(3, 2) * a(4, 4) - a(3, 4) * a(4, 2)) + a(1, 4) * (a(3, 3) * a(4, 2) - a(3, 2) * a(4, 3)));
+  B.m[1][1] = detinv * (a(1, 1) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(1, 3) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) + a(1, 4) * (a(3, 1) * a(4, 3) - a(3, 3) * a(4, 1)));
+  B.m[2][1] = detinv * (a(1, 1) * (a(3, 4) * a(4, 2) - a(3, 2) * a(4, 4)) + a(1, 2) * (a(3, 1) * a(4, 4) - a(3, 4) * a(4, 1)) + a(1, 4) * (a(3, 2) * a(4, 1) - a(3, 1) * a(4, 2)));
+  B.m[3][1] = detinv * (a(1, 1) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2)) + a(1, 2) * (a(3, 3) * a(4, 1) - a(3, 1) * a(4, 3)) + a(1, 3) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1)));
+  B.m[0][2] = detinv * (a(1, 2) * (a(2, 3) * a(4, 4) - a(2, 4) * a(4, 3)) + a(1, 3) * (a(2, 4) * a(4, 2) - a(2, 2) * a(4, 4)) + a(1, 4) * (a(2, 2) * a(4, 3) - a(2, 3) * a(4, 2)));
+  B.m[1][2] = detinv * (a(1, 1) * (a(2, 4) * a(4, 3) - a(2, 3) * a(4, 4)) + a(1, 3) * (a(2, 1) * a(4, 4) - a(2, 4) * a(4, 1)) + a(1, 4) * (a(2, 3) * a(4, 1) - a(2, 1) * a(4, 3)));
+  B.m[2][2] = detinv * (a(1, 1) * (a(2, 2) * a(4, 4) - a(2, 4) * a(4, 2)) + a(1, 2) * (a(2, 4) * a(4, 1) - a(2, 1) * a(4, 4)) + a(1, 4) * (a(2, 1) * a(4, 2) - a(2, 2) * a(4, 1)));
+  B.m[3][2] = detinv * (a(1, 1) * (a(2, 3) * a(4, 2) - a(2, 2) * a(4, 3)) + a(1, 2) * (a(2, 1) * a(4, 3) - a(2, 3) * a(4, 1)) + a(1, 3) * (a(2, 2) * a(4, 1) - a(2, 1) * a(4, 2)));
+  B.m[0][3] = detinv * (a(1, 2) * (a(2, 4) * a(3, 3) - a(2, 3) * a(3, 4)) + a(1, 3) * (a(2, 2) * a(3, 4) - a(2, 4) * a(3, 2)) + a(1, 4) * (a(2, 3) * a(3, 2) - a(2, 2) * a(3, 3)));
+  B.m[1][3] = detinv * (a(1, 1) * (a(2, 3) * a(3, 4) - a(2, 4) * a(3, 3)) + a(1, 3) * (a(2, 4) * a(3, 1) - a(2, 1) * a(3, 4)) + a(1, 4) * (a(2, 1) * a(3, 3) - a(2, 3) * a(3, 1)));
+  B.m[2][3] = detinv * (a(1, 1) * (a(2, 4) * a(3, 2) - a(2, 2) * a(3, 4)) + a(1, 2) * (a(2, 1) * a(3, 4) - a(2, 4) * a(3, 1)) + a(1, 4) * (a(2, 2) * a(3, 1) - a(2, 1) * a(3, 2)));
+  B.m[3][3] = detinv * (a(1, 1) * (a(2, 2) * a(3, 3) - a(2, 3) * a(3, 2)) + a(1, 2) * (a(2, 3) * a(3, 1) - a(2, 1) * a(3, 3)) + a(1, 3) * (a(2, 1) * a(3, 2) - a(2, 2) * a(3, 1)));
+  return B;
+}
+
+// ---------------------------------------------------------------- SDF nodes --------
+struct Mono {  // init_mono inputs, opticalProperties.f90:107-125
+  double mus, mua, hgg, n;
+};
+
+struct Prim {  // one sdfs.f90 constructor call, or a model (children)
+  int32_t kind = 0;
+  int32_t layer = 0;
+  Mono opt{0, 0, 0, 1};
+  std::vector<double> param;
+  M4 t = identity();
+  int32_t op = SMCRT_OP_UNION;
+  double k = 0.0;
+  std::vector<Prim> children;
+};
+
+Prim prim(int32_t kind, std::vector<double> param, Mono opt, int32_t layer, const M4& t = identity()) {
+  Prim p;
+  p.kind = kind; p.param = std::move(param); p.opt = opt; p.layer = layer; p.t = t;
+  return p;
+}
+Prim sphere(double r, Mono o, int32_t layer, const M4& t = identity()) { return prim(SMCRT_SDF_SPHERE, {r}, o, layer, t); }
+Prim box(double x, double y, double z, Mono o, int32_t layer, const M4& t = identity()) {
+  return prim(SMCRT_SDF_BOX, {0.5 * x, 0.5 * y, 0.5 * z}, o, layer, t);  // box_init halves, sdfs.f90:455
+}
+Prim cylinder(const double a[3], const double b[3], double r, Mono o, int32_t layer, const M4& t = identity()) {
+  return prim(SMCRT_SDF_CYLINDER, {a[0], a[1], a[2], b[0], b[1], b[2], r}, o, layer, t);
+}
+
+smcrt_sdf_node to_node(const Prim& p) {
+  smcrt_sdf_node nd;
+  std::memset(&nd, 0, sizeof(nd));
+  nd.kind = p.kind;
+  nd.layer = p.layer;
+  for (int c = 0; c < 4; ++c)
+    for (int r = 0; r < 4; ++r) nd.transform[c * 4 + r] = p.t.m[r][c];
+  for (size_t i = 0; i < p.param.size() && i < 12; ++i) nd.param[i] = p.param[i];
+  nd.mus = p.opt.mus; nd.mua = p.opt.mua; nd.hgg = p.opt.hgg; nd.n = p.opt.n;
+  nd.op = p.op;
+  nd.k = p.k;
+  return nd;
+}
+
+// Flatten the sdfs_array like rsmcrt_amd.scene.Scene: top-level nodes first, then children.
+void flatten(const std::vector<Prim>& sdfs, std::vector<smcrt_sdf_node>& nodes, std::vector<int32_t>& top) {
+  nodes.clear(); top.clear();
+  std::vector<std::pair<int32_t, const Prim*>> pending;
+  for (const Prim& s : sdfs) {
+    top.push_back((int32_t)nodes.size());
+    pending.push_back({(int32_t)nodes.size(), &s});
+    nodes.push_back(smcrt_sdf_node{});
+  }
+  for (size_t q = 0; q < pending.size(); ++q) {
+    const int32_t idx = pending[q].first;
+    const Prim& s = *pending[q].second;
+    if (s.kind == SMCRT_SDF_MODEL) {
+      smcrt_sdf_node nd = to_node(s);
+      nd.layer = s.children.front().layer;  // a model takes layer and optics of array(1)
+      nd.mus = s.children.front().opt.mus; nd.mua = s.children.front().opt.mua;
+      nd.hgg = s.children.front().opt.hgg; nd.n = s.children.front().opt.n;
+      nd.first_child = (int32_t)nodes.size();
+      nd.n_children = (int32_t)s.children.size();
+      for (const Prim& ch : s.children) {
+        pending.push_back({(int32_t)nodes.size(), &ch});
+        nodes.push_back(smcrt_sdf_node{});
+      }
+      nodes[idx] = nd;
+    } else {
+      nodes[idx] = to_node(s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- job ---------------
+struct DictEntry {
+  std::string key, value;  // value already in TOML syntax
+};
+
+std::string fmt_real(double v) {  // shortest text that reads back as v, like Python's repr
+  char b[64];
+  int prec = 1;
+  for (; prec <= 17; ++prec) {
+    std::snprintf(b, sizeof b, "%.*g", prec, v);
+    if (std::strtod(b, nullptr) == v) break;
+  }
+  const double a = std::fabs(v);
+  if (std::strchr(b, 'e') && a >= 1e-4 && a < 1e16) {
+    const int decimals = std::max(0, prec - 1 - (int)std::floor(std::log10(a)));
+    std::snprintf(b, sizeof b, "%.*f", decimals, v);
+  }
+  std::string s(b);
+  if (s.find_first_of(".eEn") == std::string::npos) s += ".0";
+  return s;
+}
+std::string fmt_str(const std::string& v) { return "\"" + v + "\""; }
+std::string i4(int i) {  // Fortran '(I4)'
+  char b[16];
+  std::snprintf(b, sizeof b, "%4d", i);
+  return b;
+}
+
+}  // namespace
+
+struct smcrt_job {
+  std::string toml_path;
+  std::string source_name, experiment;
+  int64_t nphotons = 1000000;
+  int64_t iseed = 123456789;
+  smcrt_grid grid{};
+  smcrt_source src{};
+  std::vector<smcrt_sdf_node> nodes;
+  std::vector<int32_t> top;
+  std::vector<smcrt_detector> dets;
+  std::vector<std::string> det_ids;
+  // [output]
+  std::string outfile = "fluence.nrrd", outfile_absorb = "absorb.nrrd", rendersourcefile = "source_render.nrrd";
+  bool render_source = false, overwrite = false;
+  // [simulation]
+  bool absorb = false, tev = false, loadckpt = false;
+  std::string ckptfile = "check.ckpt";
+  int64_t ckptfreq = 1000000;
+  std::vector<DictEntry> dict;  // metadata written into the NRRD headers (toml_dump)
+
+  void set(const std::string& k, const std::string& v) {
+    for (auto& e : dict)
+      if (e.key == k) { e.value = v; return; }
+    dict.push_back({k, v});
+  }
+  bool has(const std::string& k) const {
+    for (auto& e : dict)
+      if (e.key == k) return true;
+    return false;
+  }
+  double real(const std::string& k) const {
+    for (auto& e : dict)
+      if (e.key == k) return std::strtod(e.value.c_str(), nullptr);
+    return 0.0;
+  }
+  std::string dump() const {
+    std::string s;
+    for (auto& e : dict) {
+      bool bare = true;
+      for (char c : e.key) bare = bare && (std::isalnum((unsigned char)c) || c == '_' || c == '-');
+      s += (bare ? e.key : "\"" + e.key + "\"") + " = " + e.value + "\n";
+    }
+    return s;
+  }
+};
+
+namespace {
+
+struct Fail : std::runtime_error {
+  int code;
+  Fail(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+// get_vector, parse_helpers.f90:15-45
+bool get_vector(const Table* t, const std::string& key, double out[3]) {
+  const Value* v = T::find(t, key);
+  if (!v) return false;
+  if (v->kind != Value::ARRAY || v->arr.size() != 3) throw Fail(SMCRT_ERR_INVALID_ARG, "Expected vector of size 3 for " + key);
+  for (int i = 0; i < 3; ++i) {
+    if (!v->arr[i].is_number()) throw Fail(SMCRT_ERR_INVALID_ARG, "Expected numbers in " + key);
+    out[i] = v->arr[i].number();
+  }
+  return true;
+}
+
+// Fill a 3-vector of `key` into the dict as key%   i (the reference's '(I4)' keys); default
+// value d when absent. Returns the values.
+void dict_vec3(smcrt_job& J, const Table* g, const std::string& tomlkey, const std::string& dictkey, double d,
+               double out[3]) {
+  const Value* v = T::find(g, tomlkey);
+  if (v) {
+    if (v->kind != Value::ARRAY || v->arr.size() != 3) throw Fail(SMCRT_ERR_INVALID_ARG, "Need a vector of size 3 for " + tomlkey);
+    for (int i = 0; i < 3; ++i) out[i] = v->arr[i].number();
+  } else {
+    out[0] = out[1] = out[2] = d;
+  }
+  for (int i = 0; i < 3; ++i) J.set(dictkey + "%" + i4(i + 1), fmt_real(out[i]));
+}
+
+void parse_source(smcrt_job& J, const Table* root) {  // parse_source.f90:17-264
+  const Table* s = T::get_table(root, "source");
+  if (!s) throw Fail(SMCRT_ERR_INVALID_ARG, "Simulation needs Source table");
+  J.source_name = T::get_string(s, "name", "point");
+  J.nphotons = T::get_int(s, "nphotons", 1000000);
+  double pos[3] = {0, 0, 0}, dir[3] = {0, 0, 0};
+  const std::string& nm = J.source_name;
+  if (nm != "uniform" && !get_vector(s, "position", pos)) throw Fail(SMCRT_ERR_INVALID_ARG, "Expected vector of size 3 for position");
+  if (nm != "point" && nm != "uniform" && nm != "pencil")
+    throw Fail(SMCRT_ERR_UNSUPPORTED, "source '" + nm + "' is not supported by the engine (point, uniform, pencil)");
+  // direction: a vector, or a cardinal name. A vector makes the reference return early
+  // (parse_source.f90:145-159) before point1..3 and the photon emitter are set; the engine
+  // applies it and reads the rest (documented deviation).
+  const Value* dv = T::find(s, "direction");
+  if (dv && dv->kind == Value::STRING) {
+    const std::string d = dv->s;
+    const double c[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+    const char* names[6] = {"x", "-x", "y", "-y", "z", "-z"};
+    int k = -1;
+    for (int i = 0; i < 6; ++i)
+      if (d == names[i]) k = i;
+    if (k < 0) throw Fail(SMCRT_ERR_INVALID_ARG, "Direction needs a cardinal direction i.e x, y, or z");
+    for (int i = 0; i < 3; ++i) dir[i] = c[k][i];
+  } else if (dv) {
+    get_vector(s, "direction", dir);
+  } else if (nm != "point") {
+    throw Fail(SMCRT_ERR_INVALID_ARG, "Need to specify direction for source type!");
+  }
+  // corners default (-1,-1,1) (2,0,0) (0,2,0) (:58-61); uniform requires all three
+  double c[3][3] = {{-1, -1, 1}, {2, 0, 0}, {0, 2, 0}};
+  const char* pk[3] = {"point1", "point2", "point3"};
+  const char* dk[3] = {"pos1", "pos2", "pos3"};
+  const char* ax[3] = {"x", "y", "z"};
+  for (int p = 0; p < 3; ++p) {
+    const Value* v = T::find(s, pk[p]);
+    if (v) {
+      if (v->kind != Value::ARRAY || v->arr.size() < 3) throw Fail(SMCRT_ERR_INVALID_ARG, "Need a matrix row for points");
+      for (int i = 0; i < 3; ++i) {
+        c[p][i] = v->arr[i].number();
+        J.set(std::string(dk[p]) + "%" + ax[i], fmt_real(c[p][i]));
+      }
+    } else if (nm == "uniform") {
+      throw Fail(SMCRT_ERR_INVALID_ARG, std::string("Uniform source requires ") + pk[p] + " variable");
+    }
+  }
+  J.set("radius", fmt_real(T::get_real(s, "radius", 0.5)));
+  J.set("focalLength", fmt_real(T::get_real(s, "focalLength", 1.0)));
+  J.set("rhi", fmt_real(T::get_real(s, "rhi", 0.6)));
+  J.set("rlo", fmt_real(T::get_real(s, "rlo", 0.5)));
+  J.set("sigma", fmt_real(T::get_real(s, "sigma", 0.04)));
+  J.set("annulus_type", fmt_str(T::get_string(s, "annulus_type", "gaussian")));
+  J.set("focus_type", fmt_str(T::get_string(s, "focus_type", "gaussian")));
+  J.set("beam_size", fmt_real(T::get_real(s, "beam_size", 0.5)));
+  const std::string spec = T::get_string(s, "spectrum_type", "constant");  // parse_spectrum.f90
+  if (spec != "constant")
+    throw Fail(SMCRT_ERR_UNSUPPORTED, "spectrum_type '" + spec + "' is not supported by the engine (constant)");
+  J.set("wavelength", fmt_real(T::get_real(s, "wavelength", 500.0)));
+
+  std::memset(&J.src, 0, sizeof(J.src));
+  J.src.kind = nm == "point" ? SMCRT_SRC_POINT : (nm == "uniform" ? SMCRT_SRC_UNIFORM : SMCRT_SRC_PENCIL);
+  for (int i = 0; i < 3; ++i) {
+    J.src.pos[i] = pos[i];
+    J.src.dir[i] = dir[i];
+    J.src.p1[i] = c[0][i];
+    J.src.p2[i] = c[1][i];
+    J.src.p3[i] = c[2][i];
+  }
+}
+
+void parse_grid(smcrt_job& J, const Table* root) {  // parse.f90:75-112
+  const Table* g = T::get_table(root, "grid");
+  if (!g) throw Fail(SMCRT_ERR_INVALID_ARG, "Need grid table in input param file");
+  J.grid.nx = (int32_t)T::get_int(g, "nxg", 200);
+  J.grid.ny = (int32_t)T::get_int(g, "nyg", 200);
+  J.grid.nz = (int32_t)T::get_int(g, "nzg", 200);
+  J.grid.xmax = T::get_real(g, "xmax", 1.0);
+  J.grid.ymax = T::get_real(g, "ymax", 1.0);
+  J.grid.zmax = T::get_real(g, "zmax", 1.0);
+  J.set("units", fmt_str(T::get_string(g, "units", "cm")));
+}
+
+// host Philox4x32-10 (same function as detmath.h) for the build-defined sphere list
+void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (uint32_t)p1; c[3] = (uint32_t)p0; c[0] = n0; c[2] = n2;
+  }
+}
+
+std::vector<Prim> setup_geometry(smcrt_job& J, const Table* root) {  // parse_geometry + setup_simulation
+  const Table* g = T::get_table(root, "geometry");
+  if (!g) throw Fail(SMCRT_ERR_INVALID_ARG, "Need geometry table in input param file");
+  J.experiment = T::get_string(g, "geom_name", "sphere");
+  const std::string& e = J.experiment;
+  const double tau = T::get_real(g, "tau", 10.0);
+  J.set("tau", fmt_real(tau));
+  const int64_t num_spheres = T::get_int(g, "num_spheres", 10);
+  J.set("num_spheres", std::to_string(num_spheres));
+  const double musb = T::get_real(g, "musb", 0.0), muab = T::get_real(g, "muab", 0.01);
+  const double musc = T::get_real(g, "musc", 0.0), muac = T::get_real(g, "muac", 0.01);
+  const double hgga = T::get_real(g, "hgga", 0.7);
+  J.set("musb", fmt_real(musb)); J.set("muab", fmt_real(muab));
+  J.set("musc", fmt_real(musc)); J.set("muac", fmt_real(muac)); J.set("hgga", fmt_real(hgga));
+  const int64_t nop = T::get_int(g, "numOptProp", 1);
+  J.set("numOptProp", std::to_string(nop));
+  if (nop < 1 || ((e == "sphere" || e == "box") && nop != 1) || (e == "egg" && nop != 3))
+    throw Fail(SMCRT_ERR_INVALID_ARG, "numOptProp Incorrectly Specified");
+  std::vector<double> op[5];  // mua mus mur hgg n, defaults 0 1 0 0 1 (parse_geometry.f90:90-198)
+  const char* on[5] = {"mua", "mus", "mur", "hgg", "n"};
+  const double od[5] = {0.0, 1.0, 0.0, 0.0, 1.0};
+  for (int q = 0; q < 5; ++q) {
+    const Value* v = T::find(g, on[q]);
+    if (v && (v->kind != Value::ARRAY || (int64_t)v->arr.size() != nop))
+      throw Fail(SMCRT_ERR_INVALID_ARG, std::string(on[q]) + " Incorrectly Specified");
+    for (int64_t i = 0; i < nop; ++i) {
+      op[q].push_back(v ? v->arr[i].number() : od[q]);
+      J.set(std::string(on[q]) + "%" + i4((int)i + 1), fmt_real(op[q].back()));
+    }
+  }
+  double pos[3], bound[3];
+  dict_vec3(J, g, "position", "position", 0.0, pos);
+  dict_vec3(J, g, "boundingBox", "boundinglength", 2.0, bound);
+  double sphere_r = 1.0, bdim[3] = {1.0, 1.0, 1.0};
+  if (e == "sphere") {
+    sphere_r = T::get_real(g, "sphereRadius", 1.0);
+    J.set("sphereRadius", fmt_real(sphere_r));
+  }
+  if (e == "box") dict_vec3(J, g, "BoxDimensions", "BoxDimensions", 1.0, bdim);
+
+  const Mono zero{0.0, 0.0, 0.0, 1.0};
+  std::vector<Prim> a;
+  if (e == "sphere") {  // setupGeometry.f90:10-71
+    a.push_back(sphere(sphere_r, Mono{op[1][0], op[0][0], op[3][0], op[4][0]}, 1, invert(translate(pos[0], pos[1], pos[2]))));
+    a.push_back(box(bound[0], bound[1], bound[2], zero, 2));
+  } else if (e == "box" || e == "test_box") {  // :73-147 (test_box reads BoxDimensions unset: 0)
+    double d[3] = {0.0, 0.0, 0.0};
+    if (e == "box") for (int i = 0; i < 3; ++i) d[i] = bdim[i];
+    a.push_back(box(d[0], d[1], d[2], Mono{op[1][0], op[0][0], op[3][0], op[4][0]}, 1, invert(translate(pos[0], pos[1], pos[2]))));
+    a.push_back(box(bound[0], bound[1], bound[2], zero, 2));
+  } else if (e == "scat_test") {  // :409-435
+    a.push_back(sphere(1.0, Mono{tau, 0.0, 0.0, 1.0}, 1));
+    a.push_back(box(2.0, 2.0, 2.0, zero, 2));
+  } else if (e == "scat_test2") {  // :437-464
+    a.push_back(box(200.0, 200.0, 200.0, Mono{tau, 1e-17, op[3][0], 1.0}, 2));  // hgg = hgg%   1
+  } else if (e == "aptran") {  // :335-363
+    a.push_back(sphere(0.5, Mono{0.0, 1e-17, 0.0, 1.33}, 1, invert(translate(0, 0, 0))));
+    a.push_back(box(2.0, 2.0, 2.0, Mono{0.0, 1e-17, 0.0, 1.0}, 2));
+    a.push_back(box(2.01, 2.01, 2.01, Mono{0.0, 10000000.0, 0.0, 1.0}, 3));
+  } else if (e == "sphere_scene") {  // :250-294; the draws are build-defined (see smcrt.h)
+    const Mono ms{0.0, 0.0, 0.9, 1.37};
+    uint32_t draw = 0;
+    auto ranu = [&](double lo, double hi) {
+      uint32_t c[4] = {draw++, 0x5350u, 0u, 0u};
+      philox(c, (uint32_t)J.iseed, (uint32_t)((uint64_t)J.iseed >> 32));
+      const uint64_t u = ((uint64_t)c[1] << 32) | c[0];
+      return lo + (double)(u >> 11) * 0x1.0p-53 * (hi - lo);
+    };
+    for (int64_t i = 0; i < num_spheres; ++i) {
+      const double r = ranu(0.001, 0.25);
+      const double x = ranu(-1.0 + r, 1.0 - r), y = ranu(-1.0 + r, 1.0 - r), z = ranu(-1.0 + r, 1.0 - r);
+      a.push_back(sphere(r, ms, (int32_t)i + 1, invert(translate(x, y, z))));
+    }
+    a.push_back(box(2.0, 2.0, 2.0, Mono{1e-17, 1e-17, 0.0, 1.0}, (int32_t)num_spheres + 1));
+  } else if (e == "exp") {  // :365-407
+    const double p1[3] = {-8.0, 0.0, 0.0}, p2[3] = {8.0, 0.0, 0.0};
+    a.push_back(cylinder(p1, p2, 1.55, Mono{musc, muac, hgga, 1.3}, 1));
+    a.push_back(cylinder(p1, p2, 1.75, Mono{musb, muab, hgga, 1.5}, 2));
+    a.push_back(box(20.0, 20.0, 20.0, zero, 2));
+  } else if (e == "omg") {  // :466-549
+    const Mono o1{10.0, 0.16, 0.0, 2.65};
+    Prim m;
+    m.kind = SMCRT_SDF_MODEL; m.op = SMCRT_OP_SMOOTH_UNION; m.k = 0.09;
+    m.children.push_back(prim(SMCRT_SDF_TORUS, {0.2, 0.05}, o1, 1, invert(translate(0.0, 0.0, -0.7))));
+    const double seg[9][6] = {{-.25, 0, -.25, -.25, 0, .25}, {-.25, 0, -.25, .25, 0, 0}, {.25, 0, 0, -.25, 0, .25},
+                              {-.25, 0, .25, .25, 0, .25},   {-.25, 0, .5, .25, 0, .5},  {-.25, 0, .5, -.25, 0, .75},
+                              {.25, 0, .5, .25, 0, .75},     {.25, 0, .75, 0, 0, .75},   {0, 0, .625, 0, 0, .75}};
+    for (int i = 0; i < 9; ++i)
+      m.children.push_back(cylinder(seg[i], seg[i] + 3, 0.05, o1, 1, i == 0 ? invert(rotate_y(90.0)) : identity()));
+    a.push_back(m);
+    a.push_back(box(2.0, 2.0, 2.0, zero, 2));
+  } else if (e == "vessels") {  // :552-652 reads res/{edges,nodes,radii}.dat, absent from the reference
+    throw Fail(SMCRT_ERR_UNSUPPORTED, "vessels needs res/edges.dat, nodes.dat and radii.dat, which the reference does not ship");
+  } else if (e == "egg" || e == "logo") {
+    throw Fail(SMCRT_ERR_UNSUPPORTED, "geometry '" + e + "' needs SDF types the engine does not have (revolution / svg segments)");
+  } else {
+    throw Fail(SMCRT_ERR_INVALID_ARG, "no such routine");  // setup.f90:58-59
+  }
+  return a;
+}
+
+double len3(const double v[3]) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+
+void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:17-116
+  const Value* arr = T::find(root, "detectors");
+  if (!arr) return;
+  if (arr->kind != Value::TABLE_ARRAY) throw Fail(SMCRT_ERR_INVALID_ARG, "detectors must be [[detectors]] tables");
+  std::vector<std::pair<smcrt_detector, std::string>> by_kind[4];  // circle, annulus, fibre, camera
+  for (const Value& e : arr->arr) {
+    const Table* c = e.table.get();
+    const std::string type = T::get_string(c, "type", "");
+    const Value* idv = T::find(c, "ID");
+    if (!idv) throw Fail(SMCRT_ERR_INVALID_ARG, "Need to specify a detector ID");
+    const std::string id = idv->kind == Value::STRING ? idv->s : std::to_string(idv->i);
+    if (T::get_bool(c, "trackHistory", false)) throw Fail(SMCRT_ERR_UNSUPPORTED, "Track history currently incompatable with OpenMP!");
+    smcrt_detector d;
+    std::memset(&d, 0, sizeof(d));
+    d.layer = (int32_t)T::get_int(c, "layer", 1);
+    double pos[3] = {0, 0, 0}, dir[3] = {0.0, 0.0, -1.0};
+    if (type == "circle" || type == "annulus" || type == "fibre") {
+      if (!get_vector(c, "position", pos)) throw Fail(SMCRT_ERR_INVALID_ARG, "Expected vector of size 3 for position");
+      get_vector(c, "direction", dir);
+    }
+    if (type == "circle") {  // :149-178 and init_circle_dect, detectors.f90:103-145
+      const double l = len3(dir);
+      for (int i = 0; i < 3; ++i) dir[i] = dir[i] / l;
+      const int64_t nb = T::get_int(c, "nbins", 100);
+      d.kind = SMCRT_DET_CIRCLE;
+      d.radius = T::get_real(c, "radius", 1.0);
+      d.nbins = (int32_t)nb + 1;
+      d.bin_wid = nb == 0 ? 1.0 : d.radius / (double)nb;
+      for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
+      by_kind[0].push_back({d, id});
+    } else if (type == "annulus") {  // :291-311, detectors.f90:166-200 (direction not normalised)
+      const double r1 = T::get_real(c, "radius1", 0.1), r2 = T::get_real(c, "radius2", 0.2);
+      if (r2 <= r1) throw Fail(SMCRT_ERR_INVALID_ARG, "Radius2 is smaller than or equal to radius1!");
+      const int64_t nb = T::get_int(c, "nbins", 100);
+      d.kind = SMCRT_DET_ANNULUS;
+      d.r1 = r1; d.r2 = r2;
+      d.nbins = (int32_t)nb + 1;
+      d.bin_wid = nb == 0 ? 1.0 : (r2 - r1) / (double)nb;
+      for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
+      by_kind[1].push_back({d, id});
+    } else if (type == "fibre") {
+      throw Fail(SMCRT_ERR_UNSUPPORTED, "fibre detectors are not supported by the engine");
+    } else if (type == "camera") {  // :118-147, init_camera detectors.f90:401-445
+      double p1[3] = {-1.0, -1.0, -1.0}, p2[3] = {2.0, 0.0, 0.0}, p3[3] = {0.0, 2.0, 0.0};
+      get_vector(c, "p1", p1); get_vector(c, "p2", p2); get_vector(c, "p3", p3);
+      const int64_t nb = T::get_int(c, "nbins", 100);
+      const double maxval = T::get_real(c, "maxval", 100.0);
+      double e1[3], e2[3];
+      for (int i = 0; i < 3; ++i) { e1[i] = p2[i] - p1[i]; e2[i] = p3[i] - p1[i]; }
+      double n[3] = {e2[1] * e1[2] - e2[2] * e1[1], -e2[0] * e1[2] + e2[2] * e1[0], e2[0] * e1[1] - e2[1] * e1[0]};
+      const double ln = len3(n);
+      for (int i = 0; i < 3; ++i) n[i] = n[i] / ln;
+      d.kind = SMCRT_DET_CAMERA;
+      for (int i = 0; i < 3; ++i) { d.pos[i] = p1[i]; d.e1[i] = e1[i]; d.e2[i] = e2[i]; d.dir[i] = n[i]; }
+      d.width = len3(e1);
+      d.height = len3(e2);
+      d.nbins = (int32_t)nb + 1;
+      d.bin_wid = d.bin_wid_y = nb == 0 ? 1.0 : maxval / (double)d.nbins;
+      by_kind[3].push_back({d, id});
+    } else {
+      throw Fail(SMCRT_ERR_INVALID_ARG, "Invalid detector type: " + type);
+    }
+  }
+  for (int k = 0; k < 4; ++k)
+    for (auto& p : by_kind[k]) {
+      J.dets.push_back(p.first);
+      J.det_ids.push_back(p.second);
+    }
+}
+
+void parse_output(smcrt_job& J, const Table* root) {  // parse.f90:114-157
+  const Table* o = T::get_table(root, "output");
+  if (!o) throw Fail(SMCRT_ERR_INVALID_ARG, "Need output table in input param file");
+  J.outfile = T::get_string(o, "fluence", "fluence.nrrd");
+  J.outfile_absorb = T::get_string(o, "absorb", "absorb.nrrd");
+  J.rendersourcefile = T::get_string(o, "render_source_name", "source_render.nrrd");
+  J.render_source = T::get_bool(o, "render_source", false);
+  J.overwrite = T::get_bool(o, "overwrite", false);
+}
+
+void parse_simulation(smcrt_job& J, const Table* root) {  // parse.f90:159-186
+  const Table* s = T::get_table(root, "simulation");
+  if (!s) throw Fail(SMCRT_ERR_INVALID_ARG, "Need simulation table in input param file");
+  J.iseed = T::get_int(s, "iseed", 123456789);
+  J.tev = T::get_bool(s, "tev", false);
+  J.absorb = T::get_bool(s, "absorb", false);
+  J.loadckpt = T::get_bool(s, "load_checkpoint", false);
+  J.ckptfile = T::get_string(s, "checkpoint_file", "check.ckpt");
+  J.ckptfreq = T::get_int(s, "checkpoint_every_n", 1000000);
+}
+
+bool mkdirs(const std::string& d) {
+  std::string cur;
+  std::stringstream ss(d);
+  std::string part;
+  if (!d.empty() && d[0] == '/') cur = "/";
+  while (std::getline(ss, part, '/')) {
+    if (part.empty()) continue;
+    cur += part + "/";
+    ::mkdir(cur.c_str(), 0755);
+  }
+  struct stat st;
+  return ::stat(d.c_str(), &st) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int smcrt_job_load(const char* toml_path, smcrt_job** out) {
+  smcrt::g_last_error.clear();
+  if (!toml_path || !out) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  *out = nullptr;
+  std::ifstream f(toml_path, std::ios::binary);
+  if (!f) return ffail(SMCRT_ERR_INVALID_ARG, std::string("cannot read ") + toml_path);
+  std::stringstream buf;
+  buf << f.rdbuf();
+  const std::string text = buf.str();
+  smcrt_job* J = new smcrt_job();
+  J->toml_path = toml_path;
+  try {
+    Table root = smcrt::toml::Parser(text).parse();
+    // parse_params order (parse.f90:46-66); the simulation table is read first here only
+    // because the build-defined sphere_scene draws use iseed
+    parse_simulation(*J, &root);
+    parse_source(*J, &root);
+    parse_grid(*J, &root);
+    std::vector<Prim> sdfs = setup_geometry(*J, &root);
+    parse_detectors(*J, &root);
+    parse_output(*J, &root);
+    flatten(sdfs, J->nodes, J->top);
+  } catch (const smcrt::toml::ParseError& e) {
+    delete J;
+    return ffail(SMCRT_ERR_INVALID_ARG, std::string(toml_path) + ": " + e.what());
+  } catch (const Fail& e) {
+    delete J;
+    return ffail(e.code, std::string(toml_path) + ": " + e.what());
+  }
+  *out = J;
+  return SMCRT_OK;
+}
+
+void smcrt_job_destroy(smcrt_job* job) { delete job; }
+
+int smcrt_job_info(const smcrt_job* J, smcrt_job_desc* d) {
+  if (!J || !d) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  std::memset(d, 0, sizeof(*d));
+  d->n_photons = J->nphotons;
+  d->seed = J->iseed;
+  d->flags = SMCRT_FLAG_PATHLENGTH | (J->render_source ? SMCRT_FLAG_RENDER_SOURCE : 0);
+  d->n_nodes = (int32_t)J->nodes.size();
+  d->n_top = (int32_t)J->top.size();
+  d->n_dets = (int32_t)J->dets.size();
+  d->overwrite = J->overwrite ? 1 : 0;
+  d->grid = J->grid;
+  d->source = J->src;
+  std::snprintf(d->experiment, sizeof d->experiment, "%s", J->experiment.c_str());
+  std::snprintf(d->source_name, sizeof d->source_name, "%s", J->source_name.c_str());
+  return SMCRT_OK;
+}
+
+int smcrt_job_scene(const smcrt_job* J, smcrt_sdf_node* nodes, int32_t* top, smcrt_detector* dets) {
+  if (!J || !nodes || !top || (!dets && !J->dets.empty())) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  std::memcpy(nodes, J->nodes.data(), J->nodes.size() * sizeof(smcrt_sdf_node));
+  std::memcpy(top, J->top.data(), J->top.size() * sizeof(int32_t));
+  if (!J->dets.empty()) std::memcpy(dets, J->dets.data(), J->dets.size() * sizeof(smcrt_detector));
+  return SMCRT_OK;
+}
+
+int smcrt_job_metadata(const smcrt_job* J, char* buf, int32_t cap) {
+  if (!J || !buf || cap < 1) return ffail(SMCRT_ERR_INVALID_ARG, "bad arguments");
+  smcrt_job tmp = *J;
+  tmp.set("grid_data", fmt_str("fluence map"));  // finalise, kernelsMod.f90:2368-2372
+  char rs[128];
+  std::snprintf(rs, sizeof rs, "%.7g %.7g %.7g", J->grid.xmax, J->grid.ymax, J->grid.zmax);
+  tmp.set("real_size", fmt_str(rs));
+  tmp.set("nphotons", std::to_string(J->nphotons));
+  tmp.set("source", fmt_str(J->source_name));
+  tmp.set("experiment", fmt_str(J->experiment));
+  const std::string d = tmp.dump();
+  std::snprintf(buf, (size_t)cap, "%s", d.c_str());
+  return (int32_t)d.size() < cap ? SMCRT_OK : ffail(SMCRT_ERR_INVALID_ARG, "metadata buffer too small");
+}
+
+// default_MCRT without checkpoint loading (kernelsMod.f90:14-82): run_MCRT on `device`,
+// then finalise's normalisation and writes (:2321-2416) under `outdir` (the reference's
+// fileplace): jmean/<fluence>, emission/<render_source_name>, absorb/absorb.nrrd,
+// detectors/detector_<i>.dat. `io` (may be NULL) receives the tallies as well.
+int smcrt_job_run(smcrt_job* J, int32_t device, const char* outdir, double* nscatt_out) {
+  if (!J || !outdir) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (J->loadckpt) return ffail(SMCRT_ERR_UNSUPPORTED, "load_checkpoint is not supported by smcrt_job_run");
+  smcrt_scene* scene = nullptr;
+  int st = smcrt_scene_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(),
+                              &J->grid, J->dets.empty() ? nullptr : J->dets.data(), (int32_t)J->dets.size(), device,
+                              &scene);
+  if (st) return st;
+  const size_t nv = (size_t)J->grid.nx * J->grid.ny * J->grid.nz;
+  std::vector<float> jmean(nv, 0.f), absorb(nv, 0.f), emission(nv, 0.f);
+  int64_t nb = 0;
+  smcrt_scene_det_bins(scene, &nb);
+  std::vector<double> det_bins((size_t)std::max<int64_t>(1, nb), 0.0);
+  double nscatt = 0.0;
+  smcrt_tallies io;
+  std::memset(&io, 0, sizeof(io));
+  io.jmean = jmean.data(); io.absorb = absorb.data(); io.emission = emission.data();
+  io.det_bins = det_bins.data(); io.nscatt = &nscatt;
+  smcrt_run_config cfg;
+  std::memset(&cfg, 0, sizeof(cfg));
+  cfg.n_photons = (uint64_t)J->nphotons;
+  cfg.first_photon = 0;
+  cfg.seed = (uint64_t)J->iseed;
+  cfg.flags = SMCRT_FLAG_PATHLENGTH | (J->render_source ? SMCRT_FLAG_RENDER_SOURCE : 0);
+  st = smcrt_run(scene, &J->src, &cfg, &io);
+  smcrt_scene_destroy(scene);
+  if (st) return st;
+  if (nscatt_out) *nscatt_out = nscatt;
+  const std::string base = std::string(outdir) + "/";
+  if (!mkdirs(base + "jmean") || !mkdirs(base + "emission") || !mkdirs(base + "absorb") ||
+      (!J->dets.empty() && !mkdirs(base + "detectors")))
+    return ffail(SMCRT_ERR_INVALID_ARG, "cannot create output directories under " + base);
+  std::vector<char> meta(1 << 16);
+  if ((st = smcrt_job_metadata(J, meta.data(), (int32_t)meta.size()))) return st;
+  const int32_t ow = J->overwrite ? 1 : 0;
+  if ((st = smcrt_normalise_fluence(jmean.data(), &J->grid, (uint64_t)J->nphotons))) return st;
+  if ((st = smcrt_write_data_f32((base + "jmean/" + J->outfile).c_str(), jmean.data(), J->grid.nx, J->grid.ny,
+                                 J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
+    return st;
+  if ((st = smcrt_normalise_fluence(emission.data(), &J->grid, (uint64_t)J->nphotons))) return st;
+  if ((st = smcrt_write_data_f32((base + "emission/" + J->rendersourcefile).c_str(), emission.data(), J->grid.nx,
+                                 J->grid.ny, J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
+    return st;
+  if ((st = smcrt_write_data_f32((base + "absorb/absorb.nrrd").c_str(), absorb.data(), J->grid.nx, J->grid.ny,
+                                 J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
+    return st;
+  size_t off = 0;
+  for (size_t i = 0; i < J->dets.size(); ++i) {
+    const smcrt_detector& d = J->dets[i];
+    const size_t n = d.kind == SMCRT_DET_CAMERA ? (size_t)d.nbins * d.nbins : (size_t)d.nbins;
+    if ((st = smcrt_write_detector((base + "detectors/detector_" + std::to_string(i + 1) + ".dat").c_str(), &d,
+                                   det_bins.data() + off, J->det_ids[i].c_str(), J->nphotons)))
+      return st;
+    off += n;
+  }
+  return SMCRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+"""TOML front end on the reference's own input files (fixtures in
+tests/golden/res/). CPU only, except the last test.
+
+Each supported file must give exactly the scene the reference's parse_params +
+setup_simulation build -- compared node for node with the Python restatements of the
+setupGeometry builders (which the oracle KATs pin) -- and each file the reference rejects
+must be rejected with the reference's reason."""
+import ctypes as C
+import math
+import os
+
+import numpy as np
+import pytest
+
+from rsmcrt_amd import abi, builders, scene
+from rsmcrt_amd.engine import SmcrtError
+from rsmcrt_amd.job import Job
+
+RES = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "res")
+
+
+def res(name):
+    return os.path.join(RES, name)
+
+
+def node_bytes(arr, n):
+    return [bytes(memoryview(arr[i]).cast("B")) for i in range(n)]
+
+
+def same_scene(job, sc):
+    assert job.desc.n_nodes == len(sc.nodes) and job.desc.n_top == sc.n_top
+    assert list(job.top[:job.desc.n_top]) == list(sc.top)
+    assert node_bytes(job.nodes, job.desc.n_nodes) == node_bytes(sc.node_array(), len(sc.nodes))
+
+
+def same_struct(a, b):
+    return bytes(memoryview(a).cast("B")) == bytes(memoryview(b).cast("B"))
+
+
+def test_scat_test():  # res/scat_test.toml
+    j = Job(res("scat_test.toml"))
+    same_scene(j, builders.setup_scat_test(10.0))
+    d = j.desc
+    assert (d.grid.nx, d.grid.ny, d.grid.nz, d.grid.xmax) == (200, 200, 200, 1.0)
+    assert d.n_photons == 100000 and d.seed == 123456789 and d.source.kind == abi.SRC_POINT
+    assert d.flags == abi.FLAG_PATHLENGTH and d.overwrite == 1 and j.experiment == "scat_test"
+
+
+def test_scat_test2_pencil():
+    j = Job(res("scat_test2.toml"))
+    same_scene(j, builders.setup_scat_test2(10.0, 0.9))  # hgg = [0.9] -> hgg%   1
+    s = j.desc.source
+    assert s.kind == abi.SRC_PENCIL and list(s.dir) == [0.0, 0.0, 1.0] and list(s.pos) == [0.0, 0.0, 0.0]
+    assert j.desc.grid.xmax == 100.0
+
+
+def test_aptran_uniform_vector_direction():
+    j = Job(res("aptran.toml"))
+    same_scene(j, builders.setup_tran_and_jacques())
+    s = j.desc.source
+    # the vector direction is applied and the corners read (the reference returns early
+    # here and crashes later, parse_source.f90:145-159)
+    assert s.kind == abi.SRC_UNIFORM and list(s.dir) == [0.0, 0.0, -1.0]
+    assert list(s.p1) == [-0.25, 0.0, 0.99999] and list(s.p2) == [0.5, 0.0, 0.0] and list(s.p3) == [0.0, 0.0, 0.0]
+
+
+def test_validation1_box_and_circle_detectors():
+    j = Job(res("validation1.toml"))
+    same_scene(j, builders.setup_box(90.0, 10.0, 0.75, 1.0, (100.0, 100.0, 0.02), (100.0, 100.0, 0.03)))
+    want = [scene.circle_dect((0.0, 0.0, -0.01), (0.0, 0.0, -1.0), 1, 20.0, 100),
+            scene.circle_dect((0.0, 0.0, 0.01), (0.0, 0.0, 1.0), 1, 20.0, 100)]
+    assert all(same_struct(a, b) for a, b in zip(j.detectors, want))
+    assert j.desc.flags == abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE
+
+
+def test_detector_kinds_and_grouping():
+    j = Job(res("test_dects.toml"))
+    same_scene(j, builders.setup_scat_test(10.0))
+    want = [scene.circle_dect((-1.0, 0.0, 0.0), (-1.0, 0.0, 0.0), 4, 0.5, 10),
+            scene.annulus_dect((-1.0, 0.0, 0.0), (-1.0, 0.0, 0.0), 3, 0.5, 1.0, 10),
+            scene.camera((-1.0, -1.0, -1.0), (0.0, 2.0, 0.0), (0.0, 0.0, 2.0), 2, 10, 5000.0)]
+    assert all(same_struct(a, b) for a, b in zip(j.detectors, want))
+    # parse_detectors.f90:100-115 orders circles, annuli, fibres, cameras
+    kinds = [d.kind for d in Job(res("default.toml")).detectors]
+    assert kinds == sorted(kinds)
+
+
+def test_omg_csg_model():
+    same_scene(Job(res("omg.toml")), builders.setup_omg_sdf())
+
+
+def test_sphere_scene_build_defined_list():
+    j = Job(res("sphere.toml"))
+    assert j.desc.n_top == 41 and j.experiment == "sphere_scene"
+    spheres = []
+    for i in range(40):
+        nd = j.nodes[i]
+        r = nd.param[0]
+        c = (-nd.transform[3], -nd.transform[7], -nd.transform[11])
+        assert 0.001 <= r < 0.25 and all(-1.0 + r <= x <= 1.0 - r for x in c)
+        spheres.append((r, *c))
+    same_scene(j, builders.setup_sphere_scene(spheres))
+    assert Job(res("sphere.toml")).nodes[7].param[0] == j.nodes[7].param[0]  # deterministic
+
+
+@pytest.mark.parametrize("name,code,why", [
+    ("egg_test.toml", abi.ERR_UNSUPPORTED, "revolution"),
+    ("logo.toml", abi.ERR_UNSUPPORTED, "svg"),
+    ("vessels.toml", abi.ERR_UNSUPPORTED, "edges.dat"),
+    ("thinBarrier.toml", abi.ERR_UNSUPPORTED, "annulus"),
+    ("validateFibreDect.toml", abi.ERR_UNSUPPORTED, "fibre"),
+    ("test_spectra_1D.toml", abi.ERR_UNSUPPORTED, "spectrum_type"),
+    # rejected by the reference itself:
+    ("skin.toml", abi.ERR_INVALID_ARG, "Uniform source requires point1"),   # parse_source.f90:183-186
+    ("exp.toml", abi.ERR_INVALID_ARG, "position"),                          # annulus without position
+    ("slab_test.toml", abi.ERR_INVALID_ARG, "position"),
+    ("input.toml", abi.ERR_INVALID_ARG, "no such routine"),                 # setup.f90:58-59
+    ("jacques.toml", abi.ERR_INVALID_ARG, "no such routine"),
+])
+def test_rejections(name, code, why):
+    with pytest.raises(SmcrtError) as e:
+        Job(res(name))
+    assert abi.STATUS_NAMES[code] in str(e.value) and why in str(e.value)
+
+
+def test_metadata_dict():
+    meta = Job(res("validation1.toml")).metadata()
+    lines = dict(l.split(" = ", 1) for l in meta.strip().splitlines())
+    assert lines["nphotons"] == "1000000" and lines['"mus%   1"'] == "90.0"
+    assert lines["source"] == '"pencil"' and lines["experiment"] == '"box"' and lines["units"] == '"cm"'
+    assert lines['"BoxDimensions%   3"'] == "0.02"
+
+
+@pytest.mark.gpu
+def test_job_run_scat_test(tmp_path, kats):
+    """default_MCRT on res/scat_test.toml: the reference's KAT and its output files."""
+    from tests.test_writers import read_nrrd_like_reference
+    j = Job(res("scat_test.toml"))
+    nscatt = j.run(tmp_path)
+    k = kats["scat_test_nscatt"]
+    assert abs(nscatt / j.desc.n_photons - k["value"]) <= k["thr"]
+    data, hdr = read_nrrd_like_reference(tmp_path / "jmean" / "fluence.nrrd")
+    assert data.shape == (200, 200, 200) and data.dtype == np.float32 and hdr["experiment"] == '"scat_test"'
+    assert (tmp_path / "absorb" / "absorb.nrrd").exists() and (tmp_path / "emission" / "source_render.nrrd").exists()
+    # the same photons through the Python engine API, normalised the same way
+    from rsmcrt_amd import output
+    from rsmcrt_amd.engine import Engine
+    d = j.desc
+    with Engine(builders.setup_scat_test(10.0), d.grid) as eng:
+        r = eng.run(d.source, d.n_photons, seed=d.seed)
+    assert np.array_equal(output.normalise_fluence(r.jmean.astype(np.float32), d.grid, d.n_photons), data)

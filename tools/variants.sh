@@ -6,7 +6,7 @@ mkdir -p tools/diag_libs
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math --offload-arch=gfx950 $flags \
-    -o tools/diag_libs/libsmcrt_$name.so rsmcrt_amd/csrc/smcrt.hip rsmcrt_amd/csrc/writers.cpp &
+    -o tools/diag_libs/libsmcrt_$name.so rsmcrt_amd/csrc/smcrt.hip rsmcrt_amd/csrc/writers.cpp rsmcrt_amd/csrc/frontend.cpp &
 done
 wait
 ls -la tools/diag_libs/
