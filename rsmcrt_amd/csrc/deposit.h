@@ -57,7 +57,10 @@ __device__ __forceinline__ unsigned long long pack_record(uint32_t vox, double v
   return ((unsigned long long)vox << 32) | (unsigned long long)__float_as_uint((float)val);
 }
 
-constexpr uint32_t BIN_BLOCKS_ = 1024;  // == BIN_BLOCKS below
+#ifndef SMCRT_BIN_BLOCKS
+#define SMCRT_BIN_BLOCKS 1024
+#endif
+constexpr uint32_t BIN_BLOCKS_ = SMCRT_BIN_BLOCKS;  // == BIN_BLOCKS below
 
 // Add the wave's LDS tile histogram of chunk `chunk` into counts[tile][chunk % BIN_BLOCKS]
 // and clear it (wave-uniform call; LDS ops of one wave complete in order).

@@ -437,6 +437,9 @@ template <int GM>
 __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double* __restrict__ xf,
                                          const double* __restrict__ yf, const double* __restrict__ zf,
                                          bool& dep, uint32_t& dep_vox, double& dep_val) {
+#ifdef SMCRT_ASM_MARKERS
+  asm volatile("; @@DDA_BEGIN");
+#endif
   const V3 dir = L.dir;
   bool done = false;
   if (++L.dda_it > (uint32_t)MAX_DDA_ITERS) { L.fault = true; L.tflag = true; done = true; }
@@ -457,11 +460,12 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
     const double ax = dir.x == 0.0 ? 100000.0 : nx * __builtin_amdgcn_rcp(dir.x);
     const double ay = dir.y == 0.0 ? 100000.0 : ny * __builtin_amdgcn_rcp(dir.y);
     const double az = dir.z == 0.0 ? 100000.0 : nz * __builtin_amdgcn_rcp(dir.z);
+    // (all selects, no branches: the three pairwise minima first, then pick)
+    const double m_yz = dmin(ay, az), m_xz = dmin(ax, az), m_xy = dmin(ax, ay);
     const bool mx = ax <= ay && ax <= az, my = !mx && ay <= az;
     const double amin = mx ? ax : (my ? ay : az);
-    const double arest = mx ? dmin(ay, az) : (my ? dmin(ax, az) : dmin(ax, ay));
-    const bool fast = amin > 0.0 && arest > amin * (1.0 + 0x1.0p-16) && !(dir.x != dir.x) && !(dir.y != dir.y) &&
-                      !(dir.z != dir.z);
+    const double arest = mx ? m_yz : (my ? m_xz : m_xy);
+    const bool fast = amin > 0.0 && arest > amin * (1.0 + 0x1.0p-16) && ax == ax && ay == ay && az == az;
     double dcell;
     bool lx, ly, lz;
     if (fast) {
@@ -503,9 +507,10 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
         // as selects over the same expressions, so `old` stays in registers.
         const double delta = 1e-8;  // local delta, :393
         const double ax = L.old.x + dir.x * dcell, ay = L.old.y + dir.y * dcell, az = L.old.z + dir.z * dcell;
-        const double sx = dir.x > 0.0 ? fx + delta : (dir.x < 0.0 ? fx - delta : L.old.x);
-        const double sy = dir.y > 0.0 ? fy + delta : (dir.y < 0.0 ? fy - delta : L.old.y);
-        const double sz = dir.z > 0.0 ? fz + delta : (dir.z < 0.0 ? fz - delta : L.old.z);
+        // (face - delta == face + (-delta) exactly, so one add with a signed delta)
+        const double sx = dir.x > 0.0 || dir.x < 0.0 ? fx + (dir.x > 0.0 ? delta : -delta) : L.old.x;
+        const double sy = dir.y > 0.0 || dir.y < 0.0 ? fy + (dir.y > 0.0 ? delta : -delta) : L.old.y;
+        const double sz = dir.z > 0.0 || dir.z < 0.0 ? fz + (dir.z > 0.0 ? delta : -delta) : L.old.z;
         const bool snx = lx, sny = !lx && ly, snz = !lx && !ly;
         L.old.x = snx ? sx : ax;
         L.old.y = sny ? sy : ay;
@@ -521,6 +526,9 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
     L.seg = false;
     L.xcell = L.ci; L.ycell = L.cj; L.zcell = L.ck;
   }
+#ifdef SMCRT_ASM_MARKERS
+  asm volatile("; @@DDA_END");
+#endif
 }
 
 // The EVAL phase: ds(i) for every top-level SDF at L.q, reduced to minval(abs(ds)),
