@@ -441,91 +441,90 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   asm volatile("; @@DDA_BEGIN");
 #endif
   const V3 dir = L.dir;
-  bool done = false;
-  if (++L.dda_it > (uint32_t)MAX_DDA_ITERS) { L.fault = true; L.tflag = true; done = true; }
-  if (!done) {
-    // wall_dist, :467-521: d_a = (face_a - old_a)/dir_a, dcell = min, ldir_a = (dcell == d_a).
-    // Only the smallest quotient is needed exactly: the three are ranked with hardware
-    // reciprocals (relative error far below the 2^-16 margin required), and the one winner
-    // is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
-    // or negative distances, NaN), all three are divided exactly as the reference does.
-    // Both paths give the reference's dcell and ldir bit for bit.
-    // the wall each axis moves towards: xface(ci+1) going +, xface(ci) going - (0-based here)
-    const double fx = face<GM>(xf, dir.x > 0.0 ? L.ci : L.ci - 1, K.fex);
-    const double fy = face<GM>(yf, dir.y > 0.0 ? L.cj : L.cj - 1, K.fey);
-    const double fz = face<GM>(zf, dir.z > 0.0 ? L.ck : L.ck - 1, K.fez);
-    const double nx = fx - L.old.x;
-    const double ny = fy - L.old.y;
-    const double nz = fz - L.old.z;
-    const double ax = dir.x == 0.0 ? 100000.0 : nx * __builtin_amdgcn_rcp(dir.x);
-    const double ay = dir.y == 0.0 ? 100000.0 : ny * __builtin_amdgcn_rcp(dir.y);
-    const double az = dir.z == 0.0 ? 100000.0 : nz * __builtin_amdgcn_rcp(dir.z);
-    // (all selects, no branches: the three pairwise minima first, then pick)
-    const double m_yz = dmin(ay, az), m_xz = dmin(ax, az), m_xy = dmin(ax, ay);
-    const bool mx = ax <= ay && ax <= az, my = !mx && ay <= az;
-    const double amin = mx ? ax : (my ? ay : az);
-    const double arest = mx ? m_yz : (my ? m_xz : m_xy);
-    const bool fast = amin > 0.0 && arest > amin * (1.0 + 0x1.0p-16) && ax == ax && ay == ay && az == az;
-    double dcell;
-    bool lx, ly, lz;
-    if (fast) {
-      const double num = mx ? nx : (my ? ny : nz), den = mx ? dir.x : (my ? dir.y : dir.z);
-      dcell = den == 0.0 ? 100000.0 : num / den;
-      lx = mx; ly = my; lz = !mx && !my;
-    } else {
-      double dx = -999.0, dy = -999.0, dz = -999.0;
-      if (dir.x > 0.0 || dir.x < 0.0) dx = nx / dir.x;
-      else if (dir.x == 0.0) dx = 100000.0;
-      if (dir.y > 0.0 || dir.y < 0.0) dy = ny / dir.y;
-      else if (dir.y == 0.0) dy = 100000.0;
-      if (dir.z > 0.0 || dir.z < 0.0) dz = nz / dir.z;
-      else if (dir.z == 0.0) dz = 100000.0;
-      dcell = dmin(dmin(dx, dy), dz);
-      lx = (dcell == dx); ly = (dcell == dy); lz = (dcell == dz);
-    }
-    if (dcell < 0.0) {  // error stop :510-516
-      L.fault = true; L.tflag = true; done = true;
-    } else {
-      const bool last = L.sd + dcell > L.slen;
-      if (last) { dcell = L.slen - L.sd; L.sd = L.slen; }
-      else L.sd = L.sd + dcell;
-      // jmean(cell) += real(dcell,sp)*weight (inttau2.f90:427,434): handed to the caller,
-      // which appends a deposit record (binned path) or adds it atomically
-      dep = true;
-      dep_vox = (uint32_t)lin(K, L.ci, L.cj, L.ck);
-      dep_val = (double)(float)dcell * L.weight;
-      if (last) {  // update_pos(.false.)
-        L.old.x = L.old.x + dir.x * dcell;
-        L.old.y = L.old.y + dir.y * dcell;
-        L.old.z = L.old.z + dir.z * dcell;
-        done = true;
-      } else if (!(lx || ly || lz)) {  // error stop :570-573
-        L.fault = true; L.tflag = true; done = true;
-      } else {
-        // update_pos(.true.), :538-582: the first axis with ldir set is snapped to its wall
-        // +- delta (unchanged if its direction is 0), the other two advance by dcell. Written
-        // as selects over the same expressions, so `old` stays in registers.
-        const double delta = 1e-8;  // local delta, :393
-        const double ax = L.old.x + dir.x * dcell, ay = L.old.y + dir.y * dcell, az = L.old.z + dir.z * dcell;
-        // (face - delta == face + (-delta) exactly, so one add with a signed delta)
-        const double sx = dir.x > 0.0 || dir.x < 0.0 ? fx + (dir.x > 0.0 ? delta : -delta) : L.old.x;
-        const double sy = dir.y > 0.0 || dir.y < 0.0 ? fy + (dir.y > 0.0 ? delta : -delta) : L.old.y;
-        const double sz = dir.z > 0.0 || dir.z < 0.0 ? fz + (dir.z > 0.0 ? delta : -delta) : L.old.z;
-        const bool snx = lx, sny = !lx && ly, snz = !lx && !ly;
-        L.old.x = snx ? sx : ax;
-        L.old.y = sny ? sy : ay;
-        L.old.z = snz ? sz : az;
-        L.ci = cell_of<GM>(L.old.x, K.nx, K.xmax, K.inv2x);
-        L.cj = cell_of<GM>(L.old.y, K.ny, K.ymax, K.inv2y);
-        L.ck = cell_of<GM>(L.old.z, K.nz, K.zmax, K.inv2z);
-        if (L.ci == -1 || L.cj == -1 || L.ck == -1) { L.tflag = true; done = true; }
-      }
-    }
+  const bool capped = ++L.dda_it > (uint32_t)MAX_DDA_ITERS;  // runaway guard: fault
+  // wall_dist, :467-521: d_a = (face_a - old_a)/dir_a, dcell = min, ldir_a = (dcell == d_a).
+  // Only the smallest quotient is needed exactly: the three are ranked with hardware
+  // reciprocals (relative error far below the 2^-16 margin required), and the one winner
+  // is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
+  // or negative distances, NaN), all three are divided exactly as the reference does.
+  // Both paths give the reference's dcell and ldir bit for bit.
+  // the wall each axis moves towards: xface(ci+1) going +, xface(ci) going - (0-based here)
+  const double fx = face<GM>(xf, dir.x > 0.0 ? L.ci : L.ci - 1, K.fex);
+  const double fy = face<GM>(yf, dir.y > 0.0 ? L.cj : L.cj - 1, K.fey);
+  const double fz = face<GM>(zf, dir.z > 0.0 ? L.ck : L.ck - 1, K.fez);
+  const double nx = fx - L.old.x;
+  const double ny = fy - L.old.y;
+  const double nz = fz - L.old.z;
+  const double ax = dir.x == 0.0 ? 100000.0 : nx * __builtin_amdgcn_rcp(dir.x);
+  const double ay = dir.y == 0.0 ? 100000.0 : ny * __builtin_amdgcn_rcp(dir.y);
+  const double az = dir.z == 0.0 ? 100000.0 : nz * __builtin_amdgcn_rcp(dir.z);
+  // (all selects, no branches: the three pairwise minima first, then pick)
+  const double m_yz = dmin(ay, az), m_xz = dmin(ax, az), m_xy = dmin(ax, ay);
+  const bool mx = ax <= ay && ax <= az, my = !mx && ay <= az;
+  const double amin = mx ? ax : (my ? ay : az);
+  const double arest = mx ? m_yz : (my ? m_xz : m_xy);
+  const bool fast = amin > 0.0 && arest > amin * (1.0 + 0x1.0p-16) && ax == ax && ay == ay && az == az;
+  double dcell;
+  bool lx, ly, lz;
+  if (fast) {
+    const double num = mx ? nx : (my ? ny : nz), den = mx ? dir.x : (my ? dir.y : dir.z);
+    dcell = den == 0.0 ? 100000.0 : num / den;
+    lx = mx; ly = my; lz = !mx && !my;
+  } else {
+    double dx = -999.0, dy = -999.0, dz = -999.0;
+    if (dir.x > 0.0 || dir.x < 0.0) dx = nx / dir.x;
+    else if (dir.x == 0.0) dx = 100000.0;
+    if (dir.y > 0.0 || dir.y < 0.0) dy = ny / dir.y;
+    else if (dir.y == 0.0) dy = 100000.0;
+    if (dir.z > 0.0 || dir.z < 0.0) dz = nz / dir.z;
+    else if (dir.z == 0.0) dz = 100000.0;
+    dcell = dmin(dmin(dx, dy), dz);
+    lx = (dcell == dx); ly = (dcell == dy); lz = (dcell == dz);
   }
-  if (done) {
-    L.seg = false;
-    L.xcell = L.ci; L.ycell = L.cj; L.zcell = L.ck;
-  }
+  // The rest of the crossing is written as selects, not branches: lanes of a wave reach
+  // different outcomes here on almost every step, and divergent branches cost more than
+  // computing both sides.
+  const bool neg = dcell < 0.0;  // error stop :510-516
+  const bool ok = !capped && !neg;
+  const bool last = L.sd + dcell > L.slen;
+  const double dc = last ? L.slen - L.sd : dcell;
+  // jmean(cell) += real(dcell,sp)*weight (inttau2.f90:427,434): handed to the caller,
+  // which appends a deposit record (binned path) or adds it atomically
+  dep = ok;
+  dep_vox = lin(K, L.ci, L.cj, L.ck);
+  dep_val = (double)(float)dc * L.weight;
+  // update_pos (:524-584): .false. (last step) advances all three coordinates by dc;
+  // .true. snaps the first axis with ldir set to its wall +- delta (unchanged if its
+  // direction is 0) and advances the other two.
+  const double delta = 1e-8;  // local delta, :393
+  const double vx = L.old.x + dir.x * dc, vy = L.old.y + dir.y * dc, vz = L.old.z + dir.z * dc;
+  // (face - delta == face + (-delta) exactly, so one add with a signed delta)
+  const double sx = dir.x > 0.0 || dir.x < 0.0 ? fx + (dir.x > 0.0 ? delta : -delta) : L.old.x;
+  const double sy = dir.y > 0.0 || dir.y < 0.0 ? fy + (dir.y > 0.0 ? delta : -delta) : L.old.y;
+  const double sz = dir.z > 0.0 || dir.z < 0.0 ? fz + (dir.z > 0.0 ? delta : -delta) : L.old.z;
+  const bool noaxis = !(lx || ly || lz);  // error stop :570-573
+  const bool snap = ok && !last && !noaxis;
+  const bool snx = lx, sny = !lx && ly, snz = !lx && !ly;
+  const double px = snap ? (snx ? sx : vx) : (ok && last ? vx : L.old.x);
+  const double py = snap ? (sny ? sy : vy) : (ok && last ? vy : L.old.y);
+  const double pz = snap ? (snz ? sz : vz) : (ok && last ? vz : L.old.z);
+  const int32_t ci = cell_of<GM>(px, K.nx, K.xmax, K.inv2x);  // update_voxels, :587-614
+  const int32_t cj = cell_of<GM>(py, K.ny, K.ymax, K.inv2y);
+  const int32_t ck = cell_of<GM>(pz, K.nz, K.zmax, K.inv2z);
+  const bool left = snap && (ci == -1 || cj == -1 || ck == -1);  // left the grid, :437-440
+  L.old = v3(px, py, pz);
+  if (ok) L.sd = last ? L.slen : L.sd + dcell;
+  L.ci = snap ? ci : L.ci;
+  L.cj = snap ? cj : L.cj;
+  L.ck = snap ? ck : L.ck;
+  const bool bad = capped || neg || (ok && !last && noaxis);
+  L.fault = L.fault || bad;
+  L.tflag = L.tflag || bad || left;
+  const bool done = bad || (ok && last) || left;
+  L.seg = L.seg && !done;
+  L.xcell = done ? L.ci : L.xcell;
+  L.ycell = done ? L.cj : L.ycell;
+  L.zcell = done ? L.ck : L.zcell;
 #ifdef SMCRT_ASM_MARKERS
   asm volatile("; @@DDA_END");
 #endif
