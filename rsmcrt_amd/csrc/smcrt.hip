@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   L.weight = 1.0; L.tau = L.taurun = L.d = L.minabs = 0.0;
   L.xcell = L.ycell = L.zcell = L.layer = L.old_layer = L.new_layer = L.Ls = 0;
   L.hop = L.loopc = L.dda_it = 0;
-  L.sd = L.slen = 0.0; L.ci = L.cj = L.ck = 0;
+  L.sd = L.slen = 0.0;
   L.rng.init(0);
   const bool binned = K.rec_pool != nullptr;  // (set only when jmean is tallied)
   RecLog W;
@@ -357,6 +357,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
     // Placed after the program points that start segments (P3, P4) and before the ones that
     // consume them (P5), so a short segment is started, walked and finished in one trip.
+#ifdef SMCRT_ABL_NO_DDA  // timing ablation only: segments end at once, nothing is deposited
+    L.seg = false;
+#endif
     if (__ballot(L.seg)) {  // wave-uniform, so deposit records can be wave-compacted
 #pragma unroll
       for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {

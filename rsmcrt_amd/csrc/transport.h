@@ -103,23 +103,23 @@ struct KParams {
 // GM >= 1: every axis has 2*max a power of two, so the division is an exact multiply (the kernel
 // is instantiated for it; the general case keeps a per-axis uniform branch).
 template <int GM>
-__device__ __forceinline__ int32_t cell_of(double p, int32_t n, double max, double inv) {
+__device__ __forceinline__ double cell_floor(double p, int32_t n, double max, double inv, int32_t fe) {
+  if constexpr (GM == 2) return floor(ldexp(p, -fe));  // n/(2*max) == 2^-fe: one exact scaling
   const double a = (double)n * p;
-  const double f = floor(GM >= 1 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
+  return floor(GM >= 1 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
+}
+template <int GM>
+__device__ __forceinline__ int32_t cell_of(double p, int32_t n, double max, double inv, int32_t fe) {
+  const double f = cell_floor<GM>(p, n, max, inv, fe);
   if (!(f >= 0.0 && f < (double)n)) return -1;
   return (int32_t)f + 1;
 }
 // get_voxel_cart, grid.f90:51-78 (centred coordinates)
 template <int GM>
-__device__ __forceinline__ int32_t vox_of(double p, int32_t n, double max, double inv) {
-  const double a = (double)n * (p + max);
-  const double f = floor(GM >= 1 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
-  if (!(f >= 0.0 && f < (double)n)) return -1;
-  return (int32_t)f + 1;
+__device__ __forceinline__ int32_t vox_of(double p, int32_t n, double max, double inv, int32_t fe) {
+  return cell_of<GM>(p + max, n, max, inv, fe);
 }
 
-// Voxel face k (0-based; xface(k+1) of grid.f90:147-157, = ((k*2)*max)/n). GM == 2: both
-// 2*max and n are powers of two, so the face is exactly k * 2^ex and needs no table lookup.
 template <int GM>
 __device__ __forceinline__ double face(const double* __restrict__ f, int32_t k, int32_t ex) {
   if constexpr (GM == 2) return ldexp((double)k, ex);
@@ -294,8 +294,7 @@ struct Lane {
   bool seg;
   V3 old;  // DDA position, corner coordinates
   double sd, slen;
-  int32_t ci, cj, ck;
-  uint32_t dda_it;
+  uint32_t dda_it;  // (the DDA's voxel is xcell/ycell/zcell)
 };
 
 // LDS-resident per-lane values, [field][threadIdx] so lanes never share a bank.
@@ -365,9 +364,9 @@ __device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__
   }
   L.tflag = false;
   L.weight = 1.0;
-  L.xcell = vox_of<GM>(L.pos.x, K.nx, K.xmax, K.inv2x);
-  L.ycell = vox_of<GM>(L.pos.y, K.ny, K.ymax, K.inv2y);
-  L.zcell = vox_of<GM>(L.pos.z, K.nz, K.zmax, K.inv2z);
+  L.xcell = vox_of<GM>(L.pos.x, K.nx, K.xmax, K.inv2x, K.fex);
+  L.ycell = vox_of<GM>(L.pos.y, K.ny, K.ymax, K.inv2y, K.fey);
+  L.zcell = vox_of<GM>(L.pos.z, K.nz, K.zmax, K.inv2z, K.fez);
 }
 
 // scatter, photon.f90:1045-1103
@@ -412,21 +411,21 @@ template <int GM>
 __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneShared* sh, V3 p, double dlen) {
   LCTR(LC_UPD)++;
   V3 old = v3(p.x + K.xmax, p.y + K.ymax, p.z + K.zmax);
-  int32_t ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x), cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y),
-          ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z);
+  int32_t ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x, K.fex), cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y, K.fey),
+          ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z, K.fez);
   L.xcell = ci; L.ycell = cj; L.zcell = ck;
   if (!(K.flags & SMCRT_FLAG_PATHLENGTH)) {  // :446-463
     old.x = old.x + L.dir.x * dlen;
     old.y = old.y + L.dir.y * dlen;
     old.z = old.z + L.dir.z * dlen;
-    ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x); cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y);
-    ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z);
+    ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x, K.fex); cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y, K.fey);
+    ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z, K.fez);
     if (ci == -1 || cj == -1 || ck == -1) L.tflag = true;
     L.xcell = ci; L.ycell = cj; L.zcell = ck;
     return false;
   }
   if (ci == -1 || cj == -1 || ck == -1) { L.tflag = true; return false; }
-  L.old = old; L.sd = 0.0; L.slen = dlen; L.ci = ci; L.cj = cj; L.ck = ck; L.dda_it = 0;
+  L.old = old; L.sd = 0.0; L.slen = dlen; L.dda_it = 0;
   L.seg = true;
   return true;
 }
@@ -446,30 +445,31 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   // Only the smallest quotient is needed exactly: the three are ranked with hardware
   // reciprocals (relative error far below the 2^-16 margin required), and the one winner
   // is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
-  // or negative distances, NaN), all three are divided exactly as the reference does.
-  // Both paths give the reference's dcell and ldir bit for bit.
+  // or negative distances, a zero direction component, NaN), all three are divided exactly
+  // as the reference does. Both paths give the reference's dcell and ldir bit for bit.
   // the wall each axis moves towards: xface(ci+1) going +, xface(ci) going - (0-based here)
-  const double fx = face<GM>(xf, dir.x > 0.0 ? L.ci : L.ci - 1, K.fex);
-  const double fy = face<GM>(yf, dir.y > 0.0 ? L.cj : L.cj - 1, K.fey);
-  const double fz = face<GM>(zf, dir.z > 0.0 ? L.ck : L.ck - 1, K.fez);
+  const double fx = face<GM>(xf, dir.x > 0.0 ? L.xcell : L.xcell - 1, K.fex);
+  const double fy = face<GM>(yf, dir.y > 0.0 ? L.ycell : L.ycell - 1, K.fey);
+  const double fz = face<GM>(zf, dir.z > 0.0 ? L.zcell : L.zcell - 1, K.fez);
   const double nx = fx - L.old.x;
   const double ny = fy - L.old.y;
   const double nz = fz - L.old.z;
-  const double ax = dir.x == 0.0 ? 100000.0 : nx * __builtin_amdgcn_rcp(dir.x);
-  const double ay = dir.y == 0.0 ? 100000.0 : ny * __builtin_amdgcn_rcp(dir.y);
-  const double az = dir.z == 0.0 ? 100000.0 : nz * __builtin_amdgcn_rcp(dir.z);
-  // (all selects, no branches: the three pairwise minima first, then pick)
-  const double m_yz = dmin(ay, az), m_xz = dmin(ax, az), m_xy = dmin(ax, ay);
-  const bool mx = ax <= ay && ax <= az, my = !mx && ay <= az;
-  const double amin = mx ? ax : (my ? ay : az);
-  const double arest = mx ? m_yz : (my ? m_xz : m_xy);
-  const bool fast = amin > 0.0 && arest > amin * (1.0 + 0x1.0p-16) && ax == ax && ay == ay && az == az;
+  const double ax = nx * __builtin_amdgcn_rcp(dir.x);
+  const double ay = ny * __builtin_amdgcn_rcp(dir.y);
+  const double az = nz * __builtin_amdgcn_rcp(dir.z);
+  // Clear-cut: exactly two estimates lie above the margin over the smallest. (A NaN is
+  // above nothing, so it can never leave two above: such lanes take the exact path.)
+  const double amin = fmin(fmin(ax, ay), az);
+  const double thr = amin * (1.0 + 0x1.0p-16);
+  const bool ux = ax > thr, uy = ay > thr, uz = az > thr;
+  const bool two = ((ux ^ uy) ^ uz) == false && (ux || uy || uz);
+  const bool fast = two && amin > 0.0 && dir.x != 0.0 && dir.y != 0.0 && dir.z != 0.0;
   double dcell;
   bool lx, ly, lz;
   if (fast) {
-    const double num = mx ? nx : (my ? ny : nz), den = mx ? dir.x : (my ? dir.y : dir.z);
-    dcell = den == 0.0 ? 100000.0 : num / den;
-    lx = mx; ly = my; lz = !mx && !my;
+    lx = !ux; ly = !uy; lz = !uz;
+    const double num = lx ? nx : (ly ? ny : nz), den = lx ? dir.x : (ly ? dir.y : dir.z);
+    dcell = num / den;
   } else {
     double dx = -999.0, dy = -999.0, dz = -999.0;
     if (dir.x > 0.0 || dir.x < 0.0) dx = nx / dir.x;
@@ -491,7 +491,7 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   // jmean(cell) += real(dcell,sp)*weight (inttau2.f90:427,434): handed to the caller,
   // which appends a deposit record (binned path) or adds it atomically
   dep = ok;
-  dep_vox = lin(K, L.ci, L.cj, L.ck);
+  dep_vox = lin(K, L.xcell, L.ycell, L.zcell);
   dep_val = (double)(float)dc * L.weight;
   // update_pos (:524-584): .false. (last step) advances all three coordinates by dc;
   // .true. snaps the first axis with ldir set to its wall +- delta (unchanged if its
@@ -505,26 +505,27 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   const bool noaxis = !(lx || ly || lz);  // error stop :570-573
   const bool snap = ok && !last && !noaxis;
   const bool snx = lx, sny = !lx && ly, snz = !lx && !ly;
-  const double px = snap ? (snx ? sx : vx) : (ok && last ? vx : L.old.x);
-  const double py = snap ? (sny ? sy : vy) : (ok && last ? vy : L.old.y);
-  const double pz = snap ? (snz ? sz : vz) : (ok && last ? vz : L.old.z);
-  const int32_t ci = cell_of<GM>(px, K.nx, K.xmax, K.inv2x);  // update_voxels, :587-614
-  const int32_t cj = cell_of<GM>(py, K.ny, K.ymax, K.inv2y);
-  const int32_t ck = cell_of<GM>(pz, K.nz, K.zmax, K.inv2z);
-  const bool left = snap && (ci == -1 || cj == -1 || ck == -1);  // left the grid, :437-440
+  // Without a snap the segment ends here and the DDA position is dead, so only the snap
+  // case is selected (a zero direction component keeps its coordinate: vx == old.x then).
+  const double px = snx && (dir.x > 0.0 || dir.x < 0.0) ? sx : vx;
+  const double py = sny && (dir.y > 0.0 || dir.y < 0.0) ? sy : vy;
+  const double pz = snz && (dir.z > 0.0 || dir.z < 0.0) ? sz : vz;
+  const double gx = cell_floor<GM>(px, K.nx, K.xmax, K.inv2x, K.fex);  // update_voxels, :587-614
+  const double gy = cell_floor<GM>(py, K.ny, K.ymax, K.inv2y, K.fey);
+  const double gz = cell_floor<GM>(pz, K.nz, K.zmax, K.inv2z, K.fez);
+  const bool inx = gx >= 0.0 && gx < (double)K.nx, iny = gy >= 0.0 && gy < (double)K.ny,
+             inz = gz >= 0.0 && gz < (double)K.nz;
+  const bool left = snap && !(inx && iny && inz);  // left the grid, :437-440
   L.old = v3(px, py, pz);
   if (ok) L.sd = last ? L.slen : L.sd + dcell;
-  L.ci = snap ? ci : L.ci;
-  L.cj = snap ? cj : L.cj;
-  L.ck = snap ? ck : L.ck;
+  L.xcell = snap ? (inx ? (int32_t)gx + 1 : -1) : L.xcell;
+  L.ycell = snap ? (iny ? (int32_t)gy + 1 : -1) : L.ycell;
+  L.zcell = snap ? (inz ? (int32_t)gz + 1 : -1) : L.zcell;
   const bool bad = capped || neg || (ok && !last && noaxis);
   L.fault = L.fault || bad;
   L.tflag = L.tflag || bad || left;
   const bool done = bad || (ok && last) || left;
   L.seg = L.seg && !done;
-  L.xcell = done ? L.ci : L.xcell;
-  L.ycell = done ? L.cj : L.ycell;
-  L.zcell = done ? L.ck : L.zcell;
 #ifdef SMCRT_ASM_MARKERS
   asm volatile("; @@DDA_END");
 #endif
