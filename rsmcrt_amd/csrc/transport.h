@@ -108,6 +108,12 @@ __device__ __forceinline__ double cell_floor(double p, int32_t n, double max, do
   const double a = (double)n * p;
   return floor(GM >= 1 ? a * inv : (inv != 0.0 ? a * inv : a / (2.0 * max)));
 }
+// v_cvt_i32_f64 saturates out-of-range values (a C++ conversion of those is undefined)
+__device__ __forceinline__ int32_t cvt_sat_i32(double f) {
+  int32_t r;
+  asm("v_cvt_i32_f64 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+}
 template <int GM>
 __device__ __forceinline__ int32_t cell_of(double p, int32_t n, double max, double inv, int32_t fe) {
   const double f = cell_floor<GM>(p, n, max, inv, fe);
@@ -486,7 +492,8 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   // computing both sides.
   const bool neg = dcell < 0.0;  // error stop :510-516
   const bool ok = !capped && !neg;
-  const bool last = L.sd + dcell > L.slen;
+  const double sdn = L.sd + dcell;
+  const bool last = sdn > L.slen;
   const double dc = last ? L.slen - L.sd : dcell;
   // jmean(cell) += real(dcell,sp)*weight (inttau2.f90:427,434): handed to the caller,
   // which appends a deposit record (binned path) or adds it atomically
@@ -510,22 +517,24 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   const double px = snx && (dir.x > 0.0 || dir.x < 0.0) ? sx : vx;
   const double py = sny && (dir.y > 0.0 || dir.y < 0.0) ? sy : vy;
   const double pz = snz && (dir.z > 0.0 || dir.z < 0.0) ? sz : vz;
-  const double gx = cell_floor<GM>(px, K.nx, K.xmax, K.inv2x, K.fex);  // update_voxels, :587-614
-  const double gy = cell_floor<GM>(py, K.ny, K.ymax, K.inv2y, K.fey);
-  const double gz = cell_floor<GM>(pz, K.nz, K.zmax, K.inv2z, K.fez);
-  const bool inx = gx >= 0.0 && gx < (double)K.nx, iny = gy >= 0.0 && gy < (double)K.ny,
-             inz = gz >= 0.0 && gz < (double)K.nz;
+  // update_voxels, :587-614 (an out-of-range floor converts to an out-of-range integer)
+  const int32_t gx = cvt_sat_i32(cell_floor<GM>(px, K.nx, K.xmax, K.inv2x, K.fex));
+  const int32_t gy = cvt_sat_i32(cell_floor<GM>(py, K.ny, K.ymax, K.inv2y, K.fey));
+  const int32_t gz = cvt_sat_i32(cell_floor<GM>(pz, K.nz, K.zmax, K.inv2z, K.fez));
+  const bool inx = (uint32_t)gx < (uint32_t)K.nx, iny = (uint32_t)gy < (uint32_t)K.ny,
+             inz = (uint32_t)gz < (uint32_t)K.nz;
   const bool left = snap && !(inx && iny && inz);  // left the grid, :437-440
   L.old = v3(px, py, pz);
-  if (ok) L.sd = last ? L.slen : L.sd + dcell;
-  L.xcell = snap ? (inx ? (int32_t)gx + 1 : -1) : L.xcell;
-  L.ycell = snap ? (iny ? (int32_t)gy + 1 : -1) : L.ycell;
-  L.zcell = snap ? (inz ? (int32_t)gz + 1 : -1) : L.zcell;
+  L.sd = sdn;  // (dead once the segment ends, as old is)
+  L.xcell = snap ? (inx ? gx + 1 : -1) : L.xcell;
+  L.ycell = snap ? (iny ? gy + 1 : -1) : L.ycell;
+  L.zcell = snap ? (inz ? gz + 1 : -1) : L.zcell;
   const bool bad = capped || neg || (ok && !last && noaxis);
-  L.fault = L.fault || bad;
-  L.tflag = L.tflag || bad || left;
-  const bool done = bad || (ok && last) || left;
-  L.seg = L.seg && !done;
+  if (bad || left) {  // error stops and leaving the grid: rare, so a (skipped) branch
+    L.fault = L.fault || bad;
+    L.tflag = true;
+  }
+  L.seg = !(bad || (ok && last) || left);
 #ifdef SMCRT_ASM_MARKERS
   asm volatile("; @@DDA_END");
 #endif
