@@ -76,42 +76,55 @@ __device__ __forceinline__ void flush_hist(const KParams& K, const KCold* __rest
   }
 }
 
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
 __device__ __forceinline__ void emit_deposits(const KParams& K, const KCold* __restrict__ C, RecLog& W, bool dep,
                                               uint32_t vox, double val, uint32_t& overflow, uint32_t* whist) {
   const uint64_t m = __ballot(dep);
   if (!m) return;
-  const uint32_t n = __popcll(m);
+  // The cursor arithmetic is wave-uniform; readfirstlane keeps it (and the chunk address) on
+  // the scalar unit, so a lane only pays for its rank, its store and its histogram add.
+  const uint32_t n = (uint32_t)__popcll(m);
   const int lane = threadIdx.x & 63;
-  const uint32_t rank = __popcll(m & ((1ull << lane) - 1ull));
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
   const bool fused = K.hist_tiles != 0;
+  const unsigned long long rec = pack_record(vox, val);
+  const uint32_t fill = uniform(W.fill);
+  uint32_t chunk = uniform(W.chunk);
   uint32_t before = 0;  // lanes that still fit in the current chunk
-  if (W.chunk < K.n_chunks) before = (CHUNK_RECORDS - W.fill) < n ? (CHUNK_RECORDS - W.fill) : n;
-  if (dep && rank < before) {
-    K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + W.fill + rank] = pack_record(vox, val);
-    if (fused) atomicAdd(whist + (vox >> TILE_SHIFT), 1u);
+  if (chunk < K.n_chunks) before = (CHUNK_RECORDS - fill) < n ? (CHUNK_RECORDS - fill) : n;
+  if (before) {
+    unsigned long long* const base = K.rec_pool + ((uint64_t)chunk * CHUNK_RECORDS + fill);
+    if (dep && rank < before) {
+      base[rank] = rec;
+      if (fused) atomicAdd(whist + (vox >> TILE_SHIFT), 1u);
+    }
   }
-  W.fill += before;
+  W.fill = fill + before;
+  W.chunk = chunk;
   if (before < n) {  // chunk full or none yet: retire it, take the next one
     const uint32_t rest = n - before;
-    if (W.chunk != LOG_EXHAUSTED) {
-      if (W.chunk < K.n_chunks && fused) flush_hist(K, C, whist, W.chunk);
-      if (W.chunk < K.n_chunks && lane == 0) C->chunk_fill[W.chunk] = W.fill;
+    if (chunk != LOG_EXHAUSTED) {
+      if (chunk < K.n_chunks && fused) flush_hist(K, C, whist, chunk);
+      if (chunk < K.n_chunks && lane == 0) C->chunk_fill[chunk] = fill + before;
       uint32_t c = 0;
       if (lane == 0) c = atomicAdd(C->dep_ctl, 1u);
-      c = __shfl(c, 0, 64);
-      W.chunk = c < K.n_chunks ? c : LOG_EXHAUSTED;
-      W.fill = 0;
+      c = uniform(c);  // lane 0 (every lane is active here)
+      chunk = c < K.n_chunks ? c : LOG_EXHAUSTED;
     }
-    if (W.chunk < K.n_chunks) {  // rest <= 64 < CHUNK_RECORDS
+    if (chunk < K.n_chunks) {  // rest <= 64 < CHUNK_RECORDS
+      unsigned long long* const base = K.rec_pool + (uint64_t)chunk * CHUNK_RECORDS;
       if (dep && rank >= before) {
-        K.rec_pool[(uint64_t)W.chunk * CHUNK_RECORDS + (rank - before)] = pack_record(vox, val);
+        base[rank - before] = rec;
         if (fused) atomicAdd(whist + (vox >> TILE_SHIFT), 1u);
       }
       W.fill = rest;
     } else {  // pool exhausted: stay correct with fp64 atomics
       if (dep && rank >= before) atomic_add_nr(C->jmean + vox, val);
       overflow += rest;
+      W.fill = 0;
     }
+    W.chunk = chunk;
   }
 }
 
