@@ -16,8 +16,15 @@ module smcrt_mod
     ! smcrt_csg_op
     integer(c_int32_t), parameter :: SMCRT_OP_UNION = 0, SMCRT_OP_SMOOTH_UNION = 1, &
         SMCRT_OP_SUBTRACTION = 2, SMCRT_OP_INTERSECTION = 3
-    ! smcrt_source_kind
-    integer(c_int32_t), parameter :: SMCRT_SRC_POINT = 1, SMCRT_SRC_UNIFORM = 2, SMCRT_SRC_PENCIL = 3
+    ! smcrt_source_kind (photon.f90 emitters)
+    integer(c_int32_t), parameter :: SMCRT_SRC_POINT = 1, SMCRT_SRC_UNIFORM = 2, SMCRT_SRC_PENCIL = 3, &
+        SMCRT_SRC_CIRCULAR = 4, SMCRT_SRC_FOCUS = 5, SMCRT_SRC_ANNULUS = 6, SMCRT_SRC_SLM = 7, &
+        SMCRT_SRC_DSLIT = 8, SMCRT_SRC_APERTURE = 9
+    ! smcrt_beam_kind (focus_type / annulus_type)
+    integer(c_int32_t), parameter :: SMCRT_BEAM_GAUSSIAN = 0, SMCRT_BEAM_SQUARE = 1, SMCRT_BEAM_CIRCLE = 2, &
+        SMCRT_BEAM_TOPHAT = 3, SMCRT_BEAM_BESSEL = 4
+    ! smcrt_spectrum_kind (piecewise.f90)
+    integer(c_int32_t), parameter :: SMCRT_SPEC_CONSTANT = 0, SMCRT_SPEC_1D = 1, SMCRT_SPEC_2D = 2
     ! smcrt_detector_kind
     integer(c_int32_t), parameter :: SMCRT_DET_CIRCLE = 1, SMCRT_DET_ANNULUS = 2, SMCRT_DET_CAMERA = 3, &
         SMCRT_DET_FIBRE = 4
@@ -41,10 +48,25 @@ module smcrt_mod
         real(c_double)     :: xmax, ymax, zmax
     end type smcrt_grid
 
+    type, bind(C) :: smcrt_spectrum
+        integer(c_int32_t) :: kind = 0, reserved = 0
+        real(c_double)     :: wavelength = 500._c_double
+        integer(c_int64_t) :: n = 0
+        type(c_ptr)        :: array = c_null_ptr      ! c_loc(array(1,1)) of an (n,2) real(c_double) array
+        integer(c_int32_t) :: width = 0, height = 0
+        type(c_ptr)        :: image = c_null_ptr      ! c_loc(image(1,1)) of image(width,height)
+        real(c_double)     :: cell_width = 0._c_double, cell_height = 0._c_double
+    end type smcrt_spectrum
+
     type, bind(C) :: smcrt_source
         integer(c_int32_t) :: kind, reserved = 0
         real(c_double)     :: pos(3) = 0._c_double, dir(3) = 0._c_double
         real(c_double)     :: p1(3) = 0._c_double, p2(3) = 0._c_double, p3(3) = 0._c_double
+        integer(c_int32_t) :: beam = 0, reserved2 = 0
+        real(c_double)     :: radius = 0.5_c_double, beam_size = 0.5_c_double, focal_length = 1._c_double
+        real(c_double)     :: rlo = 0.5_c_double, rhi = 0.6_c_double, sigma = 0.04_c_double
+        real(c_double)     :: rotation(3) = 0._c_double
+        type(c_ptr)        :: spectrum = c_null_ptr  ! c_loc of a target smcrt_spectrum, or null (constant 500)
     end type smcrt_source
 
     type, bind(C) :: smcrt_detector

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SMCRT_ABI_VERSION 1
+#define SMCRT_ABI_VERSION 2
 
 typedef enum smcrt_status {
   SMCRT_OK = 0,
@@ -103,16 +103,62 @@ typedef struct smcrt_grid {
 
 /* ----------------------------------------------------------------- source -------- */
 typedef enum smcrt_source_kind {
-  SMCRT_SRC_POINT = 1,   /* isotropic point       photon.f90:311-359 (2 draws)  */
-  SMCRT_SRC_UNIFORM = 2, /* uniform parallelogram photon.f90:566-649 (2 draws)  */
-  SMCRT_SRC_PENCIL = 3   /* pencil beam           photon.f90:652-710 (0 draws)  */
+  SMCRT_SRC_POINT = 1,    /* isotropic point       photon.f90:311-359 (2 draws)          */
+  SMCRT_SRC_UNIFORM = 2,  /* uniform parallelogram photon.f90:566-649 (2 draws)          */
+  SMCRT_SRC_PENCIL = 3,   /* pencil beam           photon.f90:652-710 (0 draws)          */
+  SMCRT_SRC_CIRCULAR = 4, /* uniform disc          photon.f90:214-308 (2 draws)          */
+  SMCRT_SRC_FOCUS = 5,    /* focused beam          photon.f90:361-563 (2 draws)          */
+  SMCRT_SRC_ANNULUS = 6,  /* annular beam          photon.f90:850-1043 (2, gaussian 2k+1) */
+  SMCRT_SRC_SLM = 7,      /* image source          photon.f90:159-212 (2-D spectrum)     */
+  SMCRT_SRC_DSLIT = 8,    /* double slit           photon.f90:712-780 (5 draws)          */
+  SMCRT_SRC_APERTURE = 9  /* square aperture       photon.f90:782-848 (4 draws)          */
 } smcrt_source_kind;
+
+/* Beam profiles: focus_type (photon.f90:394-428) and annulus_type (:878-891). */
+typedef enum smcrt_beam_kind {
+  SMCRT_BEAM_GAUSSIAN = 0, /* focus: radius = beam_size*sqrt(-log(1-ran2)); annulus: rang(mid, sigma) */
+  SMCRT_BEAM_SQUARE = 1,   /* focus only: x, y = ranu(-beam_size, beam_size)                          */
+  SMCRT_BEAM_CIRCLE = 2,   /* focus only: radius = beam_size*sqrt(ran2)                               */
+  SMCRT_BEAM_TOPHAT = 3,   /* annulus only: radius = sqrt(rlo^2 + (rhi^2-rlo^2)*ran2)                 */
+  SMCRT_BEAM_BESSEL = 4    /* annulus only ("besselAnnulus"): radius = rlo + (rhi-rlo)*ran2           */
+} smcrt_beam_kind;
+
+/* Spectrum of a source (piecewise.f90, parse_spectrum.f90:52-117). Every source samples it
+ * once per emission (`spectrum%p%sample`): a constant draws nothing, a 1-D spectrum one
+ * ran2 (inverse CDF, trapezoid weights), a 2-D one (an image, sampled in Morton order) three.
+ * The sampled wavelength only changes the geometry of the dslit and aperture sources; the
+ * slm source takes its (x, y) from a 2-D spectrum. Arrays are host memory, read during
+ * smcrt_run only. */
+typedef enum smcrt_spectrum_kind {
+  SMCRT_SPEC_CONSTANT = 0, /* piecewise.f90:93-107  (getValue)   */
+  SMCRT_SPEC_1D = 1,       /* piecewise.f90:109-168 (sample1D)   */
+  SMCRT_SPEC_2D = 2        /* piecewise.f90:171-236 (sample2D)   */
+} smcrt_spectrum_kind;
+
+typedef struct smcrt_spectrum {
+  int32_t kind, reserved;
+  double wavelength;         /* constant value (parse default 500.0) */
+  int64_t n;                 /* 1-D: rows of array(n, 2) */
+  const double* array;       /* 1-D: Fortran array(n,2): x = array[0..n), y = array[n..2n) */
+  int32_t width, height;     /* 2-D: image(width, height), Fortran order (x fastest) */
+  const double* image;
+  double cell_width, cell_height; /* 2-D: piecewise2D cell_width / cell_height */
+} smcrt_spectrum;
 
 typedef struct smcrt_source {
   int32_t kind, reserved;
-  double pos[3];  /* photon_origin%pos (point, pencil) */
-  double dir[3];  /* photon_origin%n{x,y,z}p (uniform, pencil) */
+  double pos[3];  /* photon_origin%pos (point, pencil, circular, focus, annulus, slm) */
+  double dir[3];  /* photon_origin%n{x,y,z}p (uniform, pencil, circular, slm) */
   double p1[3], p2[3], p3[3]; /* uniform: pos1 + r1*pos2 + r2*pos3 (photon.f90:596-612) */
+  /* ---- ABI 2: the remaining sources of photon.f90 and the source spectrum ---- */
+  int32_t beam;               /* smcrt_beam_kind: focus_type / annulus_type */
+  int32_t reserved2;
+  double radius;              /* circular */
+  double beam_size;           /* focus */
+  double focal_length;        /* focus, annulus: focalLength */
+  double rlo, rhi, sigma;     /* annulus */
+  double rotation[3];         /* focus, annulus: the [source] rotation vector (normalised by the emitter) */
+  const smcrt_spectrum* spectrum; /* NULL: constant 500.0 (no draws) */
 } smcrt_source;
 
 /* ----------------------------------------------------------------- detectors ----- */

@@ -41,6 +41,14 @@ def lib():
             L.oracle_log.argtypes = [C.c_double]
             L.oracle_log.restype = C.c_double
             L.oracle_sincos.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+            L.oracle_spectrum_sample.argtypes = [C.POINTER(abi.Source), C.c_uint64, C.c_uint64, C.c_int64,
+                                                 C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                                 C.POINTER(C.c_uint32)]
+            L.oracle_atan.argtypes = [C.c_double]
+            L.oracle_atan.restype = C.c_double
+            L.oracle_emit.argtypes = [C.POINTER(abi.Grid), C.POINTER(abi.Source), C.c_uint64, C.c_uint64, C.c_int64,
+                                      C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32),
+                                      C.POINTER(C.c_uint32)]
             L.oracle_fresnel.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double, C.c_double]
             L.oracle_fresnel.restype = C.c_double
             L.oracle_reflect_refract.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_double,
@@ -77,6 +85,33 @@ def uniform(seed, pid, draw):
 
 def log(x):
     return lib().oracle_log(float(x))
+
+
+def atan(x):
+    return lib().oracle_atan(float(x))
+
+
+def spectrum_sample(source, n, seed=123456789, first=0):
+    """n draws of source.spectrum (photon p uses its own stream, from draw 0): x, y, draws."""
+    x = np.zeros(n); y = np.zeros(n); dr = np.zeros(n, dtype=np.uint32)
+    st = lib().oracle_spectrum_sample(C.byref(source), seed, first, n, _dp(x), _dp(y),
+                                      dr.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if st != 0:
+        raise RuntimeError(f"oracle_spectrum_sample failed: {abi.STATUS_NAMES.get(st, st)}")
+    return x, y, dr
+
+
+def emit(grid, source, n, seed=123456789, first=0):
+    """One emission of photons [first, first+n) (no re-emission loop): pos (n,3), dir (n,3),
+    cells (n,3), draws (n)."""
+    pos = np.zeros((n, 3)); d = np.zeros((n, 3))
+    cells = np.zeros((n, 3), dtype=np.int32); draws = np.zeros(n, dtype=np.uint32)
+    st = lib().oracle_emit(C.byref(grid), C.byref(source), seed, first, n, _dp(pos), _dp(d),
+                           cells.ctypes.data_as(C.POINTER(C.c_int32)),
+                           draws.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if st != 0:
+        raise RuntimeError(f"oracle_emit failed: {abi.STATUS_NAMES.get(st, st)}")
+    return pos, d, cells, draws
 
 
 def sincos(x):

@@ -208,6 +208,48 @@ ORACLE_API void oracle_sincos(double x, double* s, double* c) {
   }
 }
 
+/* atan, fdlibm s_atan.c (Sun Microsystems, 1993): the fibre detector's acceptance angle */
+ORACLE_API double oracle_atan(double x) {
+  static const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                                   9.82793723247329054082e-01, 1.57079632679489655800e+00};
+  static const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                                   1.39033110312309984516e-17, 6.12323399573676603587e-17};
+  static const double aT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01,
+                                1.42857142725034663711e-01, -1.11111104054623557880e-01,
+                                9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                                6.66107313738753120669e-02, -5.83357013379057348645e-02,
+                                4.97687799461593236017e-02, -3.65315727442169155270e-02,
+                                1.62858201153657823623e-02};
+  uint64_t u = d2u(x);
+  int32_t hx = (int32_t)(u >> 32);
+  uint32_t ix = (uint32_t)hx & 0x7fffffffu;
+  int id;
+  if (ix >= 0x44100000u) {
+    if (ix > 0x7ff00000u || (ix == 0x7ff00000u && (uint32_t)u != 0u)) return x + x;
+    return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3fdc0000u) {
+    if (ix < 0x3e200000u) return x;
+    id = -1;
+  } else {
+    x = fabs(x);
+    if (ix < 0x3ff30000u) {
+      if (ix < 0x3fe60000u) { id = 0; x = (2.0 * x - 1.0) / (2.0 + x); }
+      else { id = 1; x = (x - 1.0) / (x + 1.0); }
+    } else if (ix < 0x40038000u) {
+      id = 2; x = (x - 1.5) / (1.0 + 1.5 * x);
+    } else {
+      id = 3; x = -1.0 / x;
+    }
+  }
+  double z = x * x, w = z * z;
+  double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+  double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+  if (id < 0) return x - x * (s1 + s2);
+  z = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+  return hx < 0 ? -z : z;
+}
+
 /* ====================================================================== vec3 ===== */
 typedef struct { double x, y, z; } vec3;
 static inline vec3 v3(double x, double y, double z) { vec3 r = {x, y, z}; return r; }
@@ -390,6 +432,7 @@ typedef struct {
   uint64_t ctr[SMCRT_NCOUNTERS];
   double nscatt;
   int fault;
+  const struct src_plan* plan; /* general emitter (sources beyond point/uniform/pencil, spectra) */
 } ctx_t;
 
 /* update_voxels, inttau2.f90:587-614 (pos in corner coordinates) */
@@ -576,7 +619,39 @@ static void record_hits(ctx_t* C, vec3 start, vec3 dir, double pointSep, int32_t
         }
       }
     }
-    /* SMCRT_DET_FIBRE: not supported by this restatement (rejected at scene build) */
+    else if (D->kind == SMCRT_DET_FIBRE) {                           /* detectors.f90:331-393 */
+      const double* F = D->fibre;  /* f1, f2, f1Ap, f2Ap, frontOff, backOff, front2pin, pin2back, pinAp, accept, core */
+      int hit = intersect_circle(ddir, vadd(dpos, vmul(ddir, F[4])), F[2], start, dir, &t, &value1D);
+      if (hit && (t <= 0.0 || t > pointSep)) hit = 0;
+      if (hit) {
+        double costt = vdot(ddir, dir);
+        if (costt > 1.0) costt = 1.0;
+        double sintt = sqrt(1.0 - costt * costt);
+        double gradient = sintt / costt;
+        double radius = value1D;
+        gradient = -radius / F[0] + gradient;                         /* thin lens 1 */
+        radius = radius + gradient * F[6];                            /* to the pinhole */
+        if (radius > F[8]) {
+          hit = 0;
+        } else {
+          radius = radius + gradient * F[7];                          /* to lens 2 */
+          if (radius > F[3]) {
+            hit = 0;
+          } else {
+            gradient = -radius / F[1] + gradient;
+            radius = radius + gradient * F[5];                        /* to the fibre */
+            double angle = fabs(oracle_atan(gradient)) * 360.0 / 6.283185307179586;
+            if (angle > F[9] || radius > (F[10] / 2.0)) hit = 0;
+            value1D = fabs(radius);
+          }
+        }
+      }
+      if (hit) {
+        int64_t idx = f_nint(value1D / D->bin_wid) + 1;
+        if (idx > D->nbins) idx = D->nbins;
+        if (idx >= 1) { if (data) data[idx - 1] += weight; C->ctr[SMCRT_CTR_DETECTOR_HITS]++; }
+      }
+    }
   }
 }
 
@@ -820,11 +895,394 @@ static void scatter(ctx_t* C, packet_t* pk, double hgg, rng_t* rng) {  /* photon
   pk->n = v3(uxx, uyy, uzz);
 }
 
+/* ======================================================= general emitter (f3) ===== */
+/* The remaining sources of photon.f90 and the source spectrum of piecewise.f90. The
+ * per-run constants (rotation/translation matrices, CDFs) are computed once per run with the
+ * reference's operations in its order; the per-photon part follows each subroutine. */
+typedef double m4[4][4]; /* m[r][c] = Fortran t(r+1, c+1) */
+
+static void m4_identity(m4 a) { memset(a, 0, sizeof(m4)); for (int i = 0; i < 4; ++i) a[i][i] = 1.0; }
+static void m4_matmul(const m4 A, const m4 B, m4 C) {                /* matmul intrinsic, k ascending */
+  m4 T;
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      double acc = 0.0;
+      for (int k = 0; k < 4; ++k) acc = acc + A[i][k] * B[k][j];
+      T[i][j] = acc;
+    }
+  memcpy(C, T, sizeof(m4));
+}
+/* invert(translate(o)) with mat_class.f90:154-207's direct inverse, written out for a
+ * translation (rows 1-3 identity, row 4 = o): the same products, most of them with 0/1 */
+static void m4_invert(const m4 M, m4 B) {                            /* mat_class.f90:154-207 */
+#define A(i, j) M[(i)-1][(j)-1]
+  double detinv = 1.0 / (A(1,1)*(A(2,2)*(A(3,3)*A(4,4)-A(3,4)*A(4,3))+A(2,3)*(A(3,4)*A(4,2)-A(3,2)*A(4,4))+A(2,4)*(A(3,2)*A(4,3)-A(3,3)*A(4,2)))
+                       - A(1,2)*(A(2,1)*(A(3,3)*A(4,4)-A(3,4)*A(4,3))+A(2,3)*(A(3,4)*A(4,1)-A(3,1)*A(4,4))+A(2,4)*(A(3,1)*A(4,3)-A(3,3)*A(4,1)))
+                       + A(1,3)*(A(2,1)*(A(3,2)*A(4,4)-A(3,4)*A(4,2))+A(2,2)*(A(3,4)*A(4,1)-A(3,1)*A(4,4))+A(2,4)*(A(3,1)*A(4,2)-A(3,2)*A(4,1)))
+                       - A(1,4)*(A(2,1)*(A(3,2)*A(4,3)-A(3,3)*A(4,2))+A(2,2)*(A(3,3)*A(4,1)-A(3,1)*A(4,3))+A(2,3)*(A(3,1)*A(4,2)-A(3,2)*A(4,1))));
+  B[0][0] = detinv*(A(2,2)*(A(3,3)*A(4,4)-A(3,4)*A(4,3))+A(2,3)*(A(3,4)*A(4,2)-A(3,2)*A(4,4))+A(2,4)*(A(3,2)*A(4,3)-A(3,3)*A(4,2)));
+  B[1][0] = detinv*(A(2,1)*(A(3,4)*A(4,3)-A(3,3)*A(4,4))+A(2,3)*(A(3,1)*A(4,4)-A(3,4)*A(4,1))+A(2,4)*(A(3,3)*A(4,1)-A(3,1)*A(4,3)));
+  B[2][0] = detinv*(A(2,1)*(A(3,2)*A(4,4)-A(3,4)*A(4,2))+A(2,2)*(A(3,4)*A(4,1)-A(3,1)*A(4,4))+A(2,4)*(A(3,1)*A(4,2)-A(3,2)*A(4,1)));
+  B[3][0] = detinv*(A(2,1)*(A(3,3)*A(4,2)-A(3,2)*A(4,3))+A(2,2)*(A(3,1)*A(4,3)-A(3,3)*A(4,1))+A(2,3)*(A(3,2)*A(4,1)-A(3,1)*A(4,2)));
+  B[0][1] = detinv*(A(1,2)*(A(3,4)*A(4,3)-A(3,3)*A(4,4))+A(1,3)*(A(3,2)*A(4,4)-A(3,4)*A(4,2))+A(1,4)*(A(3,3)*A(4,2)-A(3,2)*A(4,3)));
+  B[1][1] = detinv*(A(1,1)*(A(3,3)*A(4,4)-A(3,4)*A(4,3))+A(1,3)*(A(3,4)*A(4,1)-A(3,1)*A(4,4))+A(1,4)*(A(3,1)*A(4,3)-A(3,3)*A(4,1)));
+  B[2][1] = detinv*(A(1,1)*(A(3,4)*A(4,2)-A(3,2)*A(4,4))+A(1,2)*(A(3,1)*A(4,4)-A(3,4)*A(4,1))+A(1,4)*(A(3,2)*A(4,1)-A(3,1)*A(4,2)));
+  B[3][1] = detinv*(A(1,1)*(A(3,2)*A(4,3)-A(3,3)*A(4,2))+A(1,2)*(A(3,3)*A(4,1)-A(3,1)*A(4,3))+A(1,3)*(A(3,1)*A(4,2)-A(3,2)*A(4,1)));
+  B[0][2] = detinv*(A(1,2)*(A(2,3)*A(4,4)-A(2,4)*A(4,3))+A(1,3)*(A(2,4)*A(4,2)-A(2,2)*A(4,4))+A(1,4)*(A(2,2)*A(4,3)-A(2,3)*A(4,2)));
+  B[1][2] = detinv*(A(1,1)*(A(2,4)*A(4,3)-A(2,3)*A(4,4))+A(1,3)*(A(2,1)*A(4,4)-A(2,4)*A(4,1))+A(1,4)*(A(2,3)*A(4,1)-A(2,1)*A(4,3)));
+  B[2][2] = detinv*(A(1,1)*(A(2,2)*A(4,4)-A(2,4)*A(4,2))+A(1,2)*(A(2,4)*A(4,1)-A(2,1)*A(4,4))+A(1,4)*(A(2,1)*A(4,2)-A(2,2)*A(4,1)));
+  B[3][2] = detinv*(A(1,1)*(A(2,3)*A(4,2)-A(2,2)*A(4,3))+A(1,2)*(A(2,1)*A(4,3)-A(2,3)*A(4,1))+A(1,3)*(A(2,2)*A(4,1)-A(2,1)*A(4,2)));
+  B[0][3] = detinv*(A(1,2)*(A(2,4)*A(3,3)-A(2,3)*A(3,4))+A(1,3)*(A(2,2)*A(3,4)-A(2,4)*A(3,2))+A(1,4)*(A(2,3)*A(3,2)-A(2,2)*A(3,3)));
+  B[1][3] = detinv*(A(1,1)*(A(2,3)*A(3,4)-A(2,4)*A(3,3))+A(1,3)*(A(2,4)*A(3,1)-A(2,1)*A(3,4))+A(1,4)*(A(2,1)*A(3,3)-A(2,3)*A(3,1)));
+  B[2][3] = detinv*(A(1,1)*(A(2,4)*A(3,2)-A(2,2)*A(3,4))+A(1,2)*(A(2,1)*A(3,4)-A(2,4)*A(3,1))+A(1,4)*(A(2,2)*A(3,1)-A(2,1)*A(3,2)));
+  B[3][3] = detinv*(A(1,1)*(A(2,2)*A(3,3)-A(2,3)*A(3,2))+A(1,2)*(A(2,3)*A(3,1)-A(2,1)*A(3,3))+A(1,3)*(A(2,1)*A(3,2)-A(2,2)*A(3,1)));
+#undef A
+}
+static void m4_translate(vec3 o, m4 a) { m4_identity(a); a[3][0] = o.x; a[3][1] = o.y; a[3][2] = o.z; } /* sdfHelpers.f90:169-182 */
+static vec3 vcross(vec3 a, vec3 b) { return v3(a.y * b.z - a.z * b.y, -a.x * b.z + a.z * b.x, a.x * b.y - a.y * b.x); }
+static vec3 vmagnitude(vec3 a) { double t = vlen(a); return v3(a.x / t, a.y / t, a.z / t); }  /* vector_class.f90:392-402 */
+static int veq(vec3 a, vec3 b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+static void rotation_align(vec3 a, vec3 b, m4 r) {                   /* sdfHelpers.f90:114-140 */
+  vec3 v = vcross(a, b);
+  double c = vdot(a, b);
+  double k = 1.0 / (1.0 + c);
+  m4 vx, vx2, I;
+  memset(vx, 0, sizeof vx);
+  vx[1][0] = -1.0 * v.z; vx[2][0] = v.y;
+  vx[0][1] = v.z;        vx[2][1] = -1.0 * v.x;
+  vx[0][2] = -1.0 * v.y; vx[1][2] = v.x;
+  m4_matmul(vx, vx, vx2);
+  m4_identity(I);
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) r[i][j] = (I[i][j] + vx[i][j]) + vx2[i][j] * k;
+}
+static void m4_colmajor(const m4 a, double* o) { for (int c = 0; c < 4; ++c) for (int r = 0; r < 4; ++r) o[c * 4 + r] = a[r][c]; }
+
+typedef struct src_plan {
+  smcrt_source src;
+  int spec_kind;
+  int circ_z;
+  double T[16], R[16];
+  double wavelength;
+  int64_t n;         /* 1-D rows / 2-D CDF entries */
+  double* x;         /* 1-D abscissae */
+  double* cdf;
+  int32_t xoff, yoff;
+  double cw, ch;
+} src_plan_t;
+
+static uint32_t pack_bits(uint64_t x) {                              /* piecewise.f90:296-315 */
+  x &= 0x5555555555555555ull;
+  x = (x >> 1) | x; x &= 0x3333333333333333ull;
+  x = (x >> 2) | x; x &= 0x0F0F0F0F0F0F0F0Full;
+  x = (x >> 4) | x; x &= 0x00FF00FF00FF00FFull;
+  x = (x >> 8) | x; x &= 0x0000FFFF0000FFFFull;
+  x = (x >> 16) | x;
+  return (uint32_t)x;
+}
+static int32_t nextpwr2(int32_t v) {                                 /* piecewise.f90:238-252 */
+  uint32_t r = (uint32_t)v - 1u;
+  r |= r >> 1; r |= r >> 2; r |= r >> 4; r |= r >> 8; r |= r >> 16;
+  return (int32_t)(r + 1u);
+}
+
+static void free_plan(src_plan_t* P) { free(P->x); free(P->cdf); P->x = P->cdf = NULL; }
+
+static int build_plan(src_plan_t* P, const smcrt_source* s) {
+  memset(P, 0, sizeof *P);
+  P->src = *s;
+  P->wavelength = 500.0;                                             /* parse_spectrum.f90:55 */
+  m4 T, R;
+  m4_identity(T); m4_identity(R);
+  if (s->kind == SMCRT_SRC_CIRCULAR) {                               /* photon.f90:239-264 */
+    vec3 a = vmagnitude(v3(1.0, 0.0, 0.0));
+    vec3 b = vmagnitude(v3(s->dir[0], s->dir[1], s->dir[2]));
+    if (veq(vabs(a), vabs(b))) { a = vmagnitude(v3(0.0, 0.0, 1.0)); P->circ_z = 1; }
+    m4 ra, tr, inv;
+    rotation_align(a, b, ra);
+    m4_translate(v3(s->pos[0], s->pos[1], s->pos[2]), tr);
+    m4_invert(tr, inv);
+    m4_matmul(ra, inv, T);
+  } else if (s->kind == SMCRT_SRC_FOCUS || s->kind == SMCRT_SRC_ANNULUS) {  /* :445-485, :917-957 */
+    if (s->kind == SMCRT_SRC_FOCUS && s->beam != SMCRT_BEAM_SQUARE && s->beam != SMCRT_BEAM_CIRCLE &&
+        s->beam != SMCRT_BEAM_GAUSSIAN) return SMCRT_ERR_INVALID_ARG;
+    if (s->kind == SMCRT_SRC_ANNULUS && s->beam != SMCRT_BEAM_TOPHAT && s->beam != SMCRT_BEAM_BESSEL &&
+        s->beam != SMCRT_BEAM_GAUSSIAN) return SMCRT_ERR_INVALID_ARG;
+    vec3 rot = v3(s->rotation[0], s->rotation[1], s->rotation[2]);
+    if (vlen(rot) < 1e-8) return SMCRT_ERR_INVALID_ARG;              /* parse_source.f90:84-88 */
+    vec3 a = vmagnitude(v3(0.0, 0.0, -1.0)), b = vmagnitude(rot);
+    vec3 start = v3(-s->pos[0], -s->pos[1], -s->pos[2]);
+    m4 t;
+    int flip = veq(vabs(a), vabs(b));
+    if (veq(a, b)) m4_identity(t);
+    else if (flip) { m4_identity(t); t[2][2] = -1.0; }
+    else rotation_align(a, b, t);
+    memcpy(R, t, sizeof(m4));
+    if (flip && !veq(a, b)) t[2][2] = 1.0;
+    m4 tr, inv;
+    m4_translate(start, tr);
+    m4_invert(tr, inv);
+    m4_matmul(t, inv, T);
+  } else if (s->kind < SMCRT_SRC_POINT || s->kind > SMCRT_SRC_APERTURE) {
+    return SMCRT_ERR_INVALID_ARG;
+  }
+  m4_colmajor(T, P->T);
+  m4_colmajor(R, P->R);
+  const smcrt_spectrum* sp = s->spectrum;
+  P->spec_kind = sp ? sp->kind : SMCRT_SPEC_CONSTANT;
+  if (sp && sp->kind == SMCRT_SPEC_CONSTANT) {
+    P->wavelength = sp->wavelength;
+  } else if (sp && sp->kind == SMCRT_SPEC_1D) {                      /* init_piecewise1D :140-168 */
+    int64_t n = sp->n;
+    if (n < 2 || !sp->array) return SMCRT_ERR_INVALID_ARG;
+    const double* x = sp->array;
+    const double* y = sp->array + n;
+    P->x = malloc((size_t)n * sizeof(double));
+    P->cdf = calloc((size_t)n, sizeof(double));
+    memcpy(P->x, x, (size_t)n * sizeof(double));
+    double sumer = 0.0;
+    for (int64_t i = 1; i < n; ++i) {                                /* do i = 2, length */
+      /* trapz_weights (stdlib): ends 0.5*(x2-x1), 0.5*(xn-xn-1); inside 0.5*(x(i+1)-x(i-1)) */
+      double w = (n == 2 || i == n - 1) ? 0.5 * (x[n - 1] - x[n - 2]) : 0.5 * (x[i + 1] - x[i - 1]);
+      sumer = sumer + w * y[i];
+      P->cdf[i] = sumer;
+    }
+    double last = P->cdf[n - 1];
+    for (int64_t i = 0; i < n; ++i) P->cdf[i] = P->cdf[i] / last;
+    P->n = n;
+  } else if (sp && sp->kind == SMCRT_SPEC_2D) {                      /* init_piecewise2D :190-236 */
+    int32_t width = sp->width, height = sp->height;
+    if (width < 1 || height < 1 || !sp->image) return SMCRT_ERR_INVALID_ARG;
+    int32_t w2 = nextpwr2(width), h2 = nextpwr2(height);
+    P->xoff = (h2 - height) / 2;
+    P->yoff = (w2 - width) / 2;
+    int32_t x0 = P->xoff > 0 ? P->xoff - 1 : 0, y0 = P->yoff > 0 ? P->yoff - 1 : 0;
+    if (x0 + width > w2 || y0 + height > h2) return SMCRT_ERR_INVALID_ARG;
+    int64_t N = (int64_t)w2 * h2;
+    double* img = calloc((size_t)N, sizeof(double));
+    for (int32_t j = 0; j < height; ++j)
+      for (int32_t i = 0; i < width; ++i)
+        img[(size_t)(x0 + i) + (size_t)w2 * (size_t)(y0 + j)] = sp->image[(size_t)i + (size_t)width * j];
+    P->cdf = calloc((size_t)N, sizeof(double));
+    for (int64_t i = 0; i < N; ++i) {
+      uint64_t li = (uint64_t)pack_bits((uint64_t)i) + (uint64_t)w2 * pack_bits((uint64_t)i >> 1);
+      double h = li < (uint64_t)N ? img[li] : 0.0;
+      P->cdf[i] = i == 0 ? h : P->cdf[i - 1] + h;
+    }
+    free(img);
+    double last = P->cdf[N - 1];
+    for (int64_t i = 0; i < N; ++i) P->cdf[i] = P->cdf[i] / last;
+    P->n = N;
+    P->cw = sp->cell_width; P->ch = sp->cell_height;
+  } else if (sp) {
+    return SMCRT_ERR_INVALID_ARG;
+  }
+  if (s->kind == SMCRT_SRC_SLM && P->spec_kind == SMCRT_SPEC_1D) { free_plan(P); return SMCRT_ERR_INVALID_ARG; }
+  return SMCRT_OK;
+}
+
+static int64_t search_1d(const double* a, int64_t n, double v) {     /* piecewise.f90:254-275 */
+  int64_t nup = n, nlow = 1;
+  while ((nup - nlow) > 1) {
+    int64_t middle = (int64_t)((float)(nup + nlow) / 2.0f);            /* int((nup+nlow)/2.), default real */
+    if (v > a[middle - 1]) nlow = middle; else nup = middle;
+  }
+  return nlow;
+}
+static double ranu(rng_t* r, double a, double b) { return a + ran2(r) * (b - a); }  /* random_mod.f90:93-103 */
+
+static void spec_sample(const src_plan_t* P, rng_t* r, double* x, double* y) {
+  if (P->spec_kind == SMCRT_SPEC_1D) {                               /* sample1D :109-137 */
+    double val = ran2(r);
+    int64_t i = search_1d(P->cdf, P->n, val);
+    *x = P->x[i - 1] + ((val - P->cdf[i - 1]) * (P->x[i] - P->x[i - 1])) / (P->cdf[i] - P->cdf[i - 1]);
+    *y = 0.0;
+  } else if (P->spec_kind == SMCRT_SPEC_2D) {                        /* sample2D :171-188 */
+    double val = ran2(r);
+    int64_t i = search_1d(P->cdf, P->n, val);
+    int32_t xr = (int32_t)pack_bits((uint64_t)i), yr = (int32_t)pack_bits((uint64_t)i >> 1);
+    *x = (double)(xr - P->xoff) + ranu(r, -P->cw, P->cw);
+    *y = (double)(yr - P->yoff) + ranu(r, -P->ch, P->ch);
+  } else {                                                           /* getValue :93-107 */
+    *x = P->wavelength;
+    *y = -9999.0;
+  }
+}
+
+static void nudge(const scene_t* S, vec3* p) {                       /* e.g. photon.f90:614-628 */
+  const double xmax = S->grid.xmax, ymax = S->grid.ymax, zmax = S->grid.zmax;
+  if (p->x == -xmax) p->x = p->x + 7.9e-7; else if (p->x == xmax) p->x = p->x - 7.9e-7;
+  if (p->y == -ymax) p->y = p->y + 7.9e-7; else if (p->y == ymax) p->y = p->y - 7.9e-7;
+  if (p->z == -zmax) p->z = p->z + 7.9e-7; else if (p->z == zmax) p->z = p->z - 7.9e-7;
+}
+
+static void emit_ext(ctx_t* C, packet_t* pk, rng_t* rng) {
+  const scene_t* S = C->S;
+  const src_plan_t* P = C->plan;
+  const smcrt_source* s = &P->src;
+  const double TWOPI = 6.283185307179586;
+  double wl, tmp;
+  switch (s->kind) {
+    case SMCRT_SRC_POINT: {                                          /* photon.f90:311-359 */
+      pk->pos = v3(s->pos[0], s->pos[1], s->pos[2]);
+      double phi = ran2(rng) * TWOPI, sinp, cosp;
+      oracle_sincos(phi, &sinp, &cosp);
+      double cost = 2.0 * ran2(rng) - 1.0;
+      double sint = sqrt(1.0 - cost * cost);
+      pk->n = v3(sint * cosp, sint * sinp, cost);
+      pk->layer = 1;
+      spec_sample(P, rng, &wl, &tmp);
+      break;
+    }
+    case SMCRT_SRC_UNIFORM: {                                        /* :566-649 */
+      double rx = ran2(rng), ry = ran2(rng);
+      pk->n = v3(s->dir[0], s->dir[1], s->dir[2]);
+      pk->pos = v3(s->p1[0] + rx * s->p2[0] + ry * s->p3[0], s->p1[1] + rx * s->p2[1] + ry * s->p3[1],
+                   s->p1[2] + rx * s->p2[2] + ry * s->p3[2]);
+      nudge(S, &pk->pos);
+      spec_sample(P, rng, &wl, &tmp);
+      break;
+    }
+    case SMCRT_SRC_PENCIL: {                                         /* :652-710 */
+      pk->pos = v3(s->pos[0], s->pos[1], s->pos[2]);
+      nudge(S, &pk->pos);
+      pk->n = v3(s->dir[0], s->dir[1], s->dir[2]);
+      pk->layer = 1;
+      spec_sample(P, rng, &wl, &tmp);
+      break;
+    }
+    case SMCRT_SRC_CIRCULAR: {                                       /* :214-308 */
+      pk->n = v3(s->dir[0], s->dir[1], s->dir[2]);
+      double r = s->radius * sqrt(ran2(rng));
+      double theta = ran2(rng) * TWOPI, st, ct;
+      oracle_sincos(theta, &st, &ct);
+      vec3 q = P->circ_z ? v3(r * ct, r * st, 0.0) : v3(0.0, r * ct, r * st);
+      vec3 t = vdotmat(q, P->T);
+      pk->pos = v3(-t.x, -t.y, -t.z);
+      nudge(S, &pk->pos);
+      spec_sample(P, rng, &wl, &tmp);
+      pk->layer = 1;
+      break;
+    }
+    case SMCRT_SRC_FOCUS:                                            /* :361-563 */
+    case SMCRT_SRC_ANNULUS: {                                        /* :850-1043 */
+      vec3 q, qd;
+      if (s->kind == SMCRT_SRC_FOCUS) {
+        if (s->beam == SMCRT_BEAM_SQUARE) {
+          double x = ranu(rng, -s->beam_size, s->beam_size);
+          double y = ranu(rng, -s->beam_size, s->beam_size);
+          q = v3(x, y, 0.0);
+        } else {
+          double radius = s->beam == SMCRT_BEAM_CIRCLE ? s->beam_size * sqrt(ran2(rng))
+                                                       : s->beam_size * sqrt(-oracle_log(1.0 - ran2(rng)));
+          double phi = TWOPI * ran2(rng), sinp, cosp;
+          oracle_sincos(phi, &sinp, &cosp);
+          q = v3(radius * cosp, radius * sinp, 0.0);
+        }
+        qd = q;
+      } else {
+        double radius, mid;
+        if (s->beam == SMCRT_BEAM_TOPHAT) {
+          radius = sqrt(s->rlo * s->rlo + (s->rhi * s->rhi - s->rlo * s->rlo) * ran2(rng));
+          mid = (s->rhi + s->rlo) / 2.0;
+        } else if (s->beam == SMCRT_BEAM_BESSEL) {
+          radius = s->rlo + (s->rhi - s->rlo) * ran2(rng);
+          mid = (s->rhi + s->rlo) / 2.0;
+        } else {                                                     /* rang, random_mod.f90:105-127 */
+          mid = (s->rhi + s->rlo) / 2.0;
+          double x = 0.0, y = 0.0, sq = 1.0;
+          int tries = 0;
+          while (sq >= 1.0) {
+            if (++tries > 1000) { C->fault = 1; break; }
+            x = ranu(rng, -1.0, 1.0);
+            y = ranu(rng, -1.0, 1.0);
+            sq = y * y + x * x;
+          }
+          radius = mid + s->sigma * (x * sqrt(-2.0 * oracle_log(sq) / sq));
+        }
+        double phi = TWOPI * ran2(rng), sinp, cosp;
+        oracle_sincos(phi, &sinp, &cosp);
+        q = v3(radius * cosp, radius * sinp, 0.0);
+        qd = v3(mid * cosp, mid * sinp, 0.0);
+      }
+      /* dir = magnitude(sign(1,f)*((-1)*(q - targ)/dist)), rotated, renormalised */
+      vec3 d0 = vsub(qd, v3(0.0, 0.0, -s->focal_length));
+      double dist = vlen(d0);
+      vec3 d = smul(-1.0, d0);
+      d = v3(d.x / dist, d.y / dist, d.z / dist);
+      d = vmul(d, copysign(1.0, s->focal_length));
+      d = vmagnitude(d);
+      pk->n = vmagnitude(vdotmat(d, P->R));
+      pk->pos = vdotmat(q, P->T);
+      spec_sample(P, rng, &wl, &tmp);
+      /* step into the grid, photon.f90:505-556 (focus: counter > 4; annulus :985-1036: > 3) */
+      int cap = s->kind == SMCRT_SRC_FOCUS ? 4 : 3;
+      int inX = 0, inY = 0, inZ = 0, tX = 0, tY = 0, tZ = 0, counter = 0;
+      const double xmax = S->grid.xmax, ymax = S->grid.ymax, zmax = S->grid.zmax;
+      vec3* p = &pk->pos;
+      vec3 dd = pk->n;
+      while (!inX || !inY || !inZ) {
+        double st;
+        if (p->x <= -xmax) { st = (-xmax - p->x + 9e-7) / dd.x; *p = v3(p->x + dd.x * st, p->y + dd.y * st, p->z + dd.z * st); tX = 1; }
+        else if (p->x >= xmax) { st = (xmax - p->x - 9e-7) / dd.x; *p = v3(p->x + dd.x * st, p->y + dd.y * st, p->z + dd.z * st); tX = 1; }
+        else inX = 1;
+        if (p->y <= -ymax) { st = (-ymax - p->y + 9e-7) / dd.y; *p = v3(p->x + dd.x * st, p->y + dd.y * st, p->z + dd.z * st); tY = 1; }
+        else if (p->y >= ymax) { st = (ymax - p->y - 9e-7) / dd.y; *p = v3(p->x + dd.x * st, p->y + dd.y * st, p->z + dd.z * st); tY = 1; }
+        else inY = 1;
+        if (p->z <= -zmax) { st = (-zmax - p->z + 9e-7) / dd.z; *p = v3(p->x + dd.x * st, p->y + dd.y * st, p->z + dd.z * st); tZ = 1; }
+        else if (p->z >= zmax) { st = (zmax - p->z - 9e-7) / dd.z; *p = v3(p->x + dd.x * st, p->y + dd.y * st, p->z + dd.z * st); tZ = 1; }
+        else inZ = 1;
+        if ((tX && tY && tZ) || counter > cap) break;
+        counter = counter + 1;
+      }
+      break;
+    }
+    case SMCRT_SRC_SLM: {                                            /* :159-212 */
+      double x, y;
+      spec_sample(P, rng, &x, &y);
+      pk->pos = v3((x - 100.0) / ((double)S->grid.nx / (2.0 * S->grid.xmax)),
+                   (y - 100.0) / ((double)S->grid.ny / (2.0 * S->grid.ymax)), s->pos[2]);
+      pk->n = v3(s->dir[0], s->dir[1], s->dir[2]);
+      pk->layer = 1;
+      break;
+    }
+    default: {                                                       /* dslit :712-780, aperture :782-848 */
+      spec_sample(P, rng, &wl, &tmp);
+      double x1, y1, z1, x2, y2, z2;
+      if (s->kind == SMCRT_SRC_DSLIT) {
+        double a = 60.0 * wl, b = 20.0 * wl;
+        if (ran2(rng) > 0.5) { x1 = ranu(rng, a / 2.0, a / 2.0 + b); y1 = ranu(rng, -b * 0.5, b * 0.5); }
+        else { x1 = ranu(rng, -a / 2.0, -a / 2.0 - b); y1 = ranu(rng, -b * 0.5, b * 0.5); }
+        z2 = 5.0 - (1.e-5 * (2.0 * (5.0 / 400.0)));
+        x2 = ranu(rng, -5.0, 5.0);
+        y2 = ranu(rng, -5.0, 5.0);
+        z1 = (10000.0 * wl) - 5.0;
+      } else {
+        double apwid = 200e-6, b = apwid / 2.0, F = 4.95;
+        x1 = ranu(rng, -b, b);
+        y1 = ranu(rng, -b, b);
+        double fa = F / apwid;
+        z1 = (1.0 / (((fa * fa) / 2.0) * wl)) - 0.5;
+        x2 = ranu(rng, -0.5, 0.5);
+        y2 = ranu(rng, -0.5, 0.5);
+        z2 = 0.5 - (1.e-5 * (2.0 * 0.5 / 400.0));
+      }
+      pk->pos = v3(x2, y2, z2);
+      double dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
+      double phase = sqrt(dx * dx + dy * dy + dz * dz);
+      pk->n = v3(dx / phase, dy / phase, -fabs(dz) / phase);
+      break;
+    }
+  }
+}
+
 /* ==================================================================== emit ===== */
 static void emit(ctx_t* C, const smcrt_source* src, packet_t* pk, rng_t* rng) {
   const scene_t* S = C->S;
   const double xmax = S->grid.xmax, ymax = S->grid.ymax, zmax = S->grid.zmax;
-  if (src->kind == SMCRT_SRC_POINT) {                                /* photon.f90:311-359 */
+  if (C->plan) {
+    emit_ext(C, pk, rng);
+  } else if (src->kind == SMCRT_SRC_POINT) {                         /* photon.f90:311-359 */
     pk->pos = v3(src->pos[0], src->pos[1], src->pos[2]);
     double phi = ran2(rng) * 6.283185307179586;
     double sinp, cosp;
@@ -974,8 +1432,6 @@ static int build_scene(scene_t* S, const smcrt_sdf_node* nodes, int32_t n_nodes,
   if (grid->nx < 1 || grid->ny < 1 || grid->nz < 1) return SMCRT_ERR_INVALID_ARG;
   for (int32_t i = 0; i < n_top; ++i)
     if (top[i] < 0 || top[i] >= n_nodes) return SMCRT_ERR_INVALID_ARG;
-  for (int32_t i = 0; i < n_dets; ++i)
-    if (dets[i].kind == SMCRT_DET_FIBRE) return SMCRT_ERR_UNSUPPORTED;
   S->nodes = nodes; S->n_nodes = n_nodes; S->top = top; S->n_top = n_top; S->grid = *grid;
   S->dets = dets; S->n_dets = n_dets;
   S->kappa = calloc(6 * (size_t)n_top, sizeof(double));
@@ -1033,10 +1489,15 @@ ORACLE_API int oracle_run(const smcrt_sdf_node* nodes, int32_t n_nodes, const in
   scene_t S;
   int st = build_scene(&S, nodes, n_nodes, top, n_top, grid, dets, n_dets);
   if (st) return st;
-  if (!src || !cfg || !io ||
-      (src->kind != SMCRT_SRC_POINT && src->kind != SMCRT_SRC_UNIFORM && src->kind != SMCRT_SRC_PENCIL)) {
+  if (!src || !cfg || !io || src->kind < SMCRT_SRC_POINT || src->kind > SMCRT_SRC_APERTURE) {
     free_scene(&S);
     return SMCRT_ERR_INVALID_ARG;
+  }
+  src_plan_t plan;
+  const int use_plan = src->kind > SMCRT_SRC_PENCIL || (src->spectrum && src->spectrum->kind != SMCRT_SPEC_CONSTANT);
+  if (use_plan && (st = build_plan(&plan, src)) != SMCRT_OK) {
+    free_scene(&S);
+    return st;
   }
   int64_t nv = (int64_t)grid->nx * grid->ny * grid->nz;
   ctx_t C;
@@ -1048,6 +1509,7 @@ ORACLE_API int oracle_run(const smcrt_sdf_node* nodes, int32_t n_nodes, const in
   C.emission = (io->emission || io->emission_f64) ? calloc((size_t)nv, sizeof(double)) : NULL;
   C.det = io->det_bins;
   C.moments = io->moments;
+  C.plan = use_plan ? &plan : NULL;
   double* ds = calloc(2 * (size_t)n_top, sizeof(double));
   for (uint64_t j = 0; j < cfg->n_photons; ++j) {
     smcrt_photon_record* rec = (io->records && (cfg->flags & SMCRT_FLAG_RECORD_PHOTONS)) ? &io->records[j] : NULL;
@@ -1068,6 +1530,40 @@ ORACLE_API int oracle_run(const smcrt_sdf_node* nodes, int32_t n_nodes, const in
   if (io->counters)
     for (int i = 0; i < SMCRT_NCOUNTERS; ++i) io->counters[i] += C.ctr[i];
   free(ds);
+  if (use_plan) free_plan(&plan);
+  free_scene(&S);
+  return SMCRT_OK;
+}
+
+/* One emission (no re-emission loop) of photons [first, first+n): pos/dir (3 each),
+ * cells (3) and RNG draws per photon, for the source unit checks of test/photon. */
+ORACLE_API int oracle_emit(const smcrt_grid* grid, const smcrt_source* src, uint64_t seed, uint64_t first,
+                           int64_t n, double* pos, double* dir, int32_t* cells, uint32_t* draws) {
+  static const int32_t top0 = 0;
+  smcrt_sdf_node nd;
+  memset(&nd, 0, sizeof nd);
+  nd.kind = SMCRT_SDF_SPHERE; nd.param[0] = 1.0; nd.n = 1.0;
+  for (int i = 0; i < 4; ++i) nd.transform[i * 5] = 1.0;
+  scene_t S;
+  int st = build_scene(&S, &nd, 1, &top0, 1, grid, NULL, 0);
+  if (st) return st;
+  src_plan_t plan;
+  if ((st = build_plan(&plan, src)) != SMCRT_OK) { free_scene(&S); return st; }
+  ctx_t C;
+  memset(&C, 0, sizeof C);
+  C.S = &S;
+  C.plan = &plan;
+  for (int64_t j = 0; j < n; ++j) {
+    rng_t rng = {first + (uint64_t)j, seed, 0};
+    packet_t pk;
+    memset(&pk, 0, sizeof pk);
+    emit(&C, src, &pk, &rng);
+    pos[3 * j] = pk.pos.x; pos[3 * j + 1] = pk.pos.y; pos[3 * j + 2] = pk.pos.z;
+    dir[3 * j] = pk.n.x; dir[3 * j + 1] = pk.n.y; dir[3 * j + 2] = pk.n.z;
+    cells[3 * j] = pk.xcell; cells[3 * j + 1] = pk.ycell; cells[3 * j + 2] = pk.zcell;
+    draws[j] = rng.draws;
+  }
+  free_plan(&plan);
   free_scene(&S);
   return SMCRT_OK;
 }
@@ -1085,5 +1581,20 @@ ORACLE_API int oracle_record_hit(const smcrt_detector* det, const double start[3
   C.det = bins;
   record_hits(&C, v3(start[0], start[1], start[2]), v3(dir[0], dir[1], dir[2]), pointSep, layer, weight);
   if (hits) *hits = C.ctr[SMCRT_CTR_DETECTOR_HITS];
+  return SMCRT_OK;
+}
+
+/* n samples of a source spectrum (sample of piecewise.f90; unit checks of test/optical_props) */
+ORACLE_API int oracle_spectrum_sample(const smcrt_source* src, uint64_t seed, uint64_t first, int64_t n,
+                                      double* x, double* y, uint32_t* draws) {
+  src_plan_t plan;
+  int st = build_plan(&plan, src);
+  if (st) return st;
+  for (int64_t j = 0; j < n; ++j) {
+    rng_t rng = {first + (uint64_t)j, seed, 0};
+    spec_sample(&plan, &rng, &x[j], &y[j]);
+    if (draws) draws[j] = rng.draws;
+  }
+  free_plan(&plan);
   return SMCRT_OK;
 }

@@ -5,7 +5,7 @@ against the library's own view of them.
 """
 import ctypes as C
 
-SMCRT_ABI_VERSION = 1
+SMCRT_ABI_VERSION = 2
 
 # smcrt_status
 OK = 0
@@ -30,8 +30,20 @@ SDF_SEGMENT, SDF_CAPSULE, SDF_CONE, SDF_EGG, SDF_PLANE, SDF_MODEL = 6, 7, 8, 9, 
 # smcrt_csg_op (src/sdfs/sdfModifiers.f90:428-491)
 OP_UNION, OP_SMOOTH_UNION, OP_SUBTRACTION, OP_INTERSECTION = 0, 1, 2, 3
 
-# smcrt_source_kind
+# smcrt_source_kind (reference src/photon.f90 emitters)
 SRC_POINT, SRC_UNIFORM, SRC_PENCIL = 1, 2, 3
+SRC_CIRCULAR, SRC_FOCUS, SRC_ANNULUS, SRC_SLM, SRC_DSLIT, SRC_APERTURE = 4, 5, 6, 7, 8, 9
+SOURCE_KINDS = {"point": SRC_POINT, "uniform": SRC_UNIFORM, "pencil": SRC_PENCIL, "circular": SRC_CIRCULAR,
+                "focus": SRC_FOCUS, "annulus": SRC_ANNULUS, "slm": SRC_SLM, "dslit": SRC_DSLIT,
+                "aperture": SRC_APERTURE}
+
+# smcrt_beam_kind: focus_type / annulus_type
+BEAM_GAUSSIAN, BEAM_SQUARE, BEAM_CIRCLE, BEAM_TOPHAT, BEAM_BESSEL = 0, 1, 2, 3, 4
+BEAM_KINDS = {"gaussian": BEAM_GAUSSIAN, "square": BEAM_SQUARE, "circle": BEAM_CIRCLE, "tophat": BEAM_TOPHAT,
+              "besselAnnulus": BEAM_BESSEL}
+
+# smcrt_spectrum_kind (src/opticalProps/piecewise.f90)
+SPEC_CONSTANT, SPEC_1D, SPEC_2D = 0, 1, 2
 
 # smcrt_detector_kind
 DET_CIRCLE, DET_ANNULUS, DET_CAMERA, DET_FIBRE = 1, 2, 3, 4
@@ -70,10 +82,21 @@ class Grid(C.Structure):
                 ("xmax", C.c_double), ("ymax", C.c_double), ("zmax", C.c_double)]
 
 
+class Spectrum(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("wavelength", C.c_double),
+                ("n", C.c_int64), ("array", C.POINTER(C.c_double)),
+                ("width", C.c_int32), ("height", C.c_int32), ("image", C.POINTER(C.c_double)),
+                ("cell_width", C.c_double), ("cell_height", C.c_double)]
+
+
 class Source(C.Structure):
     _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32),
                 ("pos", C.c_double * 3), ("dir", C.c_double * 3),
-                ("p1", C.c_double * 3), ("p2", C.c_double * 3), ("p3", C.c_double * 3)]
+                ("p1", C.c_double * 3), ("p2", C.c_double * 3), ("p3", C.c_double * 3),
+                ("beam", C.c_int32), ("reserved2", C.c_int32),
+                ("radius", C.c_double), ("beam_size", C.c_double), ("focal_length", C.c_double),
+                ("rlo", C.c_double), ("rhi", C.c_double), ("sigma", C.c_double),
+                ("rotation", C.c_double * 3), ("spectrum", C.POINTER(Spectrum))]
 
 
 class Detector(C.Structure):

@@ -13,9 +13,9 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libsmcrt.so")
-SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp")]
+SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("transport.h", "detmath.h", "geometry.h", "deposit.h",
-                                                         "hosterr.h", "toml.h")] + [
+                                                         "hosterr.h", "toml.h", "mat4.h", "srcplan.h", "png.h")] + [
     os.path.join(ROOT, "include", "smcrt.h")]
 ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no fused multiply-add, so fp64 trajectories are bit-identical to the
@@ -41,7 +41,7 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
-    cmd = [hipcc(), *FLAGS, "-o", LIB + ".tmp", *SOURCES]
+    cmd = [hipcc(), *FLAGS, "-o", LIB + ".tmp", *SOURCES, "-lz"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

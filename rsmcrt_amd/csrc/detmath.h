@@ -173,4 +173,50 @@ __device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
   }
 }
 
+
+// atan (fdlibm s_atan.c), for the fibre detector's acceptance angle (detectors.f90:386).
+__device__ inline double det_atan(double x) {
+  const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                            1.57079632679489655800e+00};
+  const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                            6.12323399573676603587e-17};
+  const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+               aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+               aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+               aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+               aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+               aT10 = 1.62858201153657823623e-02;
+  const uint64_t u = d2u(x);
+  const int32_t hx = (int32_t)(u >> 32);
+  const uint32_t ix = (uint32_t)hx & 0x7fffffffu;
+  int id;
+  if (ix >= 0x44100000u) {  // |x| >= 2^66 (or NaN)
+    if (ix > 0x7ff00000u || (ix == 0x7ff00000u && (uint32_t)u != 0u)) return x + x;
+    return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+  }
+  if (ix < 0x3fdc0000u) {  // |x| < 0.4375
+    if (ix < 0x3e200000u) return x;  // |x| < 2^-29
+    id = -1;
+  } else {
+    x = fabs(x);
+    if (ix < 0x3ff30000u) {    // |x| < 1.1875
+      if (ix < 0x3fe60000u) {  // 7/16 <= |x| < 11/16
+        id = 0; x = (2.0 * x - 1.0) / (2.0 + x);
+      } else {
+        id = 1; x = (x - 1.0) / (x + 1.0);
+      }
+    } else if (ix < 0x40038000u) {  // |x| < 2.4375
+      id = 2; x = (x - 1.5) / (1.0 + 1.5 * x);
+    } else {
+      id = 3; x = -1.0 / x;
+    }
+  }
+  const double z = x * x, w = z * z;
+  const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+  const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+  if (id < 0) return x - x * (s1 + s2);
+  const double r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+  return hx < 0 ? -r : r;
+}
+
 }  // namespace smcrt

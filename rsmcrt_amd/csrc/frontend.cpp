@@ -21,6 +21,8 @@
 
 #include "../../include/smcrt.h"
 #include "hosterr.h"
+#include "mat4.h"
+#include "png.h"
 #include "toml.h"
 
 using smcrt::toml::Table;
@@ -31,66 +33,11 @@ namespace {
 
 int ffail(int code, const std::string& m) { return smcrt::set_error(code, m); }
 
-// ---------------------------------------------------------------- 4x4 transforms ---
-// m[r][c] = Fortran t(r+1, c+1); stored column-major in smcrt_sdf_node.transform.
-struct M4 {
-  double m[4][4];
-};
-
-M4 identity() {
-  M4 a{};
-  for (int i = 0; i < 4; ++i) a.m[i][i] = 1.0;
-  return a;
-}
-
-M4 translate(double x, double y, double z) {  // sdfHelpers.f90:160-171: row 4 holds o
-  M4 a = identity();
-  a.m[3][0] = x; a.m[3][1] = y; a.m[3][2] = z;
-  return a;
-}
-
-M4 rotate_y(double angle) {  // sdfHelpers.f90:33-50, deg2rad(a) = a*pi/180
-  const double r = angle * M_PI / 180.0, c = std::cos(r), s = std::sin(r);
-  M4 a{};
-  // columns (c,0,s,0) (0,1,0,0) (-s,0,c,0) (0,0,0,1)
-  a.m[0][0] = c;  a.m[1][0] = 0; a.m[2][0] = s;  a.m[3][0] = 0;
-  a.m[0][1] = 0;  a.m[1][1] = 1; a.m[2][1] = 0;  a.m[3][1] = 0;
-  a.m[0][2] = -s; a.m[1][2] = 0; a.m[2][2] = c;  a.m[3][2] = 0;
-  a.m[0][3] = 0;  a.m[1][3] = 0; a.m[2][3] = 0;  a.m[3][3] = 1;
-  return a;
-}
-
-// Direct 4x4 inverse, term for term as mat_class.f90:154-207.
-M4 invert(const M4& A) {
-  auto a = [&](int i, int j) { return A.m[i - 1][j - 1]; };
-  const double detinv =
-      1.0 / (a(1, 1) * (a(2, 2) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(2, 3) * (a(3, 4) * a(4, 2) - a(3, 2) * a(4, 4)) +
-                        a(2, 4) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2))) -
-             a(1, 2) * (a(2, 1) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(2, 3) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) +
-                        a(2, 4) * (a(3, 1) * a(4, 3) - a(3, 3) * a(4, 1))) +
-             a(1, 3) * (a(2, 1) * (a(3, 2) * a(4, 4) - a(3, 4) * a(4, 2)) + a(2, 2) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) +
-                        a(2, 4) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1))) -
-             a(1, 4) * (a(2, 1) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2)) + a(2, 2) * (a(3, 3) * a(4, 1) - a(3, 1) * a(4, 3)) +
-                        a(2, 3) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1))));
-  M4 B{};
-  B.m[0][0] = detinv * (a(2, 2) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(2, 3) * (a(3, 4) * a(4, 2) - a(3, 2) * a(4, 4)) + a(2, 4) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2)));
-  B.m[1][0] = detinv * (a(2, 1) * (a(3, 4) * a(4, 3) - a(3, 3) * a(4, 4)) + a(2, 3) * (a(3, 1) * a(4, 4) - a(3, 4) * a(4, 1)) + a(2, 4) * (a(3, 3) * a(4, 1) - a(3, 1) * a(4, 3)));
-  B.m[2][0] = detinv * (a(2, 1) * (a(3, 2) * a(4, 4) - a(3, 4) * a(4, 2)) + a(2, 2) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) + a(2, 4) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1)));
-  B.m[3][0] = detinv * (a(2, 1) * (a(3, 3) * a(4, 2) - a(3, 2) * a(4, 3)) + a(2, 2) * (a(3, 1) * a(4, 3) - a(3, 3) * a(4, 1)) + a(2, 3) * (a(3, 2) * a(4, 1) - a(3, 1) * a(4, 2)));
-  B.m[0][1] = detinv * (a(1, 2) * (a(3, 4) * a(4, 3) - a(3, 3) * a(4, 4)) + a(1, 3) * (a(3, 2) * a(4, 4) - a(3, 4) * a(4, 2)) + a(1, 4) * (a(3, 3) * a(4, 2) - a(3, 2) * a(4, 3)));
-  B.m[1][1] = detinv * (a(1, 1) * (a(3, 3) * a(4, 4) - a(3, 4) * a(4, 3)) + a(1, 3) * (a(3, 4) * a(4, 1) - a(3, 1) * a(4, 4)) + a(1, 4) * (a(3, 1) * a(4, 3) - a(3, 3) * a(4, 1)));
-  B.m[2][1] = detinv * (a(1, 1) * (a(3, 4) * a(4, 2) - a(3, 2) * a(4, 4)) + a(1, 2) * (a(3, 1) * a(4, 4) - a(3, 4) * a(4, 1)) + a(1, 4) * (a(3, 2) * a(4, 1) - a(3, 1) * a(4, 2)));
-  B.m[3][1] = detinv * (a(1, 1) * (a(3, 2) * a(4, 3) - a(3, 3) * a(4, 2)) + a(1, 2) * (a(3, 3) * a(4, 1) - a(3, 1) * a(4, 3)) + a(1, 3) * (a(3, 1) * a(4, 2) - a(3, 2) * a(4, 1)));
-  B.m[0][2] = detinv * (a(1, 2) * (a(2, 3) * a(4, 4) - a(2, 4) * a(4, 3)) + a(1, 3) * (a(2, 4) * a(4, 2) - a(2, 2) * a(4, 4)) + a(1, 4) * (a(2, 2) * a(4, 3) - a(2, 3) * a(4, 2)));
-  B.m[1][2] = detinv * (a(1, 1) * (a(2, 4) * a(4, 3) - a(2, 3) * a(4, 4)) + a(1, 3) * (a(2, 1) * a(4, 4) - a(2, 4) * a(4, 1)) + a(1, 4) * (a(2, 3) * a(4, 1) - a(2, 1) * a(4, 3)));
-  B.m[2][2] = detinv * (a(1, 1) * (a(2, 2) * a(4, 4) - a(2, 4) * a(4, 2)) + a(1, 2) * (a(2, 4) * a(4, 1) - a(2, 1) * a(4, 4)) + a(1, 4) * (a(2, 1) * a(4, 2) - a(2, 2) * a(4, 1)));
-  B.m[3][2] = detinv * (a(1, 1) * (a(2, 3) * a(4, 2) - a(2, 2) * a(4, 3)) + a(1, 2) * (a(2, 1) * a(4, 3) - a(2, 3) * a(4, 1)) + a(1, 3) * (a(2, 2) * a(4, 1) - a(2, 1) * a(4, 2)));
-  B.m[0][3] = detinv * (a(1, 2) * (a(2, 4) * a(3, 3) - a(2, 3) * a(3, 4)) + a(1, 3) * (a(2, 2) * a(3, 4) - a(2, 4) * a(3, 2)) + a(1, 4) * (a(2, 3) * a(3, 2) - a(2, 2) * a(3, 3)));
-  B.m[1][3] = detinv * (a(1, 1) * (a(2, 3) * a(3, 4) - a(2, 4) * a(3, 3)) + a(1, 3) * (a(2, 4) * a(3, 1) - a(2, 1) * a(3, 4)) + a(1, 4) * (a(2, 1) * a(3, 3) - a(2, 3) * a(3, 1)));
-  B.m[2][3] = detinv * (a(1, 1) * (a(2, 4) * a(3, 2) - a(2, 2) * a(3, 4)) + a(1, 2) * (a(2, 1) * a(3, 4) - a(2, 4) * a(3, 1)) + a(1, 4) * (a(2, 2) * a(3, 1) - a(2, 1) * a(3, 2)));
-  B.m[3][3] = detinv * (a(1, 1) * (a(2, 2) * a(3, 3) - a(2, 3) * a(3, 2)) + a(1, 2) * (a(2, 3) * a(3, 1) - a(2, 1) * a(3, 3)) + a(1, 3) * (a(2, 1) * a(3, 2) - a(2, 2) * a(3, 1)));
-  return B;
-}
+using smcrt::mat::M4;
+using smcrt::mat::identity;
+using smcrt::mat::invert;
+using smcrt::mat::rotate_y;
+using smcrt::mat::translate;
 
 // ---------------------------------------------------------------- SDF nodes --------
 struct Mono {  // init_mono inputs, opticalProperties.f90:107-125
@@ -202,6 +149,8 @@ struct smcrt_job {
   int64_t iseed = 123456789;
   smcrt_grid grid{};
   smcrt_source src{};
+  smcrt_spectrum spec{};           // src.spectrum points here
+  std::vector<double> spec_data;   // 1-D array(n,2) / 2-D image(width,height)
   std::vector<smcrt_sdf_node> nodes;
   std::vector<int32_t> top;
   std::vector<smcrt_detector> dets;
@@ -274,6 +223,79 @@ void dict_vec3(smcrt_job& J, const Table* g, const std::string& tomlkey, const s
   for (int i = 0; i < 3; ++i) J.set(dictkey + "%" + i4(i + 1), fmt_real(out[i]));
 }
 
+// stdlib loadtxt: whitespace-separated rows of numbers -> d(nrows, ncols), Fortran order.
+// `single` reads into real(sp) first, as parse_spectrum's 1-D branch does (array_sp, :61-63).
+std::vector<double> loadtxt(const std::string& path, bool single, int64_t& rows, int64_t& cols) {
+  std::ifstream f(path);
+  if (!f) throw Fail(SMCRT_ERR_INVALID_ARG, "cannot read spectrum file " + path);
+  std::vector<std::vector<double>> r;
+  std::string line;
+  while (std::getline(f, line)) {
+    for (char& ch : line)
+      if (ch == ',') ch = ' ';  // list-directed read: commas separate values too
+    std::istringstream ls(line);
+    std::vector<double> v;
+    double x;
+    while (ls >> x) v.push_back(single ? (double)(float)x : x);
+    if (v.empty()) continue;
+    if (!r.empty() && v.size() != r[0].size()) throw Fail(SMCRT_ERR_INVALID_ARG, "ragged rows in " + path);
+    r.push_back(std::move(v));
+  }
+  rows = (int64_t)r.size();
+  cols = rows ? (int64_t)r[0].size() : 0;
+  std::vector<double> out((size_t)(rows * cols));
+  for (int64_t i = 0; i < rows; ++i)
+    for (int64_t j = 0; j < cols; ++j) out[(size_t)(i + rows * j)] = r[(size_t)i][(size_t)j];
+  return out;
+}
+
+// parse_spectrum, parse_spectrum.f90:17-118. Files are read relative to the input file's
+// directory (the reference's res/: "res/"//sfile for 1-D, resdir//sfile for 2-D).
+void parse_spectrum(smcrt_job& J, const Table* s) {
+  std::memset(&J.spec, 0, sizeof(J.spec));
+  const std::string stype = T::get_string(s, "spectrum_type", "constant");
+  std::string resdir = J.toml_path;
+  const size_t slash = resdir.find_last_of('/');
+  resdir = slash == std::string::npos ? std::string(".") : resdir.substr(0, slash);
+  if (stype == "constant") {
+    J.spec.kind = SMCRT_SPEC_CONSTANT;
+    J.spec.wavelength = T::get_real(s, "wavelength", 500.0);
+    J.set("wavelength", fmt_real(J.spec.wavelength));
+  } else if (stype == "1D") {
+    const std::string sfile = T::get_string(s, "spectrum_file", "");
+    int64_t rows = 0, cols = 0;
+    J.spec_data = loadtxt(resdir + "/" + sfile, true, rows, cols);
+    if (cols != 2 || rows < 2) throw Fail(SMCRT_ERR_INVALID_ARG, "Array must be size (n, 2)");  // piecewise.f90:152
+    J.spec.kind = SMCRT_SPEC_1D;
+    J.spec.n = rows;
+    J.spec.array = J.spec_data.data();
+  } else if (stype == "2D") {
+    const std::string sfile = T::get_string(s, "spectrum_file", "");
+    const Value* cs = T::find(s, "cell_size");
+    if (!cs || cs->kind != Value::ARRAY || cs->arr.size() != 2)
+      throw Fail(SMCRT_ERR_INVALID_ARG, "Need a vector of size 2 for cell_size");
+    const std::string ft = sfile.size() >= 3 ? sfile.substr(sfile.size() - 3) : sfile;
+    int32_t w = 0, h = 0;
+    if (ft == "png") {
+      const std::string e = smcrt::read_png_first_channel(resdir + "/" + sfile, w, h, J.spec_data);
+      if (!e.empty()) throw Fail(SMCRT_ERR_INVALID_ARG, e);
+    } else if (ft == "dat" || ft == "txt") {
+      int64_t rows = 0, cols = 0;
+      J.spec_data = loadtxt(resdir + "/" + sfile, false, rows, cols);
+      w = (int32_t)rows; h = (int32_t)cols;
+    } else {
+      throw Fail(SMCRT_ERR_INVALID_ARG, "Unknown spectrum file type:" + ft);
+    }
+    J.spec.kind = SMCRT_SPEC_2D;
+    J.spec.width = w; J.spec.height = h;
+    J.spec.image = J.spec_data.data();
+    J.spec.cell_width = cs->arr[0].number();
+    J.spec.cell_height = cs->arr[1].number();
+  } else {
+    throw Fail(SMCRT_ERR_INVALID_ARG, "Not a valid spectrum type! expected one of either ['constant', '1D', '2D']");
+  }
+}
+
 void parse_source(smcrt_job& J, const Table* root) {  // parse_source.f90:17-264
   const Table* s = T::get_table(root, "source");
   if (!s) throw Fail(SMCRT_ERR_INVALID_ARG, "Simulation needs Source table");
@@ -282,8 +304,26 @@ void parse_source(smcrt_job& J, const Table* root) {  // parse_source.f90:17-264
   double pos[3] = {0, 0, 0}, dir[3] = {0, 0, 0};
   const std::string& nm = J.source_name;
   if (nm != "uniform" && !get_vector(s, "position", pos)) throw Fail(SMCRT_ERR_INVALID_ARG, "Expected vector of size 3 for position");
-  if (nm != "point" && nm != "uniform" && nm != "pencil")
-    throw Fail(SMCRT_ERR_UNSUPPORTED, "source '" + nm + "' is not supported by the engine (point, uniform, pencil)");
+  static const char* const names[9] = {"point", "uniform", "pencil", "circular", "focus", "annulus", "slm", "dslit",
+                                       "aperture"};
+  int kind = 0;
+  for (int i = 0; i < 9; ++i)
+    if (nm == names[i]) kind = i + 1;  // smcrt_source_kind order
+  if (!kind) throw Fail(SMCRT_ERR_INVALID_ARG, "No such source! (" + nm + ")");  // init_source, photon.f90:127-156
+  // rotation: every source but uniform, point, circular and pencil (parse_source.f90:67-91)
+  double rot[3] = {0, 0, 0};
+  if (nm != "uniform" && nm != "point" && nm != "circular" && nm != "pencil") {
+    const Value* rv = T::find(s, "rotation");
+    if (!rv) throw Fail(SMCRT_ERR_INVALID_ARG, "Source requires rotation variable");
+    if (rv->kind != Value::ARRAY || rv->arr.size() != 3) throw Fail(SMCRT_ERR_INVALID_ARG, "Need a matrix row for points");
+    for (int i = 0; i < 3; ++i) {
+      rot[i] = rv->arr[i].number();
+      J.set(std::string("rotation%") + "xyz"[i], fmt_real(rot[i]));
+    }
+    // a zero rotation makes the reference warn and return with the source half set up
+    if (std::sqrt(rot[0] * rot[0] + rot[1] * rot[1] + rot[2] * rot[2]) < 1e-8)
+      throw Fail(SMCRT_ERR_INVALID_ARG, "Need to specify rotation that has length greater than 0.0");
+  }
   // direction: a vector, or a cardinal name. A vector makes the reference return early
   // (parse_source.f90:145-159) before point1..3 and the photon emitter are set; the engine
   // applies it and reads the rest (documented deviation).
@@ -299,7 +339,7 @@ void parse_source(smcrt_job& J, const Table* root) {  // parse_source.f90:17-264
     for (int i = 0; i < 3; ++i) dir[i] = c[k][i];
   } else if (dv) {
     get_vector(s, "direction", dir);
-  } else if (nm != "point") {
+  } else if (nm != "point" && nm != "annulus" && nm != "focus") {
     throw Fail(SMCRT_ERR_INVALID_ARG, "Need to specify direction for source type!");
   }
   // corners default (-1,-1,1) (2,0,0) (0,2,0) (:58-61); uniform requires all three
@@ -319,28 +359,49 @@ void parse_source(smcrt_job& J, const Table* root) {  // parse_source.f90:17-264
       throw Fail(SMCRT_ERR_INVALID_ARG, std::string("Uniform source requires ") + pk[p] + " variable");
     }
   }
-  J.set("radius", fmt_real(T::get_real(s, "radius", 0.5)));
-  J.set("focalLength", fmt_real(T::get_real(s, "focalLength", 1.0)));
-  J.set("rhi", fmt_real(T::get_real(s, "rhi", 0.6)));
-  J.set("rlo", fmt_real(T::get_real(s, "rlo", 0.5)));
-  J.set("sigma", fmt_real(T::get_real(s, "sigma", 0.04)));
-  J.set("annulus_type", fmt_str(T::get_string(s, "annulus_type", "gaussian")));
-  J.set("focus_type", fmt_str(T::get_string(s, "focus_type", "gaussian")));
-  J.set("beam_size", fmt_real(T::get_real(s, "beam_size", 0.5)));
-  const std::string spec = T::get_string(s, "spectrum_type", "constant");  // parse_spectrum.f90
-  if (spec != "constant")
-    throw Fail(SMCRT_ERR_UNSUPPORTED, "spectrum_type '" + spec + "' is not supported by the engine (constant)");
-  J.set("wavelength", fmt_real(T::get_real(s, "wavelength", 500.0)));
+  const double radius = T::get_real(s, "radius", 0.5), focal = T::get_real(s, "focalLength", 1.0);
+  const double rhi = T::get_real(s, "rhi", 0.6), rlo = T::get_real(s, "rlo", 0.5), sigma = T::get_real(s, "sigma", 0.04);
+  const std::string annulus_type = T::get_string(s, "annulus_type", "gaussian");
+  const std::string focus_type = T::get_string(s, "focus_type", "gaussian");
+  const double beam_size = T::get_real(s, "beam_size", 0.5);
+  J.set("radius", fmt_real(radius));
+  J.set("focalLength", fmt_real(focal));
+  J.set("rhi", fmt_real(rhi));
+  J.set("rlo", fmt_real(rlo));
+  J.set("sigma", fmt_real(sigma));
+  J.set("annulus_type", fmt_str(annulus_type));
+  J.set("focus_type", fmt_str(focus_type));
+  J.set("beam_size", fmt_real(beam_size));
+  parse_spectrum(J, s);
 
   std::memset(&J.src, 0, sizeof(J.src));
-  J.src.kind = nm == "point" ? SMCRT_SRC_POINT : (nm == "uniform" ? SMCRT_SRC_UNIFORM : SMCRT_SRC_PENCIL);
+  J.src.kind = kind;
   for (int i = 0; i < 3; ++i) {
     J.src.pos[i] = pos[i];
     J.src.dir[i] = dir[i];
     J.src.p1[i] = c[0][i];
     J.src.p2[i] = c[1][i];
     J.src.p3[i] = c[2][i];
+    J.src.rotation[i] = rot[i];
   }
+  J.src.radius = radius; J.src.focal_length = focal; J.src.beam_size = beam_size;
+  J.src.rlo = rlo; J.src.rhi = rhi; J.src.sigma = sigma;
+  // focus_type / annulus_type: an unknown name is an `error stop` at the first emission in
+  // the reference (photon.f90:426, :891); it is refused at load here
+  if (kind == SMCRT_SRC_FOCUS) {
+    if (focus_type == "square") J.src.beam = SMCRT_BEAM_SQUARE;
+    else if (focus_type == "circle") J.src.beam = SMCRT_BEAM_CIRCLE;
+    else if (focus_type == "gaussian") J.src.beam = SMCRT_BEAM_GAUSSIAN;
+    else throw Fail(SMCRT_ERR_INVALID_ARG, "No such beam type! (focus_type = " + focus_type + ")");
+  } else if (kind == SMCRT_SRC_ANNULUS) {
+    if (annulus_type == "tophat") J.src.beam = SMCRT_BEAM_TOPHAT;
+    else if (annulus_type == "besselAnnulus") J.src.beam = SMCRT_BEAM_BESSEL;
+    else if (annulus_type == "gaussian") J.src.beam = SMCRT_BEAM_GAUSSIAN;
+    else throw Fail(SMCRT_ERR_INVALID_ARG, "No such beam type! (annulus_type = " + annulus_type + ")");
+  }
+  J.src.spectrum = &J.spec;
+  if (kind == SMCRT_SRC_SLM && J.spec.kind == SMCRT_SPEC_1D)
+    throw Fail(SMCRT_ERR_INVALID_ARG, "slm source needs a 2D (image) spectrum");
 }
 
 void parse_grid(smcrt_job& J, const Table* root) {  // parse.f90:75-112
@@ -508,8 +569,26 @@ void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:
       d.bin_wid = nb == 0 ? 1.0 : (r2 - r1) / (double)nb;
       for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
       by_kind[1].push_back({d, id});
-    } else if (type == "fibre") {
-      throw Fail(SMCRT_ERR_UNSUPPORTED, "fibre detectors are not supported by the engine");
+    } else if (type == "fibre") {  // handle_fibre_collection_dect :233-294, init_fibre_dect detectors.f90:246-329
+      const double l = len3(dir);
+      for (int i = 0; i < 3; ++i) dir[i] = dir[i] / l;
+      const double f1 = T::get_real(c, "focalLength1", 1.0), f2 = T::get_real(c, "focalLength2", 1.0);
+      const double a1 = T::get_real(c, "f1Aperture", 1.0), a2 = T::get_real(c, "f2Aperture", 1.0);
+      double* F = d.fibre;
+      F[0] = f1; F[1] = f2; F[2] = a1; F[3] = a2;
+      F[4] = T::get_real(c, "frontOffset", 0.0);
+      F[5] = T::get_real(c, "backOffset", f2);
+      F[6] = T::get_real(c, "frontToPinSep", f1);
+      F[7] = T::get_real(c, "pinToBackSep", f2);
+      F[8] = T::get_real(c, "pinAperture", a1 > a2 ? a1 : a2);
+      F[9] = T::get_real(c, "acceptanceAngle", 90.0);  // (sic: validateFibreDect.toml's acceptAngle is not read)
+      F[10] = T::get_real(c, "coreDiameter", 0.01);
+      const int64_t nb = T::get_int(c, "nbins", 1);
+      d.kind = SMCRT_DET_FIBRE;
+      d.nbins = (int32_t)nb + 1;
+      d.bin_wid = nb == 0 ? 1.0 : F[10] / 2.0 / (double)nb;
+      for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
+      by_kind[2].push_back({d, id});
     } else if (type == "camera") {  // :118-147, init_camera detectors.f90:401-445
       double p1[3] = {-1.0, -1.0, -1.0}, p2[3] = {2.0, 0.0, 0.0}, p3[3] = {0.0, 2.0, 0.0};
       get_vector(c, "p1", p1); get_vector(c, "p2", p2); get_vector(c, "p3", p3);

@@ -58,7 +58,7 @@ __device__ unsigned long long g_diag[72];
 __device__ unsigned long long g_diag_t[9];
 #endif
 
-template <bool LDS_FACES, int GM>
+template <bool LDS_FACES, int GM, bool XSRC>
 #ifndef SMCRT_WAVES_PER_EU
 #define SMCRT_WAVES_PER_EU 3
 #endif
@@ -498,13 +498,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           L.fault = false; L.layer = 0;
           LU(LU_STATUS) = 0; LU(LU_NSCATT) = 0; LU(LU_INTER) = 0; LU(LU_BOUNCES) = 0;
           L.xcell = L.ycell = L.zcell = 0;
-          emit<GM>(K, C, L);
+          emit<GM, XSRC>(K, C, L);
           if (!test_kernel) {
             int64_t tries = 0;
             while (cell_out(K, L)) {
               if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
               LCTR(LC_RETRIES)++;
-              emit<GM>(K, C, L);
+              emit<GM, XSRC>(K, C, L);
             }
             if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, C->emission, L, 1.0);
           }
@@ -640,6 +640,11 @@ struct smcrt_scene {
   size_t records_cap = 0;
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
+  int grid_blocks_x = 0;  // the XSRC (general emitter) instantiation
+  // source spectrum tables of the last general-emitter run (srcplan.h), device copy
+  std::vector<double> h_spec;
+  double* d_spec = nullptr;
+  size_t spec_cap = 0;
   bool lds_faces = false;
   size_t face_bytes = 0;
   uint32_t hist_tiles = 0;  // fused tile histogram in the transport kernel (0: bin_hist kernel)
@@ -698,13 +703,12 @@ static hipError_t harvest_times(smcrt_scene* s) {
 }
 
 // The transport kernel instantiation for this scene (LDS faces? power-of-two grid?).
-static const void* transport_fn(const smcrt_scene* s) {
-  static const void* const fns[2][3] = {
-      {(const void*)transport_kernel<false, 0>, (const void*)transport_kernel<false, 1>,
-       (const void*)transport_kernel<false, 2>},
-      {(const void*)transport_kernel<true, 0>, (const void*)transport_kernel<true, 1>,
-       (const void*)transport_kernel<true, 2>}};
-  return fns[s->lds_faces ? 1 : 0][s->grid_mode];
+static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
+#define TK(F, G) {(const void*)transport_kernel<F, G, false>, (const void*)transport_kernel<F, G, true>}
+  static const void* const fns[2][3][2] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
+                                           {TK(true, 0), TK(true, 1), TK(true, 2)}};
+#undef TK
+  return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : 0];
 }
 
 // Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
@@ -742,7 +746,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
-  void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off,
+  void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_dep_ctl, s->d_tile_count,
                   s->d_tile_start, s->d_bin_counts, s->d_pieces};
@@ -785,8 +789,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   for (int32_t i = 0; i < n_top; ++i)
     if (top[i] < 0 || top[i] >= n_nodes) return fail(SMCRT_ERR_INVALID_ARG, "top index out of range");
   for (int32_t i = 0; i < n_dets; ++i) {
-    if (dets[i].kind == SMCRT_DET_FIBRE) return fail(SMCRT_ERR_UNSUPPORTED, "fibre detector not supported");
-    if (dets[i].kind < SMCRT_DET_CIRCLE || dets[i].kind > SMCRT_DET_CAMERA || dets[i].nbins < 1)
+    if (dets[i].kind < SMCRT_DET_CIRCLE || dets[i].kind > SMCRT_DET_FIBRE || dets[i].nbins < 1)
       return fail(SMCRT_ERR_INVALID_ARG, "bad detector " + std::to_string(i));
   }
   int ndev = 0;
@@ -909,11 +912,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     }
     s->grid_mode = f2 ? 2 : (p2 ? 1 : 0);
   }
-  const void* kfn = transport_fn(s);
-  hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, s->hist_tiles));
-  if (oe != hipSuccess || per_cu < 1) per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
-  s->grid_blocks = cus * per_cu;
+  for (int x = 0; x < 2; ++x) {
+    const void* kfn = transport_fn(s, x == 1);
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, s->hist_tiles));
+    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
+    (x ? s->grid_blocks_x : s->grid_blocks) = cus * per_cu;
+  }
   *out = s;
   return SMCRT_OK;
 }
@@ -983,7 +988,7 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   return true;
 }
 
-static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t stream) {
+static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hipStream_t stream) {
   HIPCHK(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), stream));
   // this launch's cold parameters: a ring slot, written in stream order before the kernel
   KCold* C = s->d_cold + (s->cold_seq++ % COLD_SLOTS);
@@ -1008,7 +1013,8 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
   }
   const uint64_t waves_needed = (Ch.n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
-  const int blocks = (int)std::min<uint64_t>((uint64_t)s->grid_blocks, std::max<uint64_t>(1, blocks_needed));
+  const int blocks = (int)std::min<uint64_t>((uint64_t)(xsrc ? s->grid_blocks_x : s->grid_blocks),
+                                             std::max<uint64_t>(1, blocks_needed));
   {
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;
@@ -1016,7 +1022,7 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
     const smcrt_detector* a_dets = K.dets;
     const int64_t* a_off = K.det_off;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&a_dets, (void*)&a_off, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(transport_fn(s), dim3(blocks), dim3(256), args, transport_lds(s, K.hist_tiles), stream));
+    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, K.hist_tiles), stream));
   }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
@@ -1073,8 +1079,41 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, hipStream_t st
 
 static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg,
                   const smcrt_device_tallies& dt, hipStream_t stream) {
-  if (src->kind < SMCRT_SRC_POINT || src->kind > SMCRT_SRC_PENCIL) return fail(SMCRT_ERR_INVALID_ARG, "bad source kind");
+  if (src->kind < SMCRT_SRC_POINT || src->kind > SMCRT_SRC_APERTURE) return fail(SMCRT_ERR_INVALID_ARG, "bad source kind");
   if (cfg->n_photons == 0) return SMCRT_OK;
+  // sources other than point/uniform/pencil, or a sampled spectrum: the general emitter
+  const bool xsrc = src_needs_plan(src);
+  SrcPlan plan;
+  std::memset(&plan, 0, sizeof plan);
+  if (xsrc) {
+    std::vector<double> px, py, pc;
+    const char* perr = "";
+    const int pst = build_src_plan(src, &s->grid, &plan, px, py, pc, &perr);
+    if (pst) return fail(pst, perr);
+    std::vector<double> tab;
+    tab.reserve(px.size() + py.size() + pc.size());
+    tab.insert(tab.end(), px.begin(), px.end());
+    tab.insert(tab.end(), py.begin(), py.end());
+    tab.insert(tab.end(), pc.begin(), pc.end());
+    if (!tab.empty()) {
+      if (tab != s->h_spec) {  // new tables: wait for launches that may still read the old ones
+        HIPCHK(hipStreamSynchronize(stream));
+        if (s->stream != stream) HIPCHK(hipStreamSynchronize(s->stream));
+        if (tab.size() > s->spec_cap) {
+          if (s->d_spec) HIPCHK(hipFree(s->d_spec));
+          s->d_spec = nullptr;
+          s->spec_cap = 0;
+          HIPCHK(hipMalloc((void**)&s->d_spec, tab.size() * sizeof(double)));
+          s->spec_cap = tab.size();
+        }
+        HIPCHK(hipMemcpy(s->d_spec, tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice));
+        s->h_spec = tab;
+      }
+      plan.spec_x = px.empty() ? nullptr : s->d_spec;
+      plan.spec_y = py.empty() ? nullptr : s->d_spec + px.size();
+      plan.cdf = s->d_spec + px.size() + py.size();
+    }
+  }
   KParams K;
   K.nodes = s->d_nodes;
   K.prog = s->d_prog;
@@ -1094,6 +1133,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.flags = cfg->flags;
   KCold Ch;
   Ch.src = *src;
+  Ch.plan = plan;
   K.key0 = (uint32_t)cfg->seed;
   K.key1 = (uint32_t)(cfg->seed >> 32);
   Ch.jmean = dt.jmean; Ch.absorb = dt.absorb; Ch.emission = dt.emission;
@@ -1132,7 +1172,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
     Ch.first_photon = cfg->first_photon + done;
     Ch.records = dt.records ? dt.records + done : nullptr;
     if (K.rec_pool) s->h_ctl[4] = 0;
-    int st = launch_one(s, K, Ch, stream);
+    int st = launch_one(s, K, Ch, xsrc, stream);
     if (st) return st;
     if (K.rec_pool) s->h_ctl[4] = (uint32_t)std::min<uint64_t>(n, 0xFFFFFFFFull);
     if (calibrate && K.rec_pool) {

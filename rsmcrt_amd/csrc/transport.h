@@ -23,6 +23,7 @@
 #include "../../include/smcrt.h"
 #include "detmath.h"
 #include "geometry.h"
+#include "srcplan.h"
 
 namespace smcrt {
 
@@ -71,6 +72,7 @@ struct KCold {
   uint32_t* chunk_fill;       // records in each used chunk (deposit.h)
   uint32_t* dep_ctl;          // [0] next chunk, [1] overflowed deposits
   uint32_t* bin_counts;       // fused tile histogram, counts[tile][chunk % BIN_BLOCKS]
+  SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
 
 struct KParams {
@@ -220,6 +222,39 @@ __device__ __forceinline__ uint32_t record_hits(const KParams& K, double* det_bi
           w = 1.0;
         }
       }
+    } else if (D->kind == SMCRT_DET_FIBRE) {  // check_hit_fibre, detectors.f90:331-393 (4f thin-lens chain)
+      const double* F = D->fibre;  // focalLength1, focalLength2, f1Aperture, f2Aperture, frontOffset,
+                                   // backOffset, frontToPinSep, pinToBackSep, pinAperture, acceptAngle, core
+      bool hit = intersect_circle(ddir, dpos + mul(ddir, F[4]), F[2], start, dir, t, value1D);
+      if (hit && (t <= 0.0 || t > pointSep)) hit = false;
+      if (hit) {
+        double costt = dot(ddir, dir);
+        if (costt > 1.0) costt = 1.0;
+        const double sintt = sqrt(1.0 - costt * costt);
+        double gradient = sintt / costt;
+        double radius = value1D;
+        gradient = -radius / F[0] + gradient;    // front lens
+        radius = radius + gradient * F[6];       // to the pinhole
+        if (radius > F[8]) {
+          hit = false;
+        } else {
+          radius = radius + gradient * F[7];     // to the back lens
+          if (radius > F[3]) {
+            hit = false;
+          } else {
+            gradient = -radius / F[1] + gradient;
+            radius = radius + gradient * F[5];   // to the fibre
+            const double angle = fabs(det_atan(gradient)) * 360.0 / 6.283185307179586;
+            if (angle > F[9] || radius > (F[10] / 2.0)) hit = false;
+            value1D = fabs(radius);
+          }
+        }
+      }
+      if (hit) {
+        int64_t idx = f_nint(value1D / D->bin_wid) + 1;
+        if (idx > D->nbins) idx = D->nbins;
+        if (idx >= 1) bin = idx - 1;
+      }
     }
     if (bin >= 0) {
       if (data) atomic_add_nr(data + bin, w);
@@ -338,11 +373,250 @@ __device__ __forceinline__ void add_cell(const KParams& K, double* g, Lane& L, d
   if (g) atomic_add_nr(g + lin(K, L.xcell, L.ycell, L.zcell), w);
 }
 
+// ------------------------------------------------------------------ general emitter ----
+// Kernels instantiated with XSRC run every source of photon.f90 and sample the source
+// spectrum (piecewise.f90); the others keep the three-source emitter below it. The launch-
+// invariant parts (matrices, CDFs) come from the host (srcplan.h).
+
+// search_1D, piecewise.f90:254-275: bisection with middle = int((nup+nlow)/2.) in default
+// (single) precision; returns the 1-based nlow.
+__device__ __forceinline__ int64_t search_1d(const double* __restrict__ a, int64_t n, double v) {
+  int64_t nup = n, nlow = 1;
+  while ((nup - nlow) > 1) {
+    const int64_t middle = (int64_t)((float)(nup + nlow) / 2.0f);
+    if (v > a[middle - 1]) nlow = middle;
+    else nup = middle;
+  }
+  return nlow;
+}
+__device__ __forceinline__ uint32_t pack_bits(uint64_t x) {  // piecewise.f90:296-315
+  x &= 0x5555555555555555ull;
+  x = (x >> 1) | x; x &= 0x3333333333333333ull;
+  x = (x >> 2) | x; x &= 0x0F0F0F0F0F0F0F0Full;
+  x = (x >> 4) | x; x &= 0x00FF00FF00FF00FFull;
+  x = (x >> 8) | x; x &= 0x0000FFFF0000FFFFull;
+  x = (x >> 16) | x;
+  return (uint32_t)x;
+}
+// ranu(a, b) = a + ran2()*(b - a), random_mod.f90:93-103
+__device__ __forceinline__ double ranu(const KParams& K, Lane& L, double a, double b) {
+  return a + L.rng.next(K.key0, K.key1) * (b - a);
+}
+// spectrum%p%sample(x, y): constant getValue :93-107, sample1D :109-137, sample2D :171-188
+__device__ __forceinline__ void spec_sample(const KParams& K, const SrcPlan& P, Lane& L, double& x, double& y) {
+  if (P.spec_kind == SMCRT_SPEC_1D) {
+    const double val = L.rng.next(K.key0, K.key1);
+    const int64_t i = search_1d(P.cdf, P.spec_n, val);  // 1-based
+    const double* a = P.spec_x;
+    x = a[i - 1] + ((val - P.cdf[i - 1]) * (a[i] - a[i - 1])) / (P.cdf[i] - P.cdf[i - 1]);
+    y = 0.0;  // (undefined in the reference; never used)
+  } else if (P.spec_kind == SMCRT_SPEC_2D) {
+    const double val = L.rng.next(K.key0, K.key1);
+    const int64_t i = search_1d(P.cdf, P.spec_n, val);
+    const int32_t xr = (int32_t)pack_bits((uint64_t)i), yr = (int32_t)pack_bits((uint64_t)i >> 1);
+    x = (double)(xr - P.xoff) + ranu(K, L, -P.cell_w, P.cell_w);
+    y = (double)(yr - P.yoff) + ranu(K, L, -P.cell_h, P.cell_h);
+  } else {
+    x = P.wavelength;
+    y = -9999.0;
+  }
+}
+__device__ __forceinline__ void nudge_faces(const KParams& K, V3& p) {  // e.g. photon.f90:614-628
+  if (p.x == -K.xmax) p.x = p.x + 7.9e-7;
+  else if (p.x == K.xmax) p.x = p.x - 7.9e-7;
+  if (p.y == -K.ymax) p.y = p.y + 7.9e-7;
+  else if (p.y == K.ymax) p.y = p.y - 7.9e-7;
+  if (p.z == -K.zmax) p.z = p.z + 7.9e-7;
+  else if (p.z == K.zmax) p.z = p.z - 7.9e-7;
+}
+__device__ __forceinline__ V3 magnitude(V3 a) {  // vector_class.f90:392-402
+  const double t = len(a);
+  return v3(a.x / t, a.y / t, a.z / t);
+}
+// focus/annulus: dir = magnitude(sign(1,f) * (-(p - targ)/|p - targ|)) with targ = (0,0,-f),
+// then rotated and renormalised (photon.f90:430-472 / :902-944)
+__device__ __forceinline__ V3 beam_dir(const SrcPlan& P, V3 q) {
+  const V3 d0 = q - v3(0.0, 0.0, -P.focal);
+  const double dist = len(d0);
+  V3 d = smul(-1.0, d0);
+  d = v3(d.x / dist, d.y / dist, d.z / dist);
+  d = mul(d, copysign(1.0, P.focal));
+  d = magnitude(d);
+  return magnitude(dotmat(d, P.R));
+}
+// the step back into the grid of focus (cap 4) and annulus (cap 3), photon.f90:505-556
+__device__ __forceinline__ void step_into_grid(const KParams& K, Lane& L, int cap) {
+  bool inX = false, inY = false, inZ = false, tX = false, tY = false, tZ = false;
+  int counter = 0;
+  V3& p = L.pos;
+  const V3 d = L.dir;
+  while (!inX || !inY || !inZ) {
+    double st;
+    if (p.x <= -K.xmax) { st = (-K.xmax - p.x + 9e-7) / d.x; p = v3(p.x + d.x * st, p.y + d.y * st, p.z + d.z * st); tX = true; }
+    else if (p.x >= K.xmax) { st = (K.xmax - p.x - 9e-7) / d.x; p = v3(p.x + d.x * st, p.y + d.y * st, p.z + d.z * st); tX = true; }
+    else inX = true;
+    if (p.y <= -K.ymax) { st = (-K.ymax - p.y + 9e-7) / d.y; p = v3(p.x + d.x * st, p.y + d.y * st, p.z + d.z * st); tY = true; }
+    else if (p.y >= K.ymax) { st = (K.ymax - p.y - 9e-7) / d.y; p = v3(p.x + d.x * st, p.y + d.y * st, p.z + d.z * st); tY = true; }
+    else inY = true;
+    if (p.z <= -K.zmax) { st = (-K.zmax - p.z + 9e-7) / d.z; p = v3(p.x + d.x * st, p.y + d.y * st, p.z + d.z * st); tZ = true; }
+    else if (p.z >= K.zmax) { st = (K.zmax - p.z - 9e-7) / d.z; p = v3(p.x + d.x * st, p.y + d.y * st, p.z + d.z * st); tZ = true; }
+    else inZ = true;
+    if ((tX && tY && tZ) || counter > cap) break;
+    counter = counter + 1;
+  }
+}
+
+constexpr int MAX_RANG_TRIES = 1000;  // rang's rejection loop (random_mod.f90:116-121), capped
+
+// pos/dir of one emission for every source kind (the cells are set by the caller)
+__device__ __forceinline__ void emit_ext(const KParams& K, const SrcPlan& P, Lane& L) {
+  const double TWOPI = 6.283185307179586;
+  double wl, tmp;
+  switch (P.kind) {
+    case SMCRT_SRC_POINT: {  // photon.f90:311-359
+      L.pos = v3(P.origin[0], P.origin[1], P.origin[2]);
+      const double phi = L.rng.next(K.key0, K.key1) * TWOPI;
+      double sinp, cosp;
+      det_sincos(phi, &sinp, &cosp);
+      const double cost = 2.0 * L.rng.next(K.key0, K.key1) - 1.0;
+      const double sint = sqrt(1.0 - cost * cost);
+      L.dir = v3(sint * cosp, sint * sinp, cost);
+      L.layer = 1;
+      spec_sample(K, P, L, wl, tmp);
+      break;
+    }
+    case SMCRT_SRC_UNIFORM: {  // :566-649
+      const double rx = L.rng.next(K.key0, K.key1), ry = L.rng.next(K.key0, K.key1);
+      L.dir = v3(P.dir[0], P.dir[1], P.dir[2]);
+      L.pos = v3(P.p1[0] + rx * P.p2[0] + ry * P.p3[0], P.p1[1] + rx * P.p2[1] + ry * P.p3[1],
+                 P.p1[2] + rx * P.p2[2] + ry * P.p3[2]);
+      nudge_faces(K, L.pos);
+      spec_sample(K, P, L, wl, tmp);
+      break;
+    }
+    case SMCRT_SRC_PENCIL: {  // :652-710
+      L.pos = v3(P.origin[0], P.origin[1], P.origin[2]);
+      nudge_faces(K, L.pos);
+      L.dir = v3(P.dir[0], P.dir[1], P.dir[2]);
+      L.layer = 1;
+      spec_sample(K, P, L, wl, tmp);
+      break;
+    }
+    case SMCRT_SRC_CIRCULAR: {  // :214-308
+      L.dir = v3(P.dir[0], P.dir[1], P.dir[2]);
+      const double r = P.radius * sqrt(L.rng.next(K.key0, K.key1));
+      const double theta = L.rng.next(K.key0, K.key1) * TWOPI;
+      double st, ct;
+      det_sincos(theta, &st, &ct);
+      const V3 q = P.circ_z ? v3(r * ct, r * st, 0.0) : v3(0.0, r * ct, r * st);
+      const V3 t = dotmat(q, P.T);
+      L.pos = v3(-t.x, -t.y, -t.z);
+      nudge_faces(K, L.pos);
+      spec_sample(K, P, L, wl, tmp);
+      L.layer = 1;
+      break;
+    }
+    case SMCRT_SRC_FOCUS:      // :361-563
+    case SMCRT_SRC_ANNULUS: {  // :850-1043
+      V3 q, qd;
+      if (P.kind == SMCRT_SRC_FOCUS) {
+        if (P.beam == SMCRT_BEAM_SQUARE) {
+          const double x = ranu(K, L, -P.beam_size, P.beam_size);
+          const double y = ranu(K, L, -P.beam_size, P.beam_size);
+          q = v3(x, y, 0.0);
+        } else {
+          double radius;
+          if (P.beam == SMCRT_BEAM_CIRCLE) radius = P.beam_size * sqrt(L.rng.next(K.key0, K.key1));
+          else radius = P.beam_size * sqrt(-det_log(1.0 - L.rng.next(K.key0, K.key1)));
+          const double phi = TWOPI * L.rng.next(K.key0, K.key1);
+          double sinp, cosp;
+          det_sincos(phi, &sinp, &cosp);
+          q = v3(radius * cosp, radius * sinp, 0.0);
+        }
+        qd = q;
+      } else {
+        double radius, mid;
+        if (P.beam == SMCRT_BEAM_TOPHAT) {
+          radius = sqrt(P.rlo * P.rlo + (P.rhi * P.rhi - P.rlo * P.rlo) * L.rng.next(K.key0, K.key1));
+          mid = (P.rhi + P.rlo) / 2.0;
+        } else if (P.beam == SMCRT_BEAM_BESSEL) {
+          radius = P.rlo + (P.rhi - P.rlo) * L.rng.next(K.key0, K.key1);
+          mid = (P.rhi + P.rlo) / 2.0;
+        } else {  // gaussian: rang(radius, tmp, mid, sigma), random_mod.f90:105-127
+          mid = (P.rhi + P.rlo) / 2.0;
+          double x = 0.0, y = 0.0, s = 1.0;
+          int tries = 0;
+          while (s >= 1.0) {
+            if (++tries > MAX_RANG_TRIES) { L.fault = true; break; }
+            x = ranu(K, L, -1.0, 1.0);
+            y = ranu(K, L, -1.0, 1.0);
+            s = y * y + x * x;
+          }
+          radius = mid + P.sigma * (x * sqrt(-2.0 * det_log(s) / s));
+        }
+        const double phi = TWOPI * L.rng.next(K.key0, K.key1);
+        double sinp, cosp;
+        det_sincos(phi, &sinp, &cosp);
+        q = v3(radius * cosp, radius * sinp, 0.0);
+        qd = v3(mid * cosp, mid * sinp, 0.0);
+      }
+      L.dir = beam_dir(P, qd);
+      L.pos = dotmat(q, P.T);
+      spec_sample(K, P, L, wl, tmp);
+      step_into_grid(K, L, P.kind == SMCRT_SRC_FOCUS ? 4 : 3);
+      break;
+    }
+    case SMCRT_SRC_SLM: {  // :159-212
+      double x, y;
+      spec_sample(K, P, L, x, y);
+      L.pos = v3((x - 100.0) / ((double)P.nx / (2.0 * P.xmax)), (y - 100.0) / ((double)P.ny / (2.0 * P.ymax)),
+                 P.origin[2]);
+      L.dir = v3(P.dir[0], P.dir[1], P.dir[2]);
+      L.layer = 1;
+      break;
+    }
+    default: {  // dslit :712-780, aperture :782-848
+      spec_sample(K, P, L, wl, tmp);
+      double x1, y1, z1, x2, y2, z2;
+      if (P.kind == SMCRT_SRC_DSLIT) {
+        const double a = 60.0 * wl, b = 20.0 * wl;
+        if (L.rng.next(K.key0, K.key1) > 0.5) {
+          x1 = ranu(K, L, a / 2.0, a / 2.0 + b);
+          y1 = ranu(K, L, -b * 0.5, b * 0.5);
+        } else {
+          x1 = ranu(K, L, -a / 2.0, -a / 2.0 - b);
+          y1 = ranu(K, L, -b * 0.5, b * 0.5);
+        }
+        z2 = 5.0 - (1.e-5 * (2.0 * (5.0 / 400.0)));
+        x2 = ranu(K, L, -5.0, 5.0);
+        y2 = ranu(K, L, -5.0, 5.0);
+        z1 = (10000.0 * wl) - 5.0;
+      } else {
+        const double apwid = 200e-6, b = apwid / 2.0, F = 4.95;
+        x1 = ranu(K, L, -b, b);
+        y1 = ranu(K, L, -b, b);
+        const double fa = F / apwid;
+        z1 = (1.0 / (((fa * fa) / 2.0) * wl)) - 0.5;
+        x2 = ranu(K, L, -0.5, 0.5);
+        y2 = ranu(K, L, -0.5, 0.5);
+        z2 = 0.5 - (1.e-5 * (2.0 * 0.5 / 400.0));
+      }
+      L.pos = v3(x2, y2, z2);
+      const double dx = x2 - x1, dy = y2 - y1, dz = z2 - z1;
+      const double phase = sqrt(dx * dx + dy * dy + dz * dz);
+      L.dir = v3(dx / phase, dy / phase, -fabs(dz) / phase);
+      break;
+    }
+  }
+}
+
 // emit: point photon.f90:311-359 / uniform :566-649 / pencil :652-710
-template <int GM>
+template <int GM, bool XSRC>
 __device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__ C, Lane& L) {
   const smcrt_source& s = C->src;
-  if (s.kind == SMCRT_SRC_POINT) {
+  if constexpr (XSRC) {
+    emit_ext(K, C->plan, L);
+  } else if (s.kind == SMCRT_SRC_POINT) {
     L.pos = v3(s.pos[0], s.pos[1], s.pos[2]);
     const double phi = L.rng.next(K.key0, K.key1) * 6.283185307179586;
     double sinp, cosp;

@@ -23,6 +23,8 @@ import math
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
+import numpy as np
+
 from . import abi
 
 Vec = Sequence[float]
@@ -299,6 +301,98 @@ def uniform_source(p1, p2, p3, direction) -> abi.Source:
     return s
 
 
+def _src(kind, pos=(0.0, 0.0, 0.0), direction=(0.0, 0.0, 0.0)) -> abi.Source:
+    s = abi.Source()
+    s.kind = kind
+    for i in range(3):
+        s.pos[i] = float(pos[i]); s.dir[i] = float(direction[i])
+    return s
+
+
+def circular_source(pos, direction, radius) -> abi.Source:
+    """circular (photon.f90:214-308): a uniform disc of `radius` centred on pos, facing direction."""
+    s = _src(abi.SRC_CIRCULAR, pos, direction)
+    s.radius = float(radius)
+    return s
+
+
+def focus_source(pos, rotation, focal_length=1.0, focus_type="gaussian", beam_size=0.5) -> abi.Source:
+    """focus (photon.f90:361-563): a beam focused at focal_length, rotated onto `rotation`."""
+    s = _src(abi.SRC_FOCUS, pos)
+    s.beam = abi.BEAM_KINDS[focus_type]
+    s.focal_length, s.beam_size = float(focal_length), float(beam_size)
+    for i in range(3):
+        s.rotation[i] = float(rotation[i])
+    return s
+
+
+def annulus_source(pos, rotation, focal_length=1.0, annulus_type="gaussian", rlo=0.5, rhi=0.6,
+                   sigma=0.04) -> abi.Source:
+    """annulus (photon.f90:850-1043): an annular beam (tophat, besselAnnulus or gaussian)."""
+    s = _src(abi.SRC_ANNULUS, pos)
+    s.beam = abi.BEAM_KINDS[annulus_type]
+    s.focal_length, s.rlo, s.rhi, s.sigma = float(focal_length), float(rlo), float(rhi), float(sigma)
+    for i in range(3):
+        s.rotation[i] = float(rotation[i])
+    return s
+
+
+def slm_source(pos, direction, spectrum=None) -> abi.Source:
+    """slm (photon.f90:159-212): (x, y) sampled from a 2-D spectrum (an image)."""
+    s = _src(abi.SRC_SLM, pos, direction)
+    if spectrum is not None:
+        attach_spectrum(s, spectrum)
+    return s
+
+
+def dslit_source() -> abi.Source:
+    """dslit (photon.f90:712-780): double-slit diffraction source."""
+    return _src(abi.SRC_DSLIT)
+
+
+def aperture_source() -> abi.Source:
+    """aperture (photon.f90:782-848): square-aperture diffraction source."""
+    return _src(abi.SRC_APERTURE)
+
+
+def spectrum_constant(wavelength=500.0) -> abi.Spectrum:
+    sp = abi.Spectrum()
+    sp.kind, sp.wavelength = abi.SPEC_CONSTANT, float(wavelength)
+    return sp
+
+
+def spectrum_1d(array) -> abi.Spectrum:
+    """piecewise1D (piecewise.f90:140-168) of an (n, 2) array: column 0 wavelengths, column 1
+    the flux (the reference loads it in single precision, parse_spectrum.f90:61-64)."""
+    a = np.asfortranarray(np.asarray(array, dtype=np.float64))
+    assert a.ndim == 2 and a.shape[1] == 2
+    sp = abi.Spectrum()
+    sp.kind, sp.n = abi.SPEC_1D, a.shape[0]
+    sp.array = a.ctypes.data_as(C.POINTER(C.c_double))
+    sp._keep = a
+    return sp
+
+
+def spectrum_2d(image, cell_width, cell_height) -> abi.Spectrum:
+    """piecewise2D (piecewise.f90:190-236) of image(width, height) (Fortran order: the first
+    index is x)."""
+    img = np.asfortranarray(np.asarray(image, dtype=np.float64))
+    sp = abi.Spectrum()
+    sp.kind = abi.SPEC_2D
+    sp.width, sp.height = img.shape
+    sp.image = img.ctypes.data_as(C.POINTER(C.c_double))
+    sp.cell_width, sp.cell_height = float(cell_width), float(cell_height)
+    sp._keep = img
+    return sp
+
+
+def attach_spectrum(source: abi.Source, spectrum: abi.Spectrum) -> abi.Source:
+    """Point source.spectrum at `spectrum` (kept alive by the source object)."""
+    source.spectrum = C.pointer(spectrum)
+    source._spectrum = spectrum
+    return source
+
+
 DIRECTIONS = {"x": (1.0, 0.0, 0.0), "-x": (-1.0, 0.0, 0.0), "y": (0.0, 1.0, 0.0),
               "-y": (0.0, -1.0, 0.0), "z": (0.0, 0.0, 1.0), "-z": (0.0, 0.0, -1.0)}
 
@@ -355,6 +449,31 @@ def camera(p1, p2, p3, layer, nbins, maxval) -> abi.Detector:
     else:
         d.bin_wid = float(maxval) / float(d.nbins)
         d.bin_wid_y = float(maxval) / float(d.nbins)
+    return d
+
+
+def fibre_dect(pos, direction, layer, nbins, focal1=1.0, focal2=1.0, f1_aperture=1.0, f2_aperture=1.0,
+               front_offset=0.0, back_offset=None, front_to_pin=None, pin_to_back=None, pin_aperture=None,
+               accept_angle=90.0, core_diameter=0.01) -> abi.Detector:
+    """init_fibre_dect, detectors.f90:246-329, with the parser's defaults
+    (parse_detectors.f90:262-280): back_offset and pin_to_back default to focal2,
+    front_to_pin to focal1, pin_aperture to max(f1_aperture, f2_aperture)."""
+    d = abi.Detector()
+    d.kind = abi.DET_FIBRE
+    d.nbins = int(nbins) + 1
+    d.layer = int(layer)
+    direction = _norm(direction)
+    for i in range(3):
+        d.pos[i] = float(pos[i]); d.dir[i] = float(direction[i])
+    f = [focal1, focal2, f1_aperture, f2_aperture, front_offset,
+         focal2 if back_offset is None else back_offset,
+         focal1 if front_to_pin is None else front_to_pin,
+         focal2 if pin_to_back is None else pin_to_back,
+         max(f1_aperture, f2_aperture) if pin_aperture is None else pin_aperture,
+         accept_angle, core_diameter]
+    for i, v in enumerate(f):
+        d.fibre[i] = float(v)
+    d.bin_wid = 1.0 if nbins == 0 else float(core_diameter) / 2.0 / float(nbins)
     return d
 
 

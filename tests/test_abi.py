@@ -54,7 +54,9 @@ def test_errors_without_compute(lib_path):
 STRUCTS = {
     "smcrt_sdf_node": (abi.SdfNode, ["kind", "op", "transform", "param", "k", "mus", "n"]),
     "smcrt_grid": (abi.Grid, ["nx", "nz", "xmax", "zmax"]),
-    "smcrt_source": (abi.Source, ["kind", "pos", "dir", "p1", "p3"]),
+    "smcrt_source": (abi.Source, ["kind", "pos", "dir", "p1", "p3", "beam", "radius", "sigma", "rotation",
+                                  "spectrum"]),
+    "smcrt_spectrum": (abi.Spectrum, ["kind", "wavelength", "n", "array", "width", "image", "cell_height"]),
     "smcrt_detector": (abi.Detector, ["kind", "nbins", "pos", "e2", "radius", "bin_wid_y", "fibre"]),
     "smcrt_run_config": (abi.RunConfig, ["n_photons", "seed", "flags"]),
     "smcrt_photon_record": (abi.PhotonRecord, ["pos", "weight", "cell", "draws", "status"]),

@@ -19,6 +19,7 @@ FC = os.environ.get("AMDFLANG", "/opt/rocm/bin/amdflang")
 pytestmark = pytest.mark.skipif(not os.path.exists(FC), reason="no Fortran compiler in this image")
 
 TYPES = {"smcrt_sdf_node": abi.SdfNode, "smcrt_grid": abi.Grid, "smcrt_source": abi.Source,
+         "smcrt_spectrum": abi.Spectrum,
          "smcrt_detector": abi.Detector, "smcrt_run_config": abi.RunConfig, "smcrt_tallies": abi.Tallies,
          "smcrt_device_tallies": abi.DeviceTallies, "smcrt_kernel_times": abi.KernelTimes}
 

@@ -225,3 +225,87 @@ def test_skin_layers_with_detectors():
     gpu, cpu = both(sc, g, src, 3000, dets=dets)
     compare(gpu, cpu)
     assert cpu.counter("fresnel") > 0
+
+
+# ---------------------------------------------- general emitter --
+def _xsrc_cases():
+    rot = (0.3, -0.4, 0.5)
+    yield "circular", scene.circular_source((0.1, -0.2, 0.3), (1.0, 2.0, 2.0), 0.5)
+    for ft in ("square", "circle", "gaussian"):
+        yield f"focus-{ft}", scene.focus_source((0.2, -0.1, 0.4), rot, focal_length=1.5, focus_type=ft, beam_size=0.3)
+    for at in ("tophat", "besselAnnulus", "gaussian"):
+        yield f"annulus-{at}", scene.annulus_source((0.0, 0.0, 0.9), (0.0, 0.0, -1.0), focal_length=1.2,
+                                                    annulus_type=at, rlo=0.3, rhi=0.4, sigma=0.04)
+    yield "annulus-outside", scene.annulus_source((-1.5, 0.0, 0.0), (1.0, 0.0, 0.0), focal_length=1.5,
+                                                  annulus_type="besselAnnulus", rlo=0.48, rhi=0.52)
+    yield "focus-outside", scene.focus_source((0.0, 0.0, 1.6), (0.0, 0.0, -1.0), focal_length=1.6,
+                                              focus_type="circle", beam_size=0.4)
+
+
+@pytest.mark.parametrize("name,src", list(_xsrc_cases()), ids=[c[0] for c in _xsrc_cases()])
+def test_general_emitter_sources(name, src):
+    """circular / focus / annulus sources (photon.f90:214-308, 361-563, 850-1043) through the
+    XSRC kernel instantiation: every photon bit-identical to the CPU restatement."""
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    gpu, cpu = both(sc, scene.grid(40, 40, 40, 1, 1, 1), src, 3000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE)
+    compare(gpu, cpu)
+    assert cpu.counter("photons") == 3000
+
+
+def _blood():
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "test", "optical_props", "blood.dat")
+    return np.loadtxt(p, delimiter=",")
+
+
+@pytest.mark.parametrize("kind", ["point", "uniform", "pencil"])
+def test_spectrum_1d_on_basic_sources(kind):
+    """A 1-D source spectrum (piecewise1D) moves the basic sources onto the general emitter
+    and adds one draw per emission: still bit-identical."""
+    if kind == "point":
+        s = scene.point_source()
+    elif kind == "uniform":
+        s = scene.uniform_source((-1.0, -1.0, 0.9999999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    else:
+        s = scene.pencil_source((0.0, 0.0, 0.9999), (0.0, 0.0, -1.0))
+    scene.attach_spectrum(s, scene.spectrum_1d(_blood()))
+    gpu, cpu = both(builders.setup_scat_test(10.0), scene.grid(32, 32, 32, 1, 1, 1), s, 2000)
+    compare(gpu, cpu)
+
+
+def test_slm_source_2d_spectrum():
+    """slm (photon.f90:159-212) sampling a 2-D image (piecewise2D, Morton-ordered CDF)."""
+    rng = np.random.default_rng(7)
+    img = (rng.random((200, 200)) > 0.7).astype(np.float64)
+    s = scene.slm_source((0.0, 0.0, 0.9999), (0.0, 0.0, -1.0), scene.spectrum_2d(img, 2.0 / 200, 2.0 / 200))
+    # the emitter maps pixel x to (x - 100) / (nx / (2 xmax)): a 200-wide image needs nx = ny = 200
+    gpu, cpu = both(builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0), scene.grid(200, 200, 20, 1, 1, 1), s, 3000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE)
+    compare(gpu, cpu)
+    assert cpu.counter("faults") == 0
+
+
+@pytest.mark.parametrize("kind", ["dslit", "aperture"])
+def test_diffraction_sources(kind):
+    """dslit / aperture (photon.f90:712-848) with a constant and a 1-D spectrum."""
+    g = scene.grid(40, 40, 40, 5.0, 5.0, 5.0)
+    sc = builders.setup_box(0.0, 0.0, 0.0, 1.0, (10.0, 10.0, 10.0), (10.0, 10.0, 10.0))
+    for sp in (scene.spectrum_constant(500e-7), scene.spectrum_1d(_blood() * [1e-7, 1.0])):
+        s = scene.dslit_source() if kind == "dslit" else scene.aperture_source()
+        scene.attach_spectrum(s, sp)
+        gpu, cpu = both(sc, g, s, 2000)
+        compare(gpu, cpu)
+
+
+def test_fibre_detectors():
+    """check_hit_fibre (detectors.f90:331-393) on validateFibreDect.toml's layout: fibres of
+    growing aperture above a point source in an empty box; bins bit-exact."""
+    sc = builders.setup_box(0.0, 0.0, 0.0, 1.0, (10.0, 10.0, 10.0), (10.0, 10.0, 10.0))
+    g = scene.grid(20, 20, 20, 5.0, 5.0, 5.0)
+    dets = [scene.fibre_dect((0.0, 0.0, 2.0), (0.0, 0.0, 1.0), 1, 100, focal1=2.0, focal2=20.0, f1_aperture=a,
+                             f2_aperture=a, back_offset=20.0, pin_aperture=200.0, core_diameter=1.0)
+            for a in (0.5, 1.0, 1.5, 2.0)]
+    gpu, cpu = both(sc, g, scene.point_source(), 20000, dets=dets)
+    compare(gpu, cpu)
+    assert cpu.counter("detector_hits") > 0

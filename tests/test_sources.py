@@ -1,0 +1,334 @@
+"""Sources, spectra and the fibre detector in the CPU restatement (SURVEY.md §8(f) row 3 and
+§8(a) a10), pinned by the reference's own unit tests:
+
+  test/photon/test_photon.f90           Uniform/Pencil/Point/Circular/SLM sources
+  test/optical_props/test_piecewise.f90 piecewise1D (blood.dat) and piecewise2D sampling
+  test/optical_props/test_opticalprops.f90  spectral optical properties
+plus geometric properties of the emitters the reference has no test for (focus, annulus,
+dslit, aperture) and the exact RNG draw count of every emitter. CPU only.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+from rsmcrt_amd import abi, scene
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def fnint(x):
+    """Fortran nint: round half away from zero."""
+    return (np.sign(x) * np.floor(np.abs(x) + 0.5)).astype(np.int64)
+
+
+def blood():
+    return np.loadtxt(os.path.join(GOLDEN, "test", "optical_props", "blood.dat"), delimiter=",")
+
+
+# ---------------------------------------------------------------- test_photon.f90 ----
+def test_uniform_source_kat():
+    """Uniform_src (test_photon.f90:62-121): x pinned to -7.5+7.9e-7, y and z in [-1, 1]."""
+    g = scene.grid(200, 200, 200, 7.5, 7.5, 7.5)
+    s = scene.uniform_source((-7.5, -1.0, -1.0), (0.0, 2.0, 0.0), (0.0, 0.0, 2.0), (1.0, 0.0, 0.0))
+    pos, d, cells, draws = O.emit(g, s, 10000)
+    assert np.all(pos[:, 0] == -7.5 + 7.9e-7)
+    assert np.all(np.abs(pos[:, 1]) <= 1.0) and np.all(np.abs(pos[:, 2]) <= 1.0)
+    assert np.all(draws == 2) and np.all(d == [1.0, 0.0, 0.0])
+
+
+@pytest.mark.parametrize("kind", ["point", "pencil"])
+def test_point_and_pencil_kat(kind):
+    """Point_src / Pencil_src (test_photon.f90:123-161, 204-240): the position is the origin."""
+    g = scene.grid(200, 200, 200, 1.0, 1.0, 1.0)
+    s = scene.point_source((0.0, 0.5, -0.25)) if kind == "point" else \
+        scene.pencil_source((0.0, 0.5, -0.25), (1.0, 0.0, 0.0))
+    pos, d, cells, draws = O.emit(g, s, 1000)
+    assert np.all(pos == [0.0, 0.5, -0.25])
+    assert np.all(draws == (2 if kind == "point" else 0))
+    np.testing.assert_allclose(np.linalg.norm(d, axis=1), 1.0, rtol=1e-14)
+
+
+def test_circular_source_kat():
+    """Circular_src (test_photon.f90:163-202): a disc of radius 2.5 in the plane through pos
+    normal to dir (z = 1)."""
+    g = scene.grid(200, 200, 200, 1.1, 1.1, 1.1)
+    s = scene.circular_source((0.0, 0.0, 1.0), (0.0, 0.0, -1.0), 2.5)
+    pos, d, cells, draws = O.emit(g, s, 10000, seed=12345678)
+    r_kat = np.sqrt((pos[:, 0] + 1) ** 2 + (pos[:, 1] + 1) ** 2)
+    assert not np.any((r_kat > 2.5) & (pos[:, 2] != 1.0))
+    r = np.hypot(pos[:, 0], pos[:, 1])
+    assert np.all(pos[:, 2] == 1.0) and r.max() <= 2.5
+    # uniform over the disc: P(r < R/2) = 1/4
+    assert abs(np.mean(r < 1.25) - 0.25) < 0.02
+    assert np.all(draws == 2)
+
+
+def test_circular_source_tilted():
+    """pos = -(q . T) with T = rotationAlign(x, dir) . invert(translate(pos)): a disc of the given
+    radius centred on pos, in the plane normal to dir; direction = dir."""
+    g = scene.grid(64, 64, 64, 2.0, 2.0, 2.0)
+    n = np.array([1.0, 2.0, 2.0]) / 3.0
+    o = np.array([0.1, -0.2, 0.3])
+    s = scene.circular_source(tuple(o), tuple(n), 0.5)
+    pos, d, cells, draws = O.emit(g, s, 4000)
+    rel = pos - o
+    assert np.abs(rel @ n).max() < 1e-12
+    assert np.linalg.norm(rel, axis=1).max() <= 0.5 + 1e-12
+    assert np.all(np.linalg.norm(d - n, axis=1) < 1e-15)
+
+
+def test_slm_source_kat():
+    """SLM_src (test_photon.f90:242-325): 1e6 photons sampled from test.png (all non-zero
+    pixels set to 1) reproduce the image: sum|image - histogram| / 200^2 < 6e-2."""
+    img = np.load(os.path.join(GOLDEN, "slm_test_png.npz"))["first_channel"].astype(np.float64)
+    img[img > 0] = 1.0
+    g = scene.grid(200, 200, 200, 1.0, 1.0, 1.0)
+    s = scene.slm_source((0.0, 0.0, 1.0), (0.0, 0.0, -1.0), scene.spectrum_2d(img, 2.0 / 200, 2.0 / 200))
+    n = 1_000_000
+    pos, d, cells, draws = O.emit(g, s, n, seed=12345678)
+    idx = fnint((pos[:, 0] + 1.0) / (2.0 / 200)) + 2
+    idy = fnint((pos[:, 1] + 1.0) / (2.0 / 200)) + 2
+    ok = (idx >= 1) & (idy >= 1) & (idx <= 200) & (idy <= 200)
+    out = np.zeros((200, 200))
+    np.add.at(out, (idx[ok] - 1, idy[ok] - 1), 1.0)
+    out /= out.max()
+    sum_dif = np.abs(img - out).sum() / 200 ** 2
+    assert sum_dif < 6e-2, sum_dif
+    assert np.all(draws == 3) and np.all(pos[:, 2] == 1.0)
+
+
+# ----------------------------------------------------------- test_piecewise.f90 ----
+def test_piecewise1d_blood_kat():
+    """test_piecewise1D (test_piecewise.f90:31-70): 1e6 wavelengths from blood.dat reproduce
+    its shape (sum of |normalised pdf - normalised histogram| <= 2)."""
+    data = blood()
+    src = scene.attach_spectrum(scene.point_source(), scene.spectrum_1d(data.astype(np.float32).astype(np.float64)))
+    x, _, draws = O.spectrum_sample(src, 1_000_000, seed=123456789)
+    assert np.all(draws == 1) and x.min() >= 250.0 and x.max() <= 1000.0
+    bin_wid = (1000.0 - 250.0) / 376
+    idx = fnint((x - 250.0) / bin_wid) + 1
+    bins = np.zeros(376)
+    ok = (idx > 0) & (idx < 377)
+    np.add.at(bins, idx[ok] - 1, 1.0)
+    ref = data[:, 1] / data[:, 1].max()
+    diff_sum = np.abs(ref - bins / bins.max()).sum()
+    assert diff_sum <= 2.0, diff_sum
+
+
+def test_piecewise2d_gaussians_kat():
+    """test_piecewise2D (test_piecewise.f90:72-136): an image of two Gaussian blobs, sampled
+    1e6 times with cell size 0.5, is reproduced to sum|image - histogram|/n^2 <= 1e-2.
+    (The blobs are drawn here with numpy; the reference draws them with its own rang.)"""
+    n = 200
+    rng = np.random.default_rng(123456789)
+    data = np.zeros((n, n))
+    bw = 2.0 / n
+    for off in ((-10, -30), (50, 50)):
+        xy = rng.normal(1.0, 0.1, size=(10_000_000, 2))
+        ix = fnint(xy[:, 0] / bw) + off[0]
+        iy = fnint(xy[:, 1] / bw) + off[1]
+        ok = (ix >= 1) & (ix <= n) & (iy >= 1) & (iy <= n)
+        np.add.at(data, (ix[ok] - 1, iy[ok] - 1), 1.0)
+    data /= data.max()
+    src = scene.attach_spectrum(scene.point_source(), scene.spectrum_2d(data, 0.5, 0.5))
+    xr, yr, draws = O.spectrum_sample(src, 1_000_000, seed=123456789)
+    assert np.all(draws == 3)
+    ix = fnint(xr) + 2
+    iy = fnint(yr) + 2
+    ok = (ix >= 1) & (ix <= n) & (iy >= 1) & (iy <= n)
+    bins = np.zeros((n, n))
+    np.add.at(bins, (ix[ok] - 1, iy[ok] - 1), 1.0)
+    bins /= bins.max()
+    diff = np.abs(data - bins).sum() / n ** 2
+    assert diff <= 1e-2, diff
+
+
+# ------------------------------------------------------------ focus / annulus ----
+def _beam_sources():
+    out = []
+    for rot in ((0.0, 0.0, -1.0), (0.0, 0.0, 1.0), (1.0, 0.0, 0.0), (0.3, -0.4, 0.5)):
+        for ft in ("square", "circle", "gaussian"):
+            out.append(("focus", rot, ft))
+        for at in ("tophat", "besselAnnulus", "gaussian"):
+            out.append(("annulus", rot, at))
+    return out
+
+
+@pytest.mark.parametrize("kind,rot,beam", _beam_sources())
+def test_focus_and_annulus_geometry(kind, rot, beam):
+    """focus (photon.f90:361-563) / annulus (:850-1043): unit directions; focus rays pass
+    through the focal point; inside-grid photons lie on the beam plane through pos; beam
+    profile statistics; draw counts (focus 2, annulus 2 or 2k+1 for gaussian)."""
+    g = scene.grid(64, 64, 64, 4.0, 4.0, 4.0)
+    origin = (0.2, -0.1, 0.4)
+    f = 1.5
+    if kind == "focus":
+        s = scene.focus_source(origin, rot, focal_length=f, focus_type=beam, beam_size=0.3)
+    else:
+        s = scene.annulus_source(origin, rot, focal_length=f, annulus_type=beam, rlo=0.5, rhi=0.6, sigma=0.04)
+    n = 20000
+    pos, d, cells, draws = O.emit(g, s, n, seed=99)
+    np.testing.assert_allclose(np.linalg.norm(d, axis=1), 1.0, rtol=0, atol=1e-14)
+    # rotationAlign(a, b) applied as (row vector) . R maps the local beam axis a = -z onto
+    # b = rotation/|rotation| (for b = -a the emitter flips z instead): the beam plane passes
+    # through pos normal to b, the focal point is origin + f*b
+    axis = np.array(rot) / np.linalg.norm(rot)
+    rel = pos - np.array(origin)
+    assert np.abs(rel @ axis).max() < 1e-12
+    radial = np.linalg.norm(rel - np.outer(rel @ axis, axis), axis=1)
+    if kind == "focus":
+        if beam == "square":
+            assert radial.max() <= 0.3 * np.sqrt(2) + 1e-12
+        elif beam == "circle":
+            assert radial.max() <= 0.3 + 1e-12 and abs(np.mean(radial < 0.15) - 0.25) < 0.02
+        else:  # radius = w sqrt(-log(1-u)): P(r < w) = 1 - 1/e
+            assert abs(np.mean(radial < 0.3) - (1 - np.exp(-1))) < 0.02
+        assert np.all(draws == 2)
+    else:
+        if beam == "tophat":
+            assert radial.min() >= 0.5 - 1e-12 and radial.max() <= 0.6 + 1e-12
+            assert abs(np.mean(radial ** 2 < 0.5 * (0.25 + 0.36)) - 0.5) < 0.02
+            assert np.all(draws == 2)
+        elif beam == "besselAnnulus":
+            assert radial.min() >= 0.5 - 1e-12 and radial.max() <= 0.6 + 1e-12
+            assert abs(np.mean(radial < 0.55) - 0.5) < 0.02
+            assert np.all(draws == 2)
+        else:
+            assert abs(radial.mean() - 0.55) < 0.002 and abs(radial.std() - 0.04) < 0.002
+            assert np.all(draws % 2 == 1) and draws.min() >= 3
+    if kind == "focus":
+        # every ray passes through the focal point
+        w = np.array(origin) + f * axis - pos
+        assert np.abs(np.cross(d, w)).max() < 1e-9
+    else:
+        # annulus rays aim from the mid-ring point: they cross the axis at the focal point
+        # displaced by (radius - mid) along the ray's own radial direction
+        assert np.all(d @ axis > 0)
+
+
+def test_annulus_thin_barrier_direction():
+    """thinBarrier.toml's beam (rotation +x): the beam travels along +x."""
+    g = scene.grid(301, 301, 301, 1.5, 1.0, 1.0)
+    s = scene.annulus_source((-1.5, 0.0, 0.0), (1.0, 0.0, 0.0), focal_length=1.5, annulus_type="besselAnnulus",
+                             rlo=0.48, rhi=0.52, sigma=0.05)
+    pos, d, cells, draws = O.emit(g, s, 5000)
+    assert np.all(d[:, 0] > 0.9)
+    # photons start on the x = -1.5 face and are stepped 9e-7 into the grid
+    assert np.all(pos[:, 0] > -1.5) and np.all(pos[:, 0] < -1.5 + 1e-5)
+    assert np.all(cells[:, 0] == 1)
+
+
+@pytest.mark.parametrize("kind", ["dslit", "aperture"])
+def test_diffraction_sources(kind):
+    """dslit (photon.f90:712-780) / aperture (:782-848): the screen plane z2, unit directions
+    pointing down (-z), 5 / 4 draws (+1 with a 1-D spectrum, drawn first)."""
+    g = scene.grid(100, 100, 100, 5.0, 5.0, 5.0)
+    s = scene.dslit_source() if kind == "dslit" else scene.aperture_source()
+    scene.attach_spectrum(s, scene.spectrum_constant(500e-7))
+    pos, d, cells, draws = O.emit(g, s, 5000)
+    z2 = 5.0 - (1.e-5 * (2.0 * (5.0 / 400.0))) if kind == "dslit" else 0.5 - (1.e-5 * (2.0 * 0.5 / 400.0))
+    assert np.all(pos[:, 2] == z2) and np.all(d[:, 2] < 0)
+    np.testing.assert_allclose(np.linalg.norm(d, axis=1), 1.0, rtol=0, atol=1e-14)
+    assert np.all(draws == (5 if kind == "dslit" else 4))
+    s1 = scene.dslit_source() if kind == "dslit" else scene.aperture_source()
+    scene.attach_spectrum(s1, scene.spectrum_1d(blood()))
+    _, _, _, draws1 = O.emit(g, s1, 100)
+    assert np.all(draws1 == draws[:100] + 1)
+
+
+def test_spectrum_draws_shift_streams():
+    """A 1-D spectrum adds one draw per emission after the source's own (point: draws 0-1
+    position the photon, draw 2 samples the wavelength)."""
+    g = scene.grid(32, 32, 32, 1.0, 1.0, 1.0)
+    p0, d0, _, n0 = O.emit(g, scene.point_source(), 200)
+    s = scene.attach_spectrum(scene.point_source(), scene.spectrum_1d(blood()))
+    p1, d1, _, n1 = O.emit(g, s, 200)
+    assert np.array_equal(d0, d1) and np.all(n1 == n0 + 1)
+
+
+def test_bad_source_parameters():
+    g = scene.grid(8, 8, 8, 1.0, 1.0, 1.0)
+    with pytest.raises(RuntimeError):
+        O.emit(g, scene.focus_source((0, 0, 0), (0.0, 0.0, 0.0)), 1)  # zero rotation
+    s = scene.focus_source((0, 0, 0), (0.0, 0.0, 1.0))
+    s.beam = abi.BEAM_TOPHAT  # not a focus_type
+    with pytest.raises(RuntimeError):
+        O.emit(g, s, 1)
+
+
+# ------------------------------------------------------------------ fibre ----
+def test_atan_matches_libm():
+    xs = np.concatenate([np.linspace(-50, 50, 20001), np.logspace(-12, 30, 500), -np.logspace(-12, 30, 500)])
+    got = np.array([O.atan(x) for x in xs])
+    np.testing.assert_allclose(got, np.arctan(xs), rtol=3e-16, atol=0)
+
+
+def _fibre_hit(det, start, direction, sep):
+    bins = np.zeros(det.nbins)
+    hits = C.c_uint64(0)
+    O.lib().oracle_record_hit(C.byref(det), (C.c_double * 3)(*start), (C.c_double * 3)(*direction), sep, 1, 1.0,
+                              bins.ctypes.data_as(C.POINTER(C.c_double)), C.byref(hits))
+    return hits.value, bins
+
+
+def test_fibre_detector_thin_lens_chain():
+    """check_hit_fibre (detectors.f90:331-393) against the 4f chain evaluated by hand."""
+    det = scene.fibre_dect((0.0, 0.0, 2.0), (0.0, 0.0, 1.0), 1, 100, focal1=2.0, focal2=20.0, f1_aperture=0.5,
+                           f2_aperture=0.5, back_offset=20.0, pin_aperture=200.0, core_diameter=1.0)
+
+    def expect(start, direction):
+        t = (2.0 - start[2]) / direction[2]
+        p = np.array(start) + t * np.array(direction)
+        r = np.hypot(p[0], p[1])
+        if r > 0.5:
+            return None
+        cost = direction[2]
+        grad = np.sqrt(1 - cost * cost) / cost
+        grad = -r / 2.0 + grad
+        r = r + grad * 2.0
+        if r > 200.0:
+            return None
+        r = r + grad * 20.0
+        if r > 0.5:
+            return None
+        grad = -r / 20.0 + grad
+        r = r + grad * 20.0
+        if np.degrees(abs(np.arctan(grad))) > 90.0 or r > 0.5:
+            return None
+        return abs(r)
+
+    rng = np.random.default_rng(5)
+    seen = 0
+    for _ in range(400):
+        start = (rng.uniform(-0.6, 0.6), rng.uniform(-0.6, 0.6), 0.0)
+        v = np.array([rng.normal(0, 0.05), rng.normal(0, 0.05), 1.0])
+        v /= np.linalg.norm(v)
+        hits, bins = _fibre_hit(det, start, tuple(v), 10.0)
+        want = expect(start, v)
+        if want is None:
+            assert hits == 0
+        else:
+            seen += 1
+            assert hits == 1
+            idx = min(int(fnint(np.array([want / det.bin_wid]))[0]) + 1, det.nbins)
+            assert bins[idx - 1] == 1.0
+    assert seen > 20
+    # a segment ending before the front lens is not a hit
+    assert _fibre_hit(det, (0.0, 0.0, 0.0), (0.0, 0.0, 1.0), 1.5)[0] == 0
+
+
+def test_validate_fibre_scene_runs():
+    """validateFibreDect.toml's geometry on the oracle: an empty 10^3 box, point source,
+    fibres of growing aperture: hits are monotone in the aperture."""
+    from rsmcrt_amd import builders
+    sc = builders.setup_box(0.0, 0.0, 0.0, 1.0, (10.0, 10.0, 10.0), (10.0, 10.0, 10.0))
+    g = scene.grid(20, 20, 20, 5.0, 5.0, 5.0)
+    dets = [scene.fibre_dect((0.0, 0.0, 2.0), (0.0, 0.0, 1.0), 1, 100, focal1=2.0, focal2=20.0, f1_aperture=a,
+                             f2_aperture=a, back_offset=20.0, pin_aperture=200.0, core_diameter=1.0)
+            for a in (0.5, 1.0, 1.5, 2.0)]
+    r = O.run(sc, g, scene.point_source(), 20000, dets=dets)
+    tot = [r.det_bins[i * 101:(i + 1) * 101].sum() for i in range(4)]
+    assert tot[0] > 0 and all(tot[i] <= tot[i + 1] for i in range(3))
