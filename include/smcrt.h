@@ -282,6 +282,9 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes,
                        int32_t device, smcrt_scene** out);
 void smcrt_scene_destroy(smcrt_scene* scene);
 
+/* The scene's fluence grid, number of top-level SDFs and of detectors (any may be NULL). */
+int smcrt_scene_info(const smcrt_scene* scene, smcrt_grid* grid, int32_t* n_top, int32_t* n_dets);
+
 /* Total doubles of detector data the scene's detectors own (size of det_bins). */
 int smcrt_scene_det_bins(const smcrt_scene* scene, int64_t* n_doubles);
 
@@ -314,6 +317,23 @@ typedef struct smcrt_device_tallies {
 int smcrt_run_device(smcrt_scene* scene, const smcrt_source* src, const smcrt_run_config* cfg,
                      smcrt_device_tallies* dev, void* stream);
 
+/* Batched point sources: the inner loop of the escape function, which calls run_MCRT once
+ * per launch cell with packet = photon("point") placed at the cell centre
+ * (kernelsMod.f90:533-642, 959-1071). Photons [first_photon, first_photon + n_photons) of
+ * EACH of the n_origins isotropic point sources at origins[3k..3k+2] run in one batched
+ * launch; photon i of every origin uses Philox counter i, as every reference run_MCRT
+ * restarts its streams from iseed (kernelsMod.f90:1850). `src` supplies the spectrum only
+ * (NULL: constant). det_totals[k * n_dets + d] accumulates total_dect of detector d over
+ * origin k's photons (detector_base.f90 total_1D/total_2D); io accumulates the tallies of
+ * all origins (its det_bins are not written). SMCRT_FLAG_RECORD_PHOTONS is refused. */
+int smcrt_run_origins(smcrt_scene* scene, const smcrt_source* src, const double* origins, int64_t n_origins,
+                      const smcrt_run_config* cfg, double* det_totals, smcrt_tallies* io);
+
+/* The top-level SDF holding each point, maxloc(ds, mask=ds<0) (0: outside every SDF), and
+ * its kappa (0 when outside), evaluated on the scene's device: the launch-cell test of the
+ * escape function (kernelsMod.f90:589-603). `kappa` may be NULL. */
+int smcrt_scene_classify(smcrt_scene* scene, const double* points, int64_t n, int32_t* layer, double* kappa);
+
 /* Per-kernel device time (ms) of the launches made since the previous query, from HIP
  * events recorded on the launch stream around each kernel group while timing is enabled
  * (off by default; no reference counterpart: it is the measurement hook of bench.py).
@@ -331,6 +351,54 @@ int smcrt_scene_kernel_times(smcrt_scene* scene, smcrt_kernel_times* out);
 /* Normalisation of writer.f90:25-52 (normalise_fluence): grid *= nx*ny*nz / nphotons,
  * i.e. (8*xmax*ymax*zmax)/(nphotons*dx*dy*dz). Host-side helper on an fp32 grid. */
 int smcrt_normalise_fluence(float* grid, const smcrt_grid* g, uint64_t nphotons);
+
+/* ---- escape function (kernelsMod.f90:85-1460, the -DescapeFunction build) --------------
+ * The reference runs run_MCRT once per launch cell of a symmetry grid (escapenphotons
+ * photons from a point source at the cell centre), stores escapeSymmetry(d, cell) =
+ * total_dect(d) / nphotons, fills the cells the symmetry implies, then interpolates onto
+ * the fluence grid (escape(d, i, j, k)). Here every launch cell runs in ONE batched launch
+ * on the resident scene (smcrt_run_origins). Both arrays are fp32 (iarray.f90:18), in
+ * Fortran order with the detector index fastest. */
+typedef enum smcrt_symmetry {
+  SMCRT_SYM_NONE = 0,            /* every cell of the Cartesian symmetry grid        :177-213 */
+  SMCRT_SYM_PRISM = 1,           /* the z layer holding (0,0,0), copied to all z     :215-265 */
+  SMCRT_SYM_FLIPPED = 2,         /* z cells 1..nz/2+1, mirrored in z                 :267-316 */
+  SMCRT_SYM_UNIFORM_SLAB = 3,    /* the column holding (0,0,0), copied to all x, y   :318-363 */
+  SMCRT_SYM_NONE_ROTATIONAL = 4, /* every (r, theta, z) cell of the cylindrical grid :365-411 */
+  SMCRT_SYM_ROTATIONAL_360 = 5   /* theta cell 1 only, copied to every theta         :413-453 */
+} smcrt_symmetry;
+
+typedef struct smcrt_escape_config {  /* [symmetry] table, parse.f90:188-340 */
+  int32_t symmetry;  /* smcrt_symmetry (symmetryType) */
+  int32_t n[3];      /* GridSize: nx, ny, nz (Cartesian) or nr, ntheta, nz (cylindrical) */
+  double max[3];     /* maxValues: xmax, ymax, zmax, or rmax, (unused: tmax = 2 pi), zmax */
+  double pos[3];     /* position: the symmetry grid's centre (symGridPos) */
+  double dir[3];     /* direction: its z axis (symGridDir), normalised by the callee */
+  double rotation;   /* rotation about that axis in degrees, [0, 360) (symGridRot) */
+} smcrt_escape_config;
+
+/* Symmetry-grid dimensions (n0, n1, n2) of escapeSymmetry. Host only. */
+int smcrt_escape_sym_dims(const smcrt_escape_config* cfg, int32_t dims[3]);
+
+/* Launch cells in the reference's loop order: 1-based symmetry-grid indices (3 per cell) and
+ * emission positions (the cell centre taken off the symmetry grid: rotate about z, align z
+ * with `dir`, shift by `pos`; kernelsMod.f90:566-577, 1004-1021). Either output may be NULL
+ * (n_cells is always set). Host only. */
+int smcrt_escape_cells(const smcrt_escape_config* cfg, int64_t* n_cells, int32_t* cells, double* positions);
+
+/* escapeSymmetry -> escape on `grid` (cart_map_escape_sym :644-957 / cyl_map_escape_sym
+ * :1073-1460: tri/bi/linear interpolation, area weights in cylindrical cells, -1 outside the
+ * symmetry grid). escape_sym: n_dets*n0*n1*n2, escape: n_dets*nx*ny*nz. Host only. */
+int smcrt_escape_map(const smcrt_escape_config* cfg, const smcrt_grid* grid, int32_t n_dets, const float* escape_sym,
+                     float* escape);
+
+/* The escape function on a resident scene: cells -> smcrt_scene_classify (cells outside
+ * every SDF or in a kappa = 0 layer keep 0 and are not run) -> one smcrt_run_origins with
+ * run->n_photons per cell -> escapeSymmetry = total / n_photons -> symmetry fill ->
+ * smcrt_escape_map. io accumulates the tallies of every cell's photons, as the reference's
+ * jmean does over its run_MCRT calls. Either output array may be NULL. */
+int smcrt_escape_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_escape_config* cfg,
+                     const smcrt_run_config* run, float* escape_sym, float* escape, smcrt_tallies* io);
 
 /* ---- output formats (src/writer.f90), host-side, no GPU needed ------------------------
  * Written byte for byte as the reference writes them, so its readers

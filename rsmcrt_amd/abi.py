@@ -148,6 +148,17 @@ def record_dtype():
                      ("status", "<u4")])
 
 
+# smcrt_symmetry (escape function, kernelsMod.f90:85-1460)
+SYM_NONE, SYM_PRISM, SYM_FLIPPED, SYM_UNIFORM_SLAB, SYM_NONE_ROTATIONAL, SYM_ROTATIONAL_360 = 0, 1, 2, 3, 4, 5
+SYMMETRY_KINDS = {"none": SYM_NONE, "prism": SYM_PRISM, "flipped": SYM_FLIPPED, "uniformSlab": SYM_UNIFORM_SLAB,
+                  "noneRotational": SYM_NONE_ROTATIONAL, "360rotational": SYM_ROTATIONAL_360}
+
+
+class EscapeConfig(C.Structure):
+    _fields_ = [("symmetry", C.c_int32), ("n", C.c_int32 * 3), ("max", C.c_double * 3), ("pos", C.c_double * 3),
+                ("dir", C.c_double * 3), ("rotation", C.c_double)]
+
+
 class JobDesc(C.Structure):
     _fields_ = [("n_photons", C.c_int64), ("seed", C.c_int64), ("flags", C.c_int32), ("n_nodes", C.c_int32),
                 ("n_top", C.c_int32), ("n_dets", C.c_int32), ("overwrite", C.c_int32), ("grid", Grid),
@@ -165,4 +176,6 @@ EXPORTED_SYMBOLS = [
     "smcrt_run_device", "smcrt_normalise_fluence", "smcrt_scene_set_timing", "smcrt_scene_kernel_times",
     "smcrt_write_data_f32", "smcrt_write_data_f64", "smcrt_write_detector", "smcrt_write_checkpoint",
     "smcrt_job_load", "smcrt_job_destroy", "smcrt_job_info", "smcrt_job_scene", "smcrt_job_metadata", "smcrt_job_run",
+    "smcrt_scene_info", "smcrt_run_origins", "smcrt_scene_classify", "smcrt_escape_sym_dims", "smcrt_escape_cells",
+    "smcrt_escape_map", "smcrt_escape_run",
 ]

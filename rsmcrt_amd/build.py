@@ -13,7 +13,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libsmcrt.so")
-SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp")]
+SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("transport.h", "detmath.h", "geometry.h", "deposit.h",
                                                          "hosterr.h", "toml.h", "mat4.h", "srcplan.h", "png.h")] + [
     os.path.join(ROOT, "include", "smcrt.h")]

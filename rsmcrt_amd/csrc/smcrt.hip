@@ -162,7 +162,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
         const uint32_t take = n < chunk_left ? n : chunk_left;
         const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
         if (L.st == ST_FETCH && rank < take) {
-          L.rng.init(C->first_photon + chunk_base + rank);
+          uint64_t g = C->first_photon + chunk_base + rank;
+          if constexpr (XSRC) {
+            const uint64_t po = C->plan.per_origin;
+            if (po) {  // batched point sources: origin g / po, photon first + g % po
+              const uint64_t o = g / po;
+              LU(LU_ORIGIN) = (uint32_t)o;
+              g = C->plan.first + (g - o * po);
+            }
+          }
+          L.rng.init(g);
           L.st = ST_EMIT;
         }
         chunk_base += take;
@@ -410,7 +419,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
         L.st = ST_G0; L.pend = true;
       }
     }
-    if (K.n_dets && rec) LCTR(LC_HITS) += record_hits(K, C->det_bins, dets, det_off, rec_start, L.dir, rec_sep, L.layer, L.weight);
+    if (K.n_dets && rec) {
+      double* tot = nullptr;
+      if constexpr (XSRC) {
+        if (C->plan.det_totals) tot = C->plan.det_totals + (uint64_t)LU(LU_ORIGIN) * (uint64_t)K.n_dets;
+      }
+      LCTR(LC_HITS) += record_hits(K, C->det_bins, dets, det_off, rec_start, L.dir, rec_sep, L.layer, L.weight, tot);
+    }
 
     // ---- P6: tauint2 write-back checks, :341-362 -----------------------------------------
     if (!L.seg && L.st == ST_T2END) {
@@ -498,13 +513,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           L.fault = false; L.layer = 0;
           LU(LU_STATUS) = 0; LU(LU_NSCATT) = 0; LU(LU_INTER) = 0; LU(LU_BOUNCES) = 0;
           L.xcell = L.ycell = L.zcell = 0;
-          emit<GM, XSRC>(K, C, L);
+          emit<GM, XSRC>(K, C, L, XSRC ? LU(LU_ORIGIN) : 0u);
           if (!test_kernel) {
             int64_t tries = 0;
             while (cell_out(K, L)) {
               if (++tries > MAX_EMIT_TRIES) { L.fault = true; break; }
               LCTR(LC_RETRIES)++;
-              emit<GM, XSRC>(K, C, L);
+              emit<GM, XSRC>(K, C, L, XSRC ? LU(LU_ORIGIN) : 0u);
             }
             if (!L.fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE)) add_cell(K, C->emission, L, 1.0);
           }
@@ -581,6 +596,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   if (nscatt) {  // nscatt = number of scatters (kernelsMod.f90:1966)
     const uint32_t s = wave_sum_u32(LCTR(LC_SCATTERS));
     if (lane_id == 0 && s) atomic_add_nr(nscatt, (double)s);
+  }
+}
+
+// The top-level SDF containing each point: maxloc(ds, mask=ds<0), 0 outside every SDF
+// (kernelsMod.f90:589-595, 1027-1032: the escape function's launch-cell test). One lane per
+// point; the SDF program is walked wave-uniformly as in the transport kernel.
+__global__ __launch_bounds__(256) void classify_kernel(const smcrt_sdf_node* __restrict__ nodes,
+                                                       const ProgOp* __restrict__ prog, int32_t n_prog,
+                                                       const double* __restrict__ pts, int64_t n, int32_t* layer) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i - threadIdx.x < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i < n ? i : n - 1;  // whole waves walk the program together
+    const V3 q = v3(pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]);
+    const EvalOut r = eval_sdfs(nodes, prog, n_prog, q, false, 0, 0);
+    if (i < n) layer[i] = r.maxloc;
   }
 }
 
@@ -1077,12 +1107,20 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
   return SMCRT_OK;
 }
 
+// Batched point sources (smcrt_run_origins): device origin table and per-origin detector totals.
+struct OriginRun {
+  const double* d_origins;
+  double* d_totals;
+  uint64_t per_origin, first;
+};
+
 static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg,
-                  const smcrt_device_tallies& dt, hipStream_t stream) {
+                  const smcrt_device_tallies& dt, hipStream_t stream, const OriginRun* orun = nullptr) {
   if (src->kind < SMCRT_SRC_POINT || src->kind > SMCRT_SRC_APERTURE) return fail(SMCRT_ERR_INVALID_ARG, "bad source kind");
   if (cfg->n_photons == 0) return SMCRT_OK;
-  // sources other than point/uniform/pencil, or a sampled spectrum: the general emitter
-  const bool xsrc = src_needs_plan(src);
+  // sources other than point/uniform/pencil, a sampled spectrum or batched origins: the
+  // general emitter
+  const bool xsrc = src_needs_plan(src) || orun;
   SrcPlan plan;
   std::memset(&plan, 0, sizeof plan);
   if (xsrc) {
@@ -1112,6 +1150,12 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
       plan.spec_x = px.empty() ? nullptr : s->d_spec;
       plan.spec_y = py.empty() ? nullptr : s->d_spec + px.size();
       plan.cdf = s->d_spec + px.size() + py.size();
+    }
+    if (orun) {
+      plan.origins = orun->d_origins;
+      plan.det_totals = orun->d_totals;
+      plan.per_origin = orun->per_origin;
+      plan.first = orun->first;
     }
   }
   KParams K;
@@ -1169,7 +1213,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
       }
     }
     Ch.n_photons = n;
-    Ch.first_photon = cfg->first_photon + done;
+    Ch.first_photon = orun ? done : cfg->first_photon + done;  // (origins: the global queue index)
     Ch.records = dt.records ? dt.records + done : nullptr;
     if (K.rec_pool) s->h_ctl[4] = 0;
     int st = launch_one(s, K, Ch, xsrc, stream);
@@ -1193,11 +1237,11 @@ int smcrt_run_device(smcrt_scene* s, const smcrt_source* src, const smcrt_run_co
   return launch(s, src, cfg, *dev, (hipStream_t)stream);
 }
 
-int smcrt_run(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io) {
-  g_last_error.clear();
-  if (!s || !src || !cfg || !io) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
-  std::lock_guard<std::mutex> g(s->mu);
-  HIPCHK(hipSetDevice(s->device));
+}  // extern "C"
+
+// smcrt_run's body; `orun` (batched origins) is set by smcrt_run_origins. Caller holds s->mu.
+static int run_sync(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io,
+                    const OriginRun* orun) {
   const int64_t nv = (int64_t)s->grid.nx * s->grid.ny * s->grid.nz;
   const bool want[3] = {io->jmean || io->jmean_f64, io->absorb || io->absorb_f64, io->emission || io->emission_f64};
   if (!s->d_grids && (want[0] || want[1] || want[2])) {
@@ -1227,7 +1271,7 @@ int smcrt_run(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* c
   dt.moments = s->d_small + s->det_total + 1;
   dt.counters = (uint64_t*)s->d_counters;
   dt.records = rec ? s->d_records : nullptr;
-  int st = launch(s, src, cfg, dt, s->stream);
+  int st = launch(s, src, cfg, dt, s->stream, orun);
   if (st) return st;
   hipError_t e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) return fail(SMCRT_ERR_DEVICE_FAULT, std::string("transport kernel: ") + hipGetErrorString(e));
@@ -1259,6 +1303,93 @@ int smcrt_run(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* c
   if (rec)
     HIPCHK(hipMemcpy(io->records, s->d_records, sizeof(smcrt_photon_record) * cfg->n_photons, hipMemcpyDeviceToHost));
   return SMCRT_OK;
+}
+
+extern "C" {
+
+int smcrt_run(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io) {
+  g_last_error.clear();
+  if (!s || !src || !cfg || !io) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  return run_sync(s, src, cfg, io, nullptr);
+}
+
+int smcrt_run_origins(smcrt_scene* s, const smcrt_source* src, const double* origins, int64_t n_origins,
+                      const smcrt_run_config* cfg, double* det_totals, smcrt_tallies* io) {
+  g_last_error.clear();
+  if (!s || !cfg || !io || (n_origins > 0 && !origins)) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (n_origins < 0) return fail(SMCRT_ERR_INVALID_ARG, "n_origins < 0");
+  if (cfg->flags & SMCRT_FLAG_RECORD_PHOTONS) return fail(SMCRT_ERR_INVALID_ARG, "photon records are not kept for batched origins");
+  if (n_origins > 0xFFFFFFFFll) return fail(SMCRT_ERR_INVALID_ARG, "more than 2^32 origins");
+  if (n_origins == 0 || cfg->n_photons == 0) return SMCRT_OK;
+  if (cfg->n_photons > UINT64_MAX / (uint64_t)n_origins) return fail(SMCRT_ERR_INVALID_ARG, "photon count overflows");
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  smcrt_source p;  // the escape function's packet = photon("point") (kernelsMod.f90:162-166)
+  if (src) p = *src;
+  else std::memset(&p, 0, sizeof p);
+  p.kind = SMCRT_SRC_POINT;
+  const size_t nt = (size_t)n_origins * (size_t)std::max(s->n_dets, 1);
+  double* d_org = nullptr;
+  double* d_tot = nullptr;
+  int st = dalloc(&d_org, (size_t)n_origins * 3);
+  if (!st) st = dalloc(&d_tot, nt);
+  if (!st) {
+    OriginRun orun{d_org, s->n_dets ? d_tot : nullptr, cfg->n_photons, cfg->first_photon};
+    smcrt_run_config c = *cfg;
+    c.n_photons = cfg->n_photons * (uint64_t)n_origins;
+    hipError_t e = hipMemcpy(d_org, origins, sizeof(double) * 3 * (size_t)n_origins, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(d_tot, 0, sizeof(double) * nt);
+    if (e != hipSuccess) st = fail(SMCRT_ERR_HIP, std::string("origin upload: ") + hipGetErrorString(e));
+    if (!st) st = run_sync(s, &p, &c, io, &orun);
+    if (!st && det_totals && s->n_dets) {
+      std::vector<double> h(nt);
+      e = hipMemcpy(h.data(), d_tot, sizeof(double) * nt, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) st = fail(SMCRT_ERR_HIP, std::string("totals: ") + hipGetErrorString(e));
+      else for (size_t i = 0; i < nt; ++i) det_totals[i] += h[i];
+    }
+  }
+  if (d_org) (void)hipFree(d_org);
+  if (d_tot) (void)hipFree(d_tot);
+  return st;
+}
+
+int smcrt_scene_info(const smcrt_scene* s, smcrt_grid* grid, int32_t* n_top, int32_t* n_dets) {
+  if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
+  if (grid) *grid = s->grid;
+  if (n_top) *n_top = s->n_top;
+  if (n_dets) *n_dets = s->n_dets;
+  return SMCRT_OK;
+}
+
+int smcrt_scene_classify(smcrt_scene* s, const double* points, int64_t n, int32_t* layer, double* kappa) {
+  g_last_error.clear();
+  if (!s || (n > 0 && (!points || !layer))) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (n <= 0) return SMCRT_OK;
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  double* d_pts = nullptr;
+  int32_t* d_lay = nullptr;
+  int st = dalloc(&d_pts, (size_t)n * 3);
+  if (!st) st = dalloc(&d_lay, (size_t)n);
+  if (!st) {
+    hipError_t e = hipMemcpy(d_pts, points, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+      const int blocks = (int)std::min<int64_t>((n + 255) / 256, 65535);
+      hipLaunchKernelGGL(classify_kernel, dim3(blocks), dim3(256), 0, s->stream, (const smcrt_sdf_node*)s->d_nodes,
+                         (const ProgOp*)s->d_prog, (int32_t)s->n_prog, (const double*)d_pts, n, d_lay);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipMemcpy(layer, d_lay, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) st = fail(SMCRT_ERR_HIP, std::string("classify: ") + hipGetErrorString(e));
+  }
+  if (!st && kappa)
+    for (int64_t i = 0; i < n; ++i) kappa[i] = layer[i] > 0 ? s->h_props[layer[i] - 1].kappa : 0.0;
+  if (d_pts) (void)hipFree(d_pts);
+  if (d_lay) (void)hipFree(d_lay);
+  return st;
 }
 
 int smcrt_scene_set_timing(smcrt_scene* s, int32_t enable) {

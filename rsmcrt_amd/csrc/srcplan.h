@@ -34,6 +34,12 @@ struct SrcPlan {
   const double* spec_x;  // 1-D: array(:,1), device
   const double* spec_y;  // 1-D: array(:,2), device
   const double* cdf;     // 1-D / 2-D CDF, device
+  // batched point sources (smcrt_run_origins, the escape function's run_MCRT per launch
+  // cell): queue index g -> origin g / per_origin, photon first + g % per_origin
+  const double* origins;  // 3 per origin, device
+  double* det_totals;     // [origin][detector] totals (total_dect), device
+  uint64_t per_origin;    // 0: a single source
+  uint64_t first;         // photon offset within every origin
 };
 
 // Fill `p` (device pointers left NULL) and the host tables to upload: x, y (1-D) and cdf.
@@ -43,7 +49,7 @@ int build_src_plan(const smcrt_source* src, const smcrt_grid* g, SrcPlan* p, std
 
 // true when the run needs the general emitter (anything but point/uniform/pencil with a
 // constant spectrum)
-inline bool src_needs_plan(const smcrt_source* s) {
+inline bool src_needs_plan(const smcrt_source* s) {  // (batched origins always do)
   return s->kind > SMCRT_SRC_PENCIL || (s->spectrum && s->spectrum->kind != SMCRT_SPEC_CONSTANT);
 }
 

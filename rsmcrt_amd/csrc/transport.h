@@ -169,10 +169,13 @@ __device__ __forceinline__ int64_t f_int(double x) {
 
 // record_hit on every detector for one path segment (detector_base.f90:137-235,
 // detectors.f90:147-469). Returns the number of bin increments.
+// `totals` (batched point sources): add each hit to totals[detector] (total_dect,
+// detector_base.f90) instead of to its bin.
 __device__ __forceinline__ uint32_t record_hits(const KParams& K, double* det_bins,
                                                 const smcrt_detector* __restrict__ dets,
                                                 const int64_t* __restrict__ det_off, V3 start, V3 dir,
-                                                double pointSep, int32_t layer, double weight) {
+                                                double pointSep, int32_t layer, double weight,
+                                                double* totals = nullptr) {
   uint32_t hits = 0;
   double value1D = (double)layer;  // hit_t%value1D <- packet%layer
   for (int32_t di = 0; di < K.n_dets; ++di) {
@@ -257,7 +260,8 @@ __device__ __forceinline__ uint32_t record_hits(const KParams& K, double* det_bi
       }
     }
     if (bin >= 0) {
-      if (data) atomic_add_nr(data + bin, w);
+      if (totals) atomic_add_nr(totals + di, w);
+      else if (data) atomic_add_nr(data + bin, w);
       ++hits;
     }
   }
@@ -343,7 +347,7 @@ struct Lane {
 // costing a register for the whole kernel.
 enum : int { LC_PHOTONS = 0, LC_RETRIES, LC_SCATTERS, LC_ABSORBED, LC_TAU, LC_FRES, LC_REFL, LC_BABORT,
              LC_FAULTS, LC_DRAWS, LC_HITS, LC_ESCAPED, LC_UPD, LC_N };
-enum : int { LU_INTER = 0, LU_BOUNCES, LU_NSCATT, LU_STATUS, LU_N };  // per-photon fields
+enum : int { LU_INTER = 0, LU_BOUNCES, LU_NSCATT, LU_STATUS, LU_ORIGIN, LU_N };  // per-photon fields
 struct LaneShared {
   uint32_t ctr[LC_N][256];
   uint32_t u[LU_N][256];
@@ -469,12 +473,18 @@ __device__ __forceinline__ void step_into_grid(const KParams& K, Lane& L, int ca
 constexpr int MAX_RANG_TRIES = 1000;  // rang's rejection loop (random_mod.f90:116-121), capped
 
 // pos/dir of one emission for every source kind (the cells are set by the caller)
-__device__ __forceinline__ void emit_ext(const KParams& K, const SrcPlan& P, Lane& L) {
+// `oidx`: the lane's origin in a batched point-source run (SrcPlan::origins).
+__device__ __forceinline__ void emit_ext(const KParams& K, const SrcPlan& P, Lane& L, uint32_t oidx) {
   const double TWOPI = 6.283185307179586;
   double wl, tmp;
   switch (P.kind) {
     case SMCRT_SRC_POINT: {  // photon.f90:311-359
-      L.pos = v3(P.origin[0], P.origin[1], P.origin[2]);
+      if (P.origins) {  // set_photon(voxel centre) before each run_MCRT, kernelsMod.f90:579-580
+        const double* o = P.origins + 3 * (uint64_t)oidx;
+        L.pos = v3(o[0], o[1], o[2]);
+      } else {
+        L.pos = v3(P.origin[0], P.origin[1], P.origin[2]);
+      }
       const double phi = L.rng.next(K.key0, K.key1) * TWOPI;
       double sinp, cosp;
       det_sincos(phi, &sinp, &cosp);
@@ -612,10 +622,10 @@ __device__ __forceinline__ void emit_ext(const KParams& K, const SrcPlan& P, Lan
 
 // emit: point photon.f90:311-359 / uniform :566-649 / pencil :652-710
 template <int GM, bool XSRC>
-__device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__ C, Lane& L) {
+__device__ __forceinline__ void emit(const KParams& K, const KCold* __restrict__ C, Lane& L, uint32_t oidx) {
   const smcrt_source& s = C->src;
   if constexpr (XSRC) {
-    emit_ext(K, C->plan, L);
+    emit_ext(K, C->plan, L, oidx);
   } else if (s.kind == SMCRT_SRC_POINT) {
     L.pos = v3(s.pos[0], s.pos[1], s.pos[2]);
     const double phi = L.rng.next(K.key0, K.key1) * 6.283185307179586;

@@ -14,6 +14,8 @@ import ctypes as C
 import os
 import threading
 
+import numpy as np
+
 from . import abi
 from .scene import detector_array
 from .tallies import Result
@@ -53,6 +55,19 @@ def load_library(path: str = LIB_PATH):
         L.smcrt_scene_set_timing.argtypes = [C.c_void_p, C.c_int32]
         L.smcrt_scene_kernel_times.argtypes = [C.c_void_p, C.POINTER(abi.KernelTimes)]
         L.smcrt_normalise_fluence.argtypes = [C.POINTER(C.c_float), C.POINTER(abi.Grid), C.c_uint64]
+        L.smcrt_scene_info.argtypes = [C.c_void_p, C.POINTER(abi.Grid), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.smcrt_run_origins.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(C.c_double), C.c_int64,
+                                        C.POINTER(abi.RunConfig), C.POINTER(C.c_double), C.POINTER(abi.Tallies)]
+        L.smcrt_scene_classify.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_double)]
+        L.smcrt_escape_sym_dims.argtypes = [C.POINTER(abi.EscapeConfig), C.POINTER(C.c_int32)]
+        L.smcrt_escape_cells.argtypes = [C.POINTER(abi.EscapeConfig), C.POINTER(C.c_int64), C.POINTER(C.c_int32),
+                                         C.POINTER(C.c_double)]
+        L.smcrt_escape_map.argtypes = [C.POINTER(abi.EscapeConfig), C.POINTER(abi.Grid), C.c_int32,
+                                       C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.smcrt_escape_run.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.EscapeConfig),
+                                       C.POINTER(abi.RunConfig), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                       C.POINTER(abi.Tallies)]
         if L.smcrt_abi_version() != abi.SMCRT_ABI_VERSION:
             raise SmcrtError("libsmcrt.so ABI version mismatch")
         _lib = L
@@ -120,6 +135,50 @@ class Engine:
         t = res.tallies()
         _check(load_library().smcrt_run(self._h, C.byref(source), C.byref(cfg), C.byref(t)))
         return res
+
+    def run_origins(self, origins, n_photons, source=None, seed=123456789, flags=abi.FLAG_PATHLENGTH,
+                    first_photon=0, result: Result | None = None):
+        """Photons [first_photon, first_photon + n_photons) from an isotropic point source at each
+        of `origins` (k, 3), in one batched launch (smcrt_run_origins). Returns (totals (k, n_dets),
+        Result of all origins' tallies)."""
+        org = np.ascontiguousarray(origins, dtype=np.float64).reshape(-1, 3)
+        k = len(org)
+        res = result if result is not None else Result(self.grid, self.dets, 0)
+        res.n_photons += int(n_photons) * k
+        tot = np.zeros((k, max(1, len(self.dets))))
+        cfg = self.config(n_photons, seed, flags, first_photon)
+        t = res.tallies()
+        _check(load_library().smcrt_run_origins(self._h, C.byref(source) if source is not None else None,
+                                                org.ctypes.data_as(C.POINTER(C.c_double)), k, C.byref(cfg),
+                                                tot.ctypes.data_as(C.POINTER(C.c_double)), C.byref(t)))
+        return tot[:, :len(self.dets)], res
+
+    def classify(self, points):
+        """(layer, kappa) of each point: maxloc(ds, mask=ds<0) over the top-level SDFs."""
+        pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+        lay = np.zeros(len(pts), dtype=np.int32)
+        kap = np.zeros(len(pts))
+        _check(load_library().smcrt_scene_classify(self._h, pts.ctypes.data_as(C.POINTER(C.c_double)), len(pts),
+                                                   lay.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                   kap.ctypes.data_as(C.POINTER(C.c_double))))
+        return lay, kap
+
+    def escape(self, cfg: abi.EscapeConfig, n_photons, source=None, seed=123456789, flags=abi.FLAG_PATHLENGTH,
+               result: Result | None = None):
+        """The escape function (smcrt_escape_run): (escape_sym (n_dets, n0, n1, n2), escape
+        (n_dets, nx, ny, nz), Result). Arrays are fp32 in the reference's index order."""
+        from .escape import sym_dims
+        n0, n1, n2 = sym_dims(cfg)
+        nd = len(self.dets)
+        es = np.zeros((n2, n1, n0, max(nd, 1)), dtype=np.float32)
+        e = np.zeros((self.grid.nz, self.grid.ny, self.grid.nx, max(nd, 1)), dtype=np.float32)
+        res = result if result is not None else Result(self.grid, self.dets, 0)
+        rc = self.config(n_photons, seed, flags, 0)
+        t = res.tallies()
+        _check(load_library().smcrt_escape_run(self._h, C.byref(source) if source is not None else None, C.byref(cfg),
+                                               C.byref(rc), es.ctypes.data_as(C.POINTER(C.c_float)),
+                                               e.ctypes.data_as(C.POINTER(C.c_float)), C.byref(t)))
+        return es.transpose(3, 2, 1, 0)[:nd], e.transpose(3, 2, 1, 0)[:nd], res
 
     def run_device(self, source, cfg: abi.RunConfig, dev: abi.DeviceTallies, stream: int = 0):
         """Asynchronous launch into caller-owned device buffers on `stream` (hipStream_t)."""

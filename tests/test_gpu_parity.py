@@ -309,3 +309,79 @@ def test_fibre_detectors():
     gpu, cpu = both(sc, g, scene.point_source(), 20000, dets=dets)
     compare(gpu, cpu)
     assert cpu.counter("detector_hits") > 0
+
+
+# ------------------------------------ escape function --------------
+def _escape_scene():
+    sc = builders.setup_sphere(10.0, 0.5, 0.8, 1.0, 0.8)
+    g = scene.grid(20, 20, 20, 1, 1, 1)
+    dets = [scene.circle_dect((0.0, 0.0, 0.99), (0.0, 0.0, 1.0), 1, 0.6, 20),
+            scene.annulus_dect((0.0, 0.0, -0.99), (0.0, 0.0, -1.0), 1, 0.2, 0.7, 10),
+            scene.camera((-1.0, -1.0, 0.98), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), 1, 8, 5000.0)]
+    return sc, g, dets
+
+
+def test_run_origins_matches_per_origin_runs():
+    """smcrt_run_origins (all launch cells in one batched launch) == one CPU run per origin,
+    as the reference calls run_MCRT per cell: per-origin detector totals and counters
+    bit-exact, tallies of all origins equal up to summation order."""
+    sc, g, dets = _escape_scene()
+    origins = [(0.0, 0.0, 0.0), (0.3, -0.2, 0.1), (-0.5, 0.45, 0.2), (0.1, 0.1, -0.6), (0.7, 0.0, 0.0)]
+    n = 700
+    with Engine(sc, g, dets) as eng:
+        tot, res = eng.run_origins(origins, n, seed=SEED, flags=abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE)
+    cpu = None
+    want = np.zeros((len(origins), len(dets)))
+    for k, o in enumerate(origins):
+        r = O.run(sc, g, scene.point_source(o), n, seed=SEED, flags=abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE,
+                  dets=dets)
+        want[k] = [r.detector(d).sum() for d in range(len(dets))]
+        cpu = r if cpu is None else cpu.merge(r)
+    assert np.array_equal(tot, want)
+    assert want.sum() > 0
+    assert res.counters_dict() == cpu.counters_dict()
+    assert res.nscatt[0] == cpu.nscatt[0]
+    np.testing.assert_allclose(res.jmean, cpu.jmean, rtol=RTOL, atol=1e-300)
+    assert np.array_equal(res.absorb, cpu.absorb) and np.array_equal(res.emission, cpu.emission)
+
+
+def test_classify_matches_oracle_sdfs():
+    sc, g, dets = _escape_scene()
+    rng = np.random.default_rng(3)
+    pts = rng.uniform(-1.2, 1.2, size=(5000, 3))
+    with Engine(sc, g, dets) as eng:
+        lay, kap = eng.classify(pts)
+    ds = np.stack([O.sdf_eval(sc, pts, which=i) for i in range(sc.n_top)], axis=1)
+    want = np.zeros(len(pts), dtype=np.int32)
+    for p in range(len(pts)):
+        best = None
+        for i in range(sc.n_top):
+            if ds[p, i] < 0.0 and (best is None or ds[p, i] > ds[p, best]):
+                best = i
+        want[p] = 0 if best is None else best + 1
+    assert np.array_equal(lay, want)
+    assert set(np.unique(lay)) == {0, 1, 2}
+
+
+@pytest.mark.parametrize("sym", [("none", (3, 3, 3), (0.9, 0.9, 0.9)),
+                                 ("flipped", (3, 2, 4), (0.8, 0.8, 0.8)),
+                                 ("360rotational", (3, 4, 3), (0.9, 0.0, 0.9))], ids=lambda s: s[0])
+def test_escape_function_end_to_end(sym):
+    """smcrt_escape_run (classify, one batched launch, symmetry fill, interpolation) against
+    oracle/escape_oracle.py (one CPU run_MCRT per launch cell): escapeSymmetry and escape
+    bit-exact (fp32), tallies as in the per-cell runs."""
+    from oracle import escape_oracle as EO
+    from rsmcrt_amd import escape
+    sc, g, dets = _escape_scene()
+    kind, n, mx = sym
+    cfg = escape.escape_config(kind, n, mx)
+    S = EO.Sym(kind, n, mx, (0.0, 0.0, 0.0), (0.0, 0.0, 1.0), 0.0)
+    nph = 300
+    with Engine(sc, g, dets) as eng:
+        es, e, res = eng.escape(cfg, nph, seed=SEED)
+    wes, we, cpu = EO.escape_function(sc, g, dets, S, nph, seed=SEED)
+    assert np.array_equal(es, wes)
+    assert np.array_equal(e, we)
+    assert res.counters_dict() == cpu.counters_dict()
+    np.testing.assert_allclose(res.jmean, cpu.jmean, rtol=RTOL, atol=1e-300)
+    assert es.max() > 0
