@@ -400,6 +400,46 @@ int smcrt_escape_map(const smcrt_escape_config* cfg, const smcrt_grid* grid, int
 int smcrt_escape_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_escape_config* cfg,
                      const smcrt_run_config* run, float* escape_sym, float* escape, smcrt_tallies* io);
 
+/* ---- inverse MCRT (kernelsMod.f90:1462-1787, the -DinverseMCRT build) ------------------
+ * The reference draws maxNumSteps random guesses of the searched optical properties of one
+ * layer (AdaLIPO's explore stage; the exploit branch is unreachable, :1620), runs run_MCRT
+ * for each and scores it with inverse_evaluate (:1753-1787): -mean |total_dect/nphotons -
+ * inverseTarget| over the detectors with a target (/= -1). Here the scene stays resident on
+ * the GPU across the steps. */
+enum {
+  SMCRT_INVERSE_FIND_MUS = 1u << 0,  /* Findmus */
+  SMCRT_INVERSE_FIND_MUA = 1u << 1,  /* Findmua */
+  SMCRT_INVERSE_FIND_G = 1u << 2,    /* Findg   */
+  SMCRT_INVERSE_FIND_N = 1u << 3,    /* Findn   */
+  /* Apply each guess to the layer before its run. The reference builds the trial property
+   * from the layer's ORIGINAL values (mono(mus, mua, hgg, n), :1630-1631), so every step
+   * reruns the same scene; without this flag that behaviour is kept. */
+  SMCRT_INVERSE_APPLY_TRIAL = 1u << 4
+};
+
+typedef struct smcrt_inverse_config {  /* [inverse] table, parse.f90:343-413 */
+  int32_t layer;      /* layer: the first top-level SDF with this layer id is searched */
+  int32_t flags;      /* SMCRT_INVERSE_* */
+  int32_t max_steps;  /* maxNumSteps */
+  int32_t reserved;
+  double max_step_size, grad_step_size, accuracy;  /* parsed; unused by the reference's search */
+  uint64_t seed;      /* stream of the guesses (the reference draws them from its global ran2) */
+} smcrt_inverse_config;
+
+/* The top-level SDF's layer id and optical properties as the reference's getters return
+ * them (sdf_base.f90:192-269; mus = getKappa() - getMua()). Any output may be NULL. */
+int smcrt_scene_get_optprops(const smcrt_scene* scene, int32_t top_index, int32_t* layer, double* mus, double* mua,
+                             double* hgg, double* n);
+
+/* inverse_MCRT on a resident scene. targets[d] = inverseTarget of detector d (-1: none).
+ * steps: max_steps*5 doubles, gradDescentData(maxNumSteps, 5) in Fortran order: guesses of
+ * mus, mua, g, n then the error of step i at steps[(c-1)*max_steps + (i-1)]. run->n_photons
+ * photons per step, each step from photon first_photon (the reference reseeds every
+ * run_MCRT). The layer's original properties are restored at the end. io (may be NULL)
+ * accumulates the tallies of all steps. */
+int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_inverse_config* cfg,
+                      const smcrt_run_config* run, const double* targets, double* steps, smcrt_tallies* io);
+
 /* ---- output formats (src/writer.f90), host-side, no GPU needed ------------------------
  * Written byte for byte as the reference writes them, so its readers
  * (tools/read_nrrd_class.py, tools/plotDetectorsClass.py) load them unchanged. If the
@@ -461,6 +501,11 @@ typedef struct smcrt_job_desc {
 } smcrt_job_desc;
 
 int smcrt_job_load(const char* toml_path, smcrt_job** out);
+/* The reference's build variants parse one more table (parse.f90:64-70): SMCRT_JOB_ESCAPE
+ * reads [symmetry] (its escapenphotons replaces nphotons; symmetryType joins the metadata),
+ * SMCRT_JOB_INVERSE reads [inverse] (an error if absent). smcrt_job_load = DEFAULT. */
+enum { SMCRT_JOB_DEFAULT = 0, SMCRT_JOB_ESCAPE = 1, SMCRT_JOB_INVERSE = 2 };
+int smcrt_job_load_mode(const char* toml_path, int32_t mode, smcrt_job** out);
 void smcrt_job_destroy(smcrt_job* job);
 int smcrt_job_info(const smcrt_job* job, smcrt_job_desc* desc);
 /* Copies the flattened scene (desc.n_nodes nodes, desc.n_top top-level indices) and the
@@ -476,6 +521,21 @@ int smcrt_job_metadata(const smcrt_job* job, char* buf, int32_t cap);
  *   detectors/detector_<i>.dat.
  * `nscatt` (may be NULL) receives the total scatter count. */
 int smcrt_job_run(smcrt_job* job, int32_t device, const char* outdir, double* nscatt);
+
+/* The parsed [symmetry] / [inverse] tables and the detectors' inverseTarget values
+ * (parse_detectors.f90:102, -1 when absent; desc.n_dets of them). */
+int smcrt_job_escape_config(const smcrt_job* job, smcrt_escape_config* out);
+int smcrt_job_inverse_config(const smcrt_job* job, smcrt_inverse_config* out);
+int smcrt_job_targets(const smcrt_job* job, double* targets);
+/* escape_Function (kernelsMod.f90:85-530): smcrt_escape_run, then write_escape
+ * (writer.f90:136-166: escape/dectID_<ID>__escape<i>.nrrd on the fluence grid and
+ * __escapeSym<i>.nrrd on the symmetry grid, with a "dector: <ID>" header line), then
+ * finalise as smcrt_job_run (detector files hold zero bins: the reference's mapping resets
+ * the detectors). */
+int smcrt_job_run_escape(smcrt_job* job, int32_t device, const char* outdir);
+/* inverse_MCRT (kernelsMod.f90:1462-1751) on `device`: steps = gradDescentData(maxNumSteps, 5)
+ * (see smcrt_inverse_run). Writes no files, as the reference. */
+int smcrt_job_run_inverse(smcrt_job* job, int32_t device, int32_t apply_trial, double* steps);
 
 #ifdef __cplusplus
 }

@@ -159,6 +159,20 @@ class EscapeConfig(C.Structure):
                 ("dir", C.c_double * 3), ("rotation", C.c_double)]
 
 
+# inverse MCRT flags (kernelsMod.f90:1462-1787)
+INVERSE_FIND_MUS, INVERSE_FIND_MUA, INVERSE_FIND_G, INVERSE_FIND_N, INVERSE_APPLY_TRIAL = 1, 2, 4, 8, 16
+
+
+class InverseConfig(C.Structure):
+    _fields_ = [("layer", C.c_int32), ("flags", C.c_int32), ("max_steps", C.c_int32), ("reserved", C.c_int32),
+                ("max_step_size", C.c_double), ("grad_step_size", C.c_double), ("accuracy", C.c_double),
+                ("seed", C.c_uint64)]
+
+
+# job modes (the reference's build variants)
+JOB_DEFAULT, JOB_ESCAPE, JOB_INVERSE = 0, 1, 2
+
+
 class JobDesc(C.Structure):
     _fields_ = [("n_photons", C.c_int64), ("seed", C.c_int64), ("flags", C.c_int32), ("n_nodes", C.c_int32),
                 ("n_top", C.c_int32), ("n_dets", C.c_int32), ("overwrite", C.c_int32), ("grid", Grid),
@@ -177,5 +191,7 @@ EXPORTED_SYMBOLS = [
     "smcrt_write_data_f32", "smcrt_write_data_f64", "smcrt_write_detector", "smcrt_write_checkpoint",
     "smcrt_job_load", "smcrt_job_destroy", "smcrt_job_info", "smcrt_job_scene", "smcrt_job_metadata", "smcrt_job_run",
     "smcrt_scene_info", "smcrt_run_origins", "smcrt_scene_classify", "smcrt_escape_sym_dims", "smcrt_escape_cells",
-    "smcrt_escape_map", "smcrt_escape_run",
+    "smcrt_escape_map", "smcrt_escape_run", "smcrt_scene_get_optprops", "smcrt_inverse_run", "smcrt_job_load_mode",
+    "smcrt_job_escape_config", "smcrt_job_inverse_config", "smcrt_job_targets", "smcrt_job_run_escape",
+    "smcrt_job_run_inverse",
 ]

@@ -17,6 +17,7 @@
 #include <sstream>
 #include <string>
 #include <sys/stat.h>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/smcrt.h"
@@ -155,6 +156,11 @@ struct smcrt_job {
   std::vector<int32_t> top;
   std::vector<smcrt_detector> dets;
   std::vector<std::string> det_ids;
+  std::vector<double> det_targets;  // inverseTarget per detector
+  // the -DescapeFunction / -DinverseMCRT builds' extra tables (parse.f90:64-70)
+  int32_t mode = SMCRT_JOB_DEFAULT;
+  smcrt_escape_config esc{};
+  smcrt_inverse_config inv{};
   // [output]
   std::string outfile = "fluence.nrrd", outfile_absorb = "absorb.nrrd", rendersourcefile = "source_render.nrrd";
   bool render_source = false, overwrite = false;
@@ -533,13 +539,19 @@ void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:
   const Value* arr = T::find(root, "detectors");
   if (!arr) return;
   if (arr->kind != Value::TABLE_ARRAY) throw Fail(SMCRT_ERR_INVALID_ARG, "detectors must be [[detectors]] tables");
-  std::vector<std::pair<smcrt_detector, std::string>> by_kind[4];  // circle, annulus, fibre, camera
+  struct Det {
+    smcrt_detector d;
+    std::string id;
+    double target;  // inverseTarget (parse_detectors.f90:102), -1 = none
+  };
+  std::vector<Det> by_kind[4];  // circle, annulus, fibre, camera
   for (const Value& e : arr->arr) {
     const Table* c = e.table.get();
     const std::string type = T::get_string(c, "type", "");
     const Value* idv = T::find(c, "ID");
     if (!idv) throw Fail(SMCRT_ERR_INVALID_ARG, "Need to specify a detector ID");
     const std::string id = idv->kind == Value::STRING ? idv->s : std::to_string(idv->i);
+    const double target = T::get_real(c, "inverseTarget", -1.0);
     if (T::get_bool(c, "trackHistory", false)) throw Fail(SMCRT_ERR_UNSUPPORTED, "Track history currently incompatable with OpenMP!");
     smcrt_detector d;
     std::memset(&d, 0, sizeof(d));
@@ -558,7 +570,7 @@ void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:
       d.nbins = (int32_t)nb + 1;
       d.bin_wid = nb == 0 ? 1.0 : d.radius / (double)nb;
       for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
-      by_kind[0].push_back({d, id});
+      by_kind[0].push_back({d, id, target});
     } else if (type == "annulus") {  // :291-311, detectors.f90:166-200 (direction not normalised)
       const double r1 = T::get_real(c, "radius1", 0.1), r2 = T::get_real(c, "radius2", 0.2);
       if (r2 <= r1) throw Fail(SMCRT_ERR_INVALID_ARG, "Radius2 is smaller than or equal to radius1!");
@@ -568,7 +580,7 @@ void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:
       d.nbins = (int32_t)nb + 1;
       d.bin_wid = nb == 0 ? 1.0 : (r2 - r1) / (double)nb;
       for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
-      by_kind[1].push_back({d, id});
+      by_kind[1].push_back({d, id, target});
     } else if (type == "fibre") {  // handle_fibre_collection_dect :233-294, init_fibre_dect detectors.f90:246-329
       const double l = len3(dir);
       for (int i = 0; i < 3; ++i) dir[i] = dir[i] / l;
@@ -588,7 +600,7 @@ void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:
       d.nbins = (int32_t)nb + 1;
       d.bin_wid = nb == 0 ? 1.0 : F[10] / 2.0 / (double)nb;
       for (int i = 0; i < 3; ++i) { d.pos[i] = pos[i]; d.dir[i] = dir[i]; }
-      by_kind[2].push_back({d, id});
+      by_kind[2].push_back({d, id, target});
     } else if (type == "camera") {  // :118-147, init_camera detectors.f90:401-445
       double p1[3] = {-1.0, -1.0, -1.0}, p2[3] = {2.0, 0.0, 0.0}, p3[3] = {0.0, 2.0, 0.0};
       get_vector(c, "p1", p1); get_vector(c, "p2", p2); get_vector(c, "p3", p3);
@@ -605,15 +617,16 @@ void parse_detectors(smcrt_job& J, const Table* root) {  // parse_detectors.f90:
       d.height = len3(e2);
       d.nbins = (int32_t)nb + 1;
       d.bin_wid = d.bin_wid_y = nb == 0 ? 1.0 : maxval / (double)d.nbins;
-      by_kind[3].push_back({d, id});
+      by_kind[3].push_back({d, id, target});
     } else {
       throw Fail(SMCRT_ERR_INVALID_ARG, "Invalid detector type: " + type);
     }
   }
   for (int k = 0; k < 4; ++k)
     for (auto& p : by_kind[k]) {
-      J.dets.push_back(p.first);
-      J.det_ids.push_back(p.second);
+      J.dets.push_back(p.d);
+      J.det_ids.push_back(p.id);
+      J.det_targets.push_back(p.target);
     }
 }
 
@@ -638,6 +651,84 @@ void parse_simulation(smcrt_job& J, const Table* root) {  // parse.f90:159-186
   J.ckptfreq = T::get_int(s, "checkpoint_every_n", 1000000);
 }
 
+// a 3-vector of the [symmetry] table (parse.f90:225-281): absent -> default
+template <class V>
+void sym_vec3(const Table* t, const std::string& key, const char* err, V out[3], V def) {
+  const Value* v = T::find(t, key);
+  if (!v) { out[0] = out[1] = out[2] = def; return; }
+  if (v->kind != Value::ARRAY || v->arr.size() != 3) throw Fail(SMCRT_ERR_INVALID_ARG, err);
+  for (int i = 0; i < 3; ++i) {
+    if (!v->arr[i].is_number()) throw Fail(SMCRT_ERR_INVALID_ARG, err);
+    if (std::is_integral<V>::value && v->arr[i].kind != Value::INT) throw Fail(SMCRT_ERR_INVALID_ARG, err);
+    out[i] = (V)v->arr[i].number();
+  }
+}
+
+void parse_symmetry(smcrt_job& J, const Table* root) {  // parse.f90:188-340
+  smcrt_escape_config& e = J.esc;
+  std::memset(&e, 0, sizeof e);
+  e.dir[2] = 1.0;
+  const Table* c = T::get_table(root, "symmetry");
+  std::string type = "none";
+  if (c) {
+    type = T::get_string(c, "symmetryType", "none");
+    J.set("symmetryType", fmt_str(type));
+    J.nphotons = T::get_int(c, "escapenphotons", 100000);
+    sym_vec3<int32_t>(c, "GridSize", "Need a vector of size 3 for symmetry grid size.", e.n, 10);
+    sym_vec3<double>(c, "maxValues", "Need a vector of size 3 for symmetry max values.", e.max, 1.0);
+    sym_vec3<double>(c, "position", "Need a vector of size 3 for symmetry position.", e.pos, 0.0);
+    double dv[3];
+    const Value* dvv = T::find(c, "direction");
+    if (dvv) sym_vec3<double>(c, "direction", "Need a vector of size 3 for symmetry position.", dv, 0.0);
+    else { dv[0] = 0.0; dv[1] = 0.0; dv[2] = 1.0; }
+    e.rotation = T::get_real(c, "rotation", 0.0);
+    if (e.rotation < 0.0 || e.rotation >= 360.0)
+      throw Fail(SMCRT_ERR_INVALID_ARG, "Must specifcy a rotation for symmetry that is between 0.0 and 360.0, inclusive of 0.0");
+    if (dv[0] == 0.0 && dv[1] == 0.0 && dv[2] == 0.0)
+      throw Fail(SMCRT_ERR_INVALID_ARG, "Must specify a non-zero direction for symmetry");
+    const double ln = std::sqrt(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]);  // dir%magnitude()
+    for (int i = 0; i < 3; ++i) e.dir[i] = dv[i] / ln;
+    static const char* const names[6] = {"none", "prism", "flipped", "uniformSlab", "noneRotational", "360rotational"};
+    e.symmetry = -1;
+    for (int i = 0; i < 6; ++i)
+      if (type == names[i]) e.symmetry = i;
+    if (e.symmetry < 0) throw Fail(SMCRT_ERR_INVALID_ARG, "Unrecognised symmetry type");
+  } else {  // :313-339
+    J.set("symmetryType", fmt_str(type));
+    J.nphotons = 100000;
+    e.symmetry = SMCRT_SYM_NONE;
+    e.n[0] = e.n[1] = e.n[2] = 10;
+    e.max[0] = e.max[1] = e.max[2] = 1.0;
+  }
+}
+
+void parse_inverse(smcrt_job& J, const Table* root) {  // parse.f90:343-413
+  smcrt_inverse_config& v = J.inv;
+  std::memset(&v, 0, sizeof v);
+  const Table* c = T::get_table(root, "inverse");
+  if (!c) throw Fail(SMCRT_ERR_INVALID_ARG, "Need inverse table in input param file");
+  v.max_step_size = T::get_real(c, "maxStepSize", 1.0);
+  J.set("maxStepSize", fmt_real(v.max_step_size));
+  v.grad_step_size = T::get_real(c, "gradStepSize", 0.0001);
+  J.set("gradStepSize", fmt_real(v.grad_step_size));
+  v.accuracy = T::get_real(c, "accuracy", 0.01);
+  J.set("accuracy", fmt_real(v.accuracy));
+  v.max_steps = (int32_t)T::get_int(c, "maxNumSteps", 1000);
+  J.set("maxNumSteps", std::to_string(v.max_steps));
+  const char* keys[4] = {"Findmua", "Findmus", "Findg", "Findn"};
+  const int32_t bits[4] = {SMCRT_INVERSE_FIND_MUA, SMCRT_INVERSE_FIND_MUS, SMCRT_INVERSE_FIND_G, SMCRT_INVERSE_FIND_N};
+  for (int i = 0; i < 4; ++i) {
+    const bool b = T::get_bool(c, keys[i], false);
+    J.set(keys[i], b ? "true" : "false");
+    if (b) v.flags |= bits[i];
+  }
+  const int64_t layer = T::get_int(c, "layer", -985464082);
+  if (layer == -985464082) throw Fail(SMCRT_ERR_INVALID_ARG, "Must specifiy a layer in inverse table");
+  v.layer = (int32_t)layer;
+  J.set("inverseLayer", std::to_string(v.layer));
+  v.seed = (uint64_t)J.iseed;
+}
+
 bool mkdirs(const std::string& d) {
   std::string cur;
   std::stringstream ss(d);
@@ -657,8 +748,13 @@ bool mkdirs(const std::string& d) {
 extern "C" {
 
 int smcrt_job_load(const char* toml_path, smcrt_job** out) {
+  return smcrt_job_load_mode(toml_path, SMCRT_JOB_DEFAULT, out);
+}
+
+int smcrt_job_load_mode(const char* toml_path, int32_t mode, smcrt_job** out) {
   smcrt::g_last_error.clear();
   if (!toml_path || !out) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (mode < SMCRT_JOB_DEFAULT || mode > SMCRT_JOB_INVERSE) return ffail(SMCRT_ERR_INVALID_ARG, "bad job mode");
   *out = nullptr;
   std::ifstream f(toml_path, std::ios::binary);
   if (!f) return ffail(SMCRT_ERR_INVALID_ARG, std::string("cannot read ") + toml_path);
@@ -667,6 +763,7 @@ int smcrt_job_load(const char* toml_path, smcrt_job** out) {
   const std::string text = buf.str();
   smcrt_job* J = new smcrt_job();
   J->toml_path = toml_path;
+  J->mode = mode;
   try {
     Table root = smcrt::toml::Parser(text).parse();
     // parse_params order (parse.f90:46-66); the simulation table is read first here only
@@ -677,6 +774,8 @@ int smcrt_job_load(const char* toml_path, smcrt_job** out) {
     std::vector<Prim> sdfs = setup_geometry(*J, &root);
     parse_detectors(*J, &root);
     parse_output(*J, &root);
+    if (mode == SMCRT_JOB_ESCAPE) parse_symmetry(*J, &root);
+    if (mode == SMCRT_JOB_INVERSE) parse_inverse(*J, &root);
     flatten(sdfs, J->nodes, J->top);
   } catch (const smcrt::toml::ParseError& e) {
     delete J;
@@ -731,6 +830,50 @@ int smcrt_job_metadata(const smcrt_job* J, char* buf, int32_t cap) {
   return (int32_t)d.size() < cap ? SMCRT_OK : ffail(SMCRT_ERR_INVALID_ARG, "metadata buffer too small");
 }
 
+}  // extern "C"
+
+namespace {
+
+// finalise (kernelsMod.f90:2321-2416): normalise and write jmean/<fluence>,
+// emission/<render_source_name>, absorb/absorb.nrrd and detectors/detector_<i>.dat under
+// outdir (the reference's fileplace).
+int finalise_writes(smcrt_job* J, const char* outdir, std::vector<float>& jmean, std::vector<float>& absorb,
+                    std::vector<float>& emission, const std::vector<double>& det_bins) {
+  int st;
+  const std::string base = std::string(outdir) + "/";
+  if (!mkdirs(base + "jmean") || !mkdirs(base + "emission") || !mkdirs(base + "absorb") ||
+      (!J->dets.empty() && !mkdirs(base + "detectors")))
+    return ffail(SMCRT_ERR_INVALID_ARG, "cannot create output directories under " + base);
+  std::vector<char> meta(1 << 16);
+  if ((st = smcrt_job_metadata(J, meta.data(), (int32_t)meta.size()))) return st;
+  const int32_t ow = J->overwrite ? 1 : 0;
+  if ((st = smcrt_normalise_fluence(jmean.data(), &J->grid, (uint64_t)J->nphotons))) return st;
+  if ((st = smcrt_write_data_f32((base + "jmean/" + J->outfile).c_str(), jmean.data(), J->grid.nx, J->grid.ny,
+                                 J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
+    return st;
+  if ((st = smcrt_normalise_fluence(emission.data(), &J->grid, (uint64_t)J->nphotons))) return st;
+  if ((st = smcrt_write_data_f32((base + "emission/" + J->rendersourcefile).c_str(), emission.data(), J->grid.nx,
+                                 J->grid.ny, J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
+    return st;
+  if ((st = smcrt_write_data_f32((base + "absorb/absorb.nrrd").c_str(), absorb.data(), J->grid.nx, J->grid.ny,
+                                 J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
+    return st;
+  size_t off = 0;
+  for (size_t i = 0; i < J->dets.size(); ++i) {
+    const smcrt_detector& d = J->dets[i];
+    const size_t n = d.kind == SMCRT_DET_CAMERA ? (size_t)d.nbins * d.nbins : (size_t)d.nbins;
+    if ((st = smcrt_write_detector((base + "detectors/detector_" + std::to_string(i + 1) + ".dat").c_str(), &d,
+                                   det_bins.data() + off, J->det_ids[i].c_str(), J->nphotons)))
+      return st;
+    off += n;
+  }
+  return SMCRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 // default_MCRT without checkpoint loading (kernelsMod.f90:14-82): run_MCRT on `device`,
 // then finalise's normalisation and writes (:2321-2416) under `outdir` (the reference's
 // fileplace): jmean/<fluence>, emission/<render_source_name>, absorb/absorb.nrrd,
@@ -763,34 +906,106 @@ int smcrt_job_run(smcrt_job* J, int32_t device, const char* outdir, double* nsca
   smcrt_scene_destroy(scene);
   if (st) return st;
   if (nscatt_out) *nscatt_out = nscatt;
-  const std::string base = std::string(outdir) + "/";
-  if (!mkdirs(base + "jmean") || !mkdirs(base + "emission") || !mkdirs(base + "absorb") ||
-      (!J->dets.empty() && !mkdirs(base + "detectors")))
-    return ffail(SMCRT_ERR_INVALID_ARG, "cannot create output directories under " + base);
-  std::vector<char> meta(1 << 16);
-  if ((st = smcrt_job_metadata(J, meta.data(), (int32_t)meta.size()))) return st;
-  const int32_t ow = J->overwrite ? 1 : 0;
-  if ((st = smcrt_normalise_fluence(jmean.data(), &J->grid, (uint64_t)J->nphotons))) return st;
-  if ((st = smcrt_write_data_f32((base + "jmean/" + J->outfile).c_str(), jmean.data(), J->grid.nx, J->grid.ny,
-                                 J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
-    return st;
-  if ((st = smcrt_normalise_fluence(emission.data(), &J->grid, (uint64_t)J->nphotons))) return st;
-  if ((st = smcrt_write_data_f32((base + "emission/" + J->rendersourcefile).c_str(), emission.data(), J->grid.nx,
-                                 J->grid.ny, J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
-    return st;
-  if ((st = smcrt_write_data_f32((base + "absorb/absorb.nrrd").c_str(), absorb.data(), J->grid.nx, J->grid.ny,
-                                 J->grid.nz, meta.data(), nullptr, ow, nullptr, 0)))
-    return st;
-  size_t off = 0;
-  for (size_t i = 0; i < J->dets.size(); ++i) {
-    const smcrt_detector& d = J->dets[i];
-    const size_t n = d.kind == SMCRT_DET_CAMERA ? (size_t)d.nbins * d.nbins : (size_t)d.nbins;
-    if ((st = smcrt_write_detector((base + "detectors/detector_" + std::to_string(i + 1) + ".dat").c_str(), &d,
-                                   det_bins.data() + off, J->det_ids[i].c_str(), J->nphotons)))
-      return st;
-    off += n;
-  }
+  return finalise_writes(J, outdir, jmean, absorb, emission, det_bins);
   return SMCRT_OK;
+}
+
+int smcrt_job_escape_config(const smcrt_job* J, smcrt_escape_config* out) {
+  if (!J || !out) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (J->mode != SMCRT_JOB_ESCAPE) return ffail(SMCRT_ERR_INVALID_ARG, "job was not loaded in SMCRT_JOB_ESCAPE mode");
+  *out = J->esc;
+  return SMCRT_OK;
+}
+
+int smcrt_job_inverse_config(const smcrt_job* J, smcrt_inverse_config* out) {
+  if (!J || !out) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (J->mode != SMCRT_JOB_INVERSE) return ffail(SMCRT_ERR_INVALID_ARG, "job was not loaded in SMCRT_JOB_INVERSE mode");
+  *out = J->inv;
+  return SMCRT_OK;
+}
+
+int smcrt_job_targets(const smcrt_job* J, double* targets) {
+  if (!J || (!targets && !J->det_targets.empty())) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  for (size_t i = 0; i < J->det_targets.size(); ++i) targets[i] = J->det_targets[i];
+  return SMCRT_OK;
+}
+
+int smcrt_job_run_escape(smcrt_job* J, int32_t device, const char* outdir) {
+  if (!J || !outdir) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (J->mode != SMCRT_JOB_ESCAPE) return ffail(SMCRT_ERR_INVALID_ARG, "job was not loaded in SMCRT_JOB_ESCAPE mode");
+  if (J->loadckpt) return ffail(SMCRT_ERR_UNSUPPORTED, "load_checkpoint is not supported by smcrt_job_run_escape");
+  int32_t dims[3];
+  int st = smcrt_escape_sym_dims(&J->esc, dims);
+  if (st) return st;
+  smcrt_scene* scene = nullptr;
+  st = smcrt_scene_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(), &J->grid,
+                          J->dets.empty() ? nullptr : J->dets.data(), (int32_t)J->dets.size(), device, &scene);
+  if (st) return st;
+  const size_t nv = (size_t)J->grid.nx * J->grid.ny * J->grid.nz;
+  const size_t nd = J->dets.size();
+  const size_t ns = (size_t)dims[0] * dims[1] * dims[2];
+  std::vector<float> jmean(nv, 0.f), absorb(nv, 0.f), emission(nv, 0.f);
+  std::vector<float> esym(std::max<size_t>(1, nd * ns)), esc(std::max<size_t>(1, nd * nv));
+  double nscatt = 0.0;
+  smcrt_tallies io;
+  std::memset(&io, 0, sizeof(io));
+  io.jmean = jmean.data(); io.absorb = absorb.data(); io.emission = emission.data();
+  io.nscatt = &nscatt;
+  smcrt_run_config cfg;
+  std::memset(&cfg, 0, sizeof(cfg));
+  cfg.n_photons = (uint64_t)J->nphotons;  // escapenphotons per launch cell (parse.f90:222-223)
+  cfg.seed = (uint64_t)J->iseed;
+  cfg.flags = SMCRT_FLAG_PATHLENGTH | (J->render_source ? SMCRT_FLAG_RENDER_SOURCE : 0);
+  st = smcrt_escape_run(scene, &J->src, &J->esc, &cfg, esym.data(), esc.data(), &io);
+  smcrt_scene_destroy(scene);
+  if (st) return st;
+  // write_escape (writer.f90:136-166), before finalise: the metadata is the parsed dict
+  const std::string base = std::string(outdir) + "/";
+  if (!mkdirs(base + "escape")) return ffail(SMCRT_ERR_INVALID_ARG, "cannot create " + base + "escape");
+  const std::string meta = J->dump();
+  const int32_t ow = J->overwrite ? 1 : 0;
+  std::vector<float> slice;
+  for (size_t i = 0; i < nd; ++i) {
+    const std::string stem = base + "escape/dectID_" + J->det_ids[i];
+    slice.resize(nv);
+    for (size_t k = 0; k < nv; ++k) slice[k] = esc[k * nd + i];
+    if ((st = smcrt_write_data_f32((stem + "__escape" + std::to_string(i + 1) + ".nrrd").c_str(), slice.data(),
+                                   J->grid.nx, J->grid.ny, J->grid.nz, meta.c_str(), J->det_ids[i].c_str(), ow,
+                                   nullptr, 0)))
+      return st;
+    slice.resize(ns);
+    for (size_t k = 0; k < ns; ++k) slice[k] = esym[k * nd + i];
+    if ((st = smcrt_write_data_f32((stem + "__escapeSym" + std::to_string(i + 1) + ".nrrd").c_str(), slice.data(),
+                                   dims[0], dims[1], dims[2], meta.c_str(), J->det_ids[i].c_str(), ow, nullptr, 0)))
+      return st;
+  }
+  // finalise: the mapping reset the detectors (reset(dects) per fluence cell, :676), so
+  // their files hold zero bins
+  int64_t nb = 0;
+  for (const auto& d : J->dets) nb += d.kind == SMCRT_DET_CAMERA ? (int64_t)d.nbins * d.nbins : d.nbins;
+  std::vector<double> zero((size_t)std::max<int64_t>(1, nb), 0.0);
+  return finalise_writes(J, outdir, jmean, absorb, emission, zero);
+}
+
+int smcrt_job_run_inverse(smcrt_job* J, int32_t device, int32_t apply_trial, double* steps) {
+  if (!J || !steps) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if (J->mode != SMCRT_JOB_INVERSE) return ffail(SMCRT_ERR_INVALID_ARG, "job was not loaded in SMCRT_JOB_INVERSE mode");
+  smcrt_scene* scene = nullptr;
+  int st = smcrt_scene_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(),
+                              &J->grid, J->dets.empty() ? nullptr : J->dets.data(), (int32_t)J->dets.size(), device,
+                              &scene);
+  if (st) return st;
+  smcrt_run_config cfg;
+  std::memset(&cfg, 0, sizeof(cfg));
+  cfg.n_photons = (uint64_t)J->nphotons;
+  cfg.seed = (uint64_t)J->iseed;
+  cfg.flags = SMCRT_FLAG_PATHLENGTH | (J->render_source ? SMCRT_FLAG_RENDER_SOURCE : 0);
+  smcrt_inverse_config inv = J->inv;
+  if (apply_trial) inv.flags |= SMCRT_INVERSE_APPLY_TRIAL;
+  st = smcrt_inverse_run(scene, &J->src, &inv, &cfg, J->det_targets.empty() ? nullptr : J->det_targets.data(), steps,
+                         nullptr);
+  smcrt_scene_destroy(scene);
+  return st;
 }
 
 }  // extern "C"

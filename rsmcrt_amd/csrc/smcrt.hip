@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/smcrt.h"
+#include "scene_internal.h"
 #include "transport.h"
 #include "deposit.h"
 #include "hosterr.h"
@@ -970,6 +971,35 @@ int smcrt_scene_set_optprops(smcrt_scene* s, int32_t i, double mus, double mua, 
   HIPCHK(hipStreamSynchronize(s->stream));
   return SMCRT_OK;
 }
+
+int smcrt_scene_get_optprops(const smcrt_scene* s, int32_t i, int32_t* layer, double* mus, double* mua, double* hgg,
+                             double* n) {
+  if (!s || i < 0 || i >= s->n_top) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or index");
+  const smcrt_sdf_node& nd = s->h_nodes[s->h_top[i]];
+  if (layer) *layer = nd.layer;
+  if (mua) *mua = nd.mua;
+  if (mus) *mus = s->h_props[i].kappa - nd.mua;  // getKappa() - getMua(), kernelsMod.f90:1574-1575
+  if (hgg) *hgg = nd.hgg;
+  if (n) *n = nd.n;
+  return SMCRT_OK;
+}
+
+}  // extern "C"
+
+int smcrt::scene_node_optprops(const smcrt_scene* s, int32_t i, double out[4]) {
+  if (!s || i < 0 || i >= s->n_top) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or index");
+  const smcrt_sdf_node& nd = s->h_nodes[s->h_top[i]];
+  out[0] = nd.mus; out[1] = nd.mua; out[2] = nd.hgg; out[3] = nd.n;
+  return SMCRT_OK;
+}
+
+int smcrt::scene_det_size(const smcrt_scene* s, int32_t d, int64_t* n) {
+  if (!s || d < 0 || d >= s->n_dets) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or detector");
+  *n = (d + 1 < s->n_dets ? s->h_det_off[d + 1] : s->det_total) - s->h_det_off[d];
+  return SMCRT_OK;
+}
+
+extern "C" {
 
 // Refine the records-per-photon estimate from the last binned launch, if it has landed.
 static void refine_rpp(smcrt_scene* s) {

@@ -60,6 +60,10 @@ def load_library(path: str = LIB_PATH):
                                         C.POINTER(abi.RunConfig), C.POINTER(C.c_double), C.POINTER(abi.Tallies)]
         L.smcrt_scene_classify.argtypes = [C.c_void_p, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_int32),
                                            C.POINTER(C.c_double)]
+        L.smcrt_scene_get_optprops.argtypes = [C.c_void_p, C.c_int32, C.POINTER(C.c_int32)] + [C.POINTER(C.c_double)] * 4
+        L.smcrt_inverse_run.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.InverseConfig),
+                                        C.POINTER(abi.RunConfig), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                        C.POINTER(abi.Tallies)]
         L.smcrt_escape_sym_dims.argtypes = [C.POINTER(abi.EscapeConfig), C.POINTER(C.c_int32)]
         L.smcrt_escape_cells.argtypes = [C.POINTER(abi.EscapeConfig), C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                                          C.POINTER(C.c_double)]
@@ -179,6 +183,27 @@ class Engine:
                                                C.byref(rc), es.ctypes.data_as(C.POINTER(C.c_float)),
                                                e.ctypes.data_as(C.POINTER(C.c_float)), C.byref(t)))
         return es.transpose(3, 2, 1, 0)[:nd], e.transpose(3, 2, 1, 0)[:nd], res
+
+    def get_optprops(self, top_index: int):
+        """(layer, mus, mua, hgg, n) as the reference's getters return them (mus = kappa - mua)."""
+        lay = C.c_int32()
+        v = [C.c_double() for _ in range(4)]
+        _check(load_library().smcrt_scene_get_optprops(self._h, top_index, C.byref(lay), *[C.byref(x) for x in v]))
+        return (lay.value, *[x.value for x in v])
+
+    def inverse(self, source, cfg: abi.InverseConfig, n_photons, targets, seed=123456789,
+                flags=abi.FLAG_PATHLENGTH, result: Result | None = None):
+        """inverse_MCRT on the resident scene: gradDescentData (max_steps, 5)."""
+        m = cfg.max_steps
+        out = np.zeros((5, m))
+        tg = np.ascontiguousarray(targets, dtype=np.float64)
+        rc = self.config(n_photons, seed, flags, 0)
+        t = result.tallies() if result is not None else None
+        _check(load_library().smcrt_inverse_run(self._h, C.byref(source), C.byref(cfg), C.byref(rc),
+                                                tg.ctypes.data_as(C.POINTER(C.c_double)),
+                                                out.ctypes.data_as(C.POINTER(C.c_double)),
+                                                C.byref(t) if t is not None else None))
+        return out.T.copy()
 
     def run_device(self, source, cfg: abi.RunConfig, dev: abi.DeviceTallies, stream: int = 0):
         """Asynchronous launch into caller-owned device buffers on `stream` (hipStream_t)."""

@@ -23,6 +23,12 @@ def _lib():
                                       C.POINTER(abi.Detector)]
         L.smcrt_job_metadata.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
         L.smcrt_job_run.argtypes = [C.c_void_p, C.c_int32, C.c_char_p, C.POINTER(C.c_double)]
+        L.smcrt_job_load_mode.argtypes = [C.c_char_p, C.c_int32, C.POINTER(C.c_void_p)]
+        L.smcrt_job_escape_config.argtypes = [C.c_void_p, C.POINTER(abi.EscapeConfig)]
+        L.smcrt_job_inverse_config.argtypes = [C.c_void_p, C.POINTER(abi.InverseConfig)]
+        L.smcrt_job_targets.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        L.smcrt_job_run_escape.argtypes = [C.c_void_p, C.c_int32, C.c_char_p]
+        L.smcrt_job_run_inverse.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_double)]
         _declared = True
     return L
 
@@ -33,12 +39,16 @@ def _check(st):
 
 
 class Job:
-    """A parsed input file (smcrt_job_load)."""
+    """A parsed input file (smcrt_job_load_mode). mode: "default", "escape" (the
+    -DescapeFunction build: [symmetry]) or "inverse" (-DinverseMCRT: [inverse])."""
 
-    def __init__(self, toml_path):
+    MODES = {"default": abi.JOB_DEFAULT, "escape": abi.JOB_ESCAPE, "inverse": abi.JOB_INVERSE}
+
+    def __init__(self, toml_path, mode: str = "default"):
         L = _lib()
         h = C.c_void_p()
-        _check(L.smcrt_job_load(str(toml_path).encode(), C.byref(h)))
+        self.mode = mode
+        _check(L.smcrt_job_load_mode(str(toml_path).encode(), self.MODES[mode], C.byref(h)))
         self._h = h
         self.desc = abi.JobDesc()
         _check(L.smcrt_job_info(self._h, C.byref(self.desc)))
@@ -77,3 +87,32 @@ class Job:
         ns = C.c_double()
         _check(_lib().smcrt_job_run(self._h, device, str(outdir).encode(), C.byref(ns)))
         return ns.value
+
+    def targets(self):
+        """inverseTarget of each detector (-1: none)."""
+        t = (C.c_double * max(1, self.desc.n_dets))()
+        _check(_lib().smcrt_job_targets(self._h, t))
+        return [t[i] for i in range(self.desc.n_dets)]
+
+    def escape_config(self) -> abi.EscapeConfig:
+        c = abi.EscapeConfig()
+        _check(_lib().smcrt_job_escape_config(self._h, C.byref(c)))
+        return c
+
+    def inverse_config(self) -> abi.InverseConfig:
+        c = abi.InverseConfig()
+        _check(_lib().smcrt_job_inverse_config(self._h, C.byref(c)))
+        return c
+
+    def run_escape(self, outdir, device: int = 0):
+        """escape_Function: the batched escape run, write_escape and finalise under outdir."""
+        _check(_lib().smcrt_job_run_escape(self._h, device, str(outdir).encode()))
+
+    def run_inverse(self, device: int = 0, apply_trial: bool = False):
+        """inverse_MCRT: gradDescentData (maxNumSteps, 5) as a numpy array."""
+        import numpy as np
+        m = self.inverse_config().max_steps
+        out = np.zeros((5, m))  # Fortran (maxNumSteps, 5): column c contiguous
+        _check(_lib().smcrt_job_run_inverse(self._h, device, 1 if apply_trial else 0,
+                                            out.ctypes.data_as(C.POINTER(C.c_double))))
+        return out.T.copy()

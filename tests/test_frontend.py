@@ -201,3 +201,110 @@ def test_job_run_scat_test(tmp_path, kats):
     with Engine(builders.setup_scat_test(10.0), d.grid) as eng:
         r = eng.run(d.source, d.n_photons, seed=d.seed)
     assert np.array_equal(output.normalise_fluence(r.jmean.astype(np.float32), d.grid, d.n_photons), data)
+
+
+# ------------------------- the escape / inverse build variants --------
+def test_escape_mode_symmetry_table():
+    """res/default.toml under -DescapeFunction: parse_symmetry (parse.f90:188-340)."""
+    j = Job(res("default.toml"), mode="escape")
+    c = j.escape_config()
+    assert c.symmetry == abi.SYM_ROTATIONAL_360
+    assert list(c.n) == [100, 500, 200] and list(c.max) == [60.0, 360.0, 30.0]
+    assert list(c.pos) == [0.0, 0.0, 0.0] and list(c.dir) == [1.0, 0.0, 0.0] and c.rotation == 0.0
+    assert j.desc.n_photons == 100000  # escapenphotons replaces nphotons
+    assert 'symmetryType = "360rotational"' in j.metadata()
+    assert j.targets() == [-1.0] * 11
+    # the default build neither parses nor records the table
+    d = Job(res("default.toml"))
+    assert d.desc.n_photons == 1000000 and "symmetryType" not in d.metadata()
+    with pytest.raises(SmcrtError):
+        d.escape_config()
+
+
+def test_escape_mode_defaults_without_table():
+    """No [symmetry] table: symmetry none, 10^3 grid of half-size 1, 1e5 photons (:313-339)."""
+    j = Job(res("scat_test.toml"), mode="escape")
+    c = j.escape_config()
+    assert c.symmetry == abi.SYM_NONE and list(c.n) == [10, 10, 10] and list(c.max) == [1.0, 1.0, 1.0]
+    assert list(c.dir) == [0.0, 0.0, 1.0] and j.desc.n_photons == 100000
+
+
+def test_inverse_mode_table():
+    """res/thinBarrier.toml under -DinverseMCRT: parse_inverse (parse.f90:343-413)."""
+    j = Job(res("thinBarrier.toml"), mode="inverse")
+    c = j.inverse_config()
+    assert c.layer == 1 and c.max_steps == 30000
+    assert (c.max_step_size, c.grad_step_size, c.accuracy) == (1.0, 0.0005, 0.001)
+    assert c.flags == abi.INVERSE_FIND_MUA | abi.INVERSE_FIND_MUS
+    meta = j.metadata()
+    for k in ("maxStepSize", "gradStepSize", "accuracy", "maxNumSteps", "Findmua", "Findmus", "Findg", "Findn",
+              "inverseLayer"):
+        assert k + " = " in meta
+    with pytest.raises(SmcrtError, match="Need inverse table"):
+        Job(res("default.toml"), mode="inverse")
+
+
+def test_escape_mode_bad_symmetry(tmp_path):
+    text = open(res("scat_test.toml")).read()
+    for extra, why in (('[symmetry]\nsymmetryType = "cubic"\n', "Unrecognised symmetry type"),
+                       ('[symmetry]\nrotation = 360.0\n', "rotation for symmetry"),
+                       ('[symmetry]\ndirection = [0.0, 0.0, 0.0]\n', "non-zero direction"),
+                       ('[symmetry]\nGridSize = [1, 2]\n', "grid size")):
+        p = tmp_path / "s.toml"
+        p.write_text(text + "\n" + extra)
+        with pytest.raises(SmcrtError, match=why):
+            Job(str(p), mode="escape")
+
+
+@pytest.mark.gpu
+def test_job_run_escape_files(tmp_path):
+    """escape_Function on res/default.toml (360rotational symmetry, 11 annulus detectors) with
+    a smaller symmetry grid, fluence grid and photon count: write_escape's files hold the
+    arrays of the batched escape run (smcrt_escape_run on the same scene)."""
+    from tests.test_writers import read_nrrd_like_reference
+    from rsmcrt_amd.engine import Engine
+    text = open(res("default.toml")).read()
+    text = (text.replace("GridSize = [100,500,200]", "GridSize = [4,3,5]")
+            .replace("escapenphotons = 100000", "escapenphotons = 300")
+            .replace("nxg = 200", "nxg = 20").replace("nyg = 110", "nyg = 11").replace("nzg = 100", "nzg = 10"))
+    p = tmp_path / "esc.toml"
+    p.write_text(text)
+    j = Job(str(p), mode="escape")
+    out = tmp_path / "out"
+    j.run_escape(out)
+    d = j.desc
+    sc = scene.Scene([])
+    sc.nodes = [j.nodes[i] for i in range(d.n_nodes)]
+    sc.top = list(j.top[:d.n_top])
+    with Engine(sc, d.grid, j.detectors) as eng:
+        es, e, _ = eng.escape(j.escape_config(), d.n_photons, source=d.source, seed=d.seed)
+    assert es.max() > 0
+    for i, det_id in enumerate([f"Offset{k}mm" for k in range(1, 12)]):
+        a, hdr = read_nrrd_like_reference(out / "escape" / f"dectID_{det_id}__escape{i + 1}.nrrd")
+        b, _ = read_nrrd_like_reference(out / "escape" / f"dectID_{det_id}__escapeSym{i + 1}.nrrd")
+        assert np.array_equal(a, e[i]) and np.array_equal(b, es[i])
+    assert (out / "jmean" / "fluence.nrrd").exists() and (out / "detectors" / "detector_1.dat").exists()
+
+
+@pytest.mark.gpu
+def test_job_run_inverse(tmp_path):
+    """inverse_MCRT on res/thinBarrier.toml (with a target detector added, fewer steps and
+    photons): guesses inside AdaLIPO's bounds, every step's error identical (the reference
+    reruns the original layer), and a different error per step with the trial applied."""
+    text = open(res("thinBarrier.toml")).read()
+    # (a 0.5-thick barrier: the file's zero-thickness box never scatters)
+    text = (text.replace("maxNumSteps = 30000", "maxNumSteps = 3").replace("nphotons = 10000000", "nphotons = 2000")
+            .replace("BoxDimensions = [0.0,2.0,2.0]", "BoxDimensions = [0.5,2.0,2.0]")
+            + '\n[[detectors]]\ntype = "circle"\nID = "T"\nposition = [1.49, 0.0, 0.0]\ndirection = [1.0, 0.0, 0.0]\n'
+            'radius = 1.0\nnbins = 10\ninverseTarget = 0.2\n')
+    p = tmp_path / "inv.toml"
+    p.write_text(text)
+    j = Job(str(p), mode="inverse")
+    assert j.targets() == [0.2]
+    g = j.run_inverse()
+    assert g.shape == (3, 5)
+    assert np.all((g[:, 0] >= 0) & (g[:, 0] <= 100)) and np.all((g[:, 1] >= 0) & (g[:, 1] <= 100))
+    assert np.all(g[:, 2] == 0.0) and np.all(g[:, 3] == 1.0)  # hgg, n not searched
+    assert np.all(g[:, 4] == g[0, 4]) and g[0, 4] < 0
+    t = j.run_inverse(apply_trial=True)
+    assert np.array_equal(t[:, :4], g[:, :4]) and len(set(t[:, 4])) > 1

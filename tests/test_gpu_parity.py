@@ -385,3 +385,26 @@ def test_escape_function_end_to_end(sym):
     assert res.counters_dict() == cpu.counters_dict()
     np.testing.assert_allclose(res.jmean, cpu.jmean, rtol=RTOL, atol=1e-300)
     assert es.max() > 0
+
+
+@pytest.mark.parametrize("apply_trial", [False, True], ids=["reference", "apply-trial"])
+def test_inverse_mcrt(apply_trial):
+    """smcrt_inverse_run (resident scene, one run per step) against oracle/inverse_oracle.py
+    (one CPU run_MCRT per step): gradDescentData bit-exact; the layer is restored."""
+    from oracle import inverse_oracle as IO
+    sc, g, dets = _escape_scene()
+    targets = [0.05, -1.0, 0.3]
+    cfg = abi.InverseConfig()
+    cfg.layer, cfg.max_steps, cfg.seed = 1, 4, SEED
+    cfg.flags = abi.INVERSE_FIND_MUS | abi.INVERSE_FIND_G | (abi.INVERSE_APPLY_TRIAL if apply_trial else 0)
+    src = scene.point_source((0.0, 0.0, 0.1))
+    with Engine(sc, g, dets) as eng:
+        before = eng.get_optprops(0)
+        got = eng.inverse(src, cfg, 400, targets, seed=SEED)
+        assert eng.get_optprops(0) == before
+    want = IO.inverse_mcrt(sc, g, dets, src, 1, {"mus", "g"}, 4, 400, targets, seed=SEED, apply_trial=apply_trial)
+    assert np.array_equal(got, want)
+    if not apply_trial:
+        assert np.all(got[:, 4] == got[0, 4])  # the reference reruns the same scene every step
+    else:
+        assert len(set(got[:, 4])) > 1
