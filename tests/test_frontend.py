@@ -282,29 +282,31 @@ def test_job_run_escape_files(tmp_path):
     for i, det_id in enumerate([f"Offset{k}mm" for k in range(1, 12)]):
         a, hdr = read_nrrd_like_reference(out / "escape" / f"dectID_{det_id}__escape{i + 1}.nrrd")
         b, _ = read_nrrd_like_reference(out / "escape" / f"dectID_{det_id}__escapeSym{i + 1}.nrrd")
-        assert np.array_equal(a, e[i]) and np.array_equal(b, es[i])
+        assert np.array_equal(a, e[i].T) and np.array_equal(b, es[i].T)  # (the reader gives z, y, x)
     assert (out / "jmean" / "fluence.nrrd").exists() and (out / "detectors" / "detector_1.dat").exists()
 
 
 @pytest.mark.gpu
 def test_job_run_inverse(tmp_path):
     """inverse_MCRT on res/thinBarrier.toml (with a target detector added, fewer steps and
-    photons): guesses inside AdaLIPO's bounds, every step's error identical (the reference
+    photons, searching g only): guesses inside AdaLIPO's bounds, every step's error identical (the reference
     reruns the original layer), and a different error per step with the trial applied."""
     text = open(res("thinBarrier.toml")).read()
     # (a 0.5-thick barrier: the file's zero-thickness box never scatters)
     text = (text.replace("maxNumSteps = 30000", "maxNumSteps = 3").replace("nphotons = 10000000", "nphotons = 2000")
             .replace("BoxDimensions = [0.0,2.0,2.0]", "BoxDimensions = [0.5,2.0,2.0]")
+            .replace("Findmua = true", "Findmua = false").replace("Findmus = true", "Findmus = false")
+            .replace("Findg = false", "Findg = true")
             + '\n[[detectors]]\ntype = "circle"\nID = "T"\nposition = [1.49, 0.0, 0.0]\ndirection = [1.0, 0.0, 0.0]\n'
-            'radius = 1.0\nnbins = 10\ninverseTarget = 0.2\n')
+            'radius = 1.0\nnbins = 10\nlayer = 2\ninverseTarget = 0.2\n')
     p = tmp_path / "inv.toml"
     p.write_text(text)
     j = Job(str(p), mode="inverse")
     assert j.targets() == [0.2]
     g = j.run_inverse()
     assert g.shape == (3, 5)
-    assert np.all((g[:, 0] >= 0) & (g[:, 0] <= 100)) and np.all((g[:, 1] >= 0) & (g[:, 1] <= 100))
-    assert np.all(g[:, 2] == 0.0) and np.all(g[:, 3] == 1.0)  # hgg, n not searched
+    assert np.all((g[:, 2] >= -1) & (g[:, 2] <= 1)) and len(set(g[:, 2])) == 3  # only g is searched
+    assert np.all(g[:, 0] == g[0, 0]) and np.all(g[:, 1] == 0.075) and np.all(g[:, 3] == 1.0)
     assert np.all(g[:, 4] == g[0, 4]) and g[0, 4] < 0
     t = j.run_inverse(apply_trial=True)
     assert np.array_equal(t[:, :4], g[:, :4]) and len(set(t[:, 4])) > 1

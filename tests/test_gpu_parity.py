@@ -408,3 +408,16 @@ def test_inverse_mcrt(apply_trial):
         assert np.all(got[:, 4] == got[0, 4])  # the reference reruns the same scene every step
     else:
         assert len(set(got[:, 4])) > 1
+
+
+def test_general_emitter_with_detectors():
+    """thinBarrier.toml's annulus beam through a 0.5-thick scattering barrier onto a circle
+    detector: the general emitter (XSRC) with detector tallies, bit-exact."""
+    sc = builders.setup_box(10.0, 0.075, 0.0, 1.0, (0.5, 2.0, 2.0), (3.0, 2.0, 2.0), position=(-0.75, 0.0, 0.0))
+    g = scene.grid(61, 41, 41, 1.5, 1.0, 1.0)
+    src = scene.annulus_source((-1.5, 0.0, 0.0), (1.0, 0.0, 0.0), focal_length=1.5, annulus_type="besselAnnulus",
+                               rlo=0.48, rhi=0.52, sigma=0.05)
+    dets = [scene.circle_dect((1.49, 0.0, 0.0), (1.0, 0.0, 0.0), 2, 1.0, 10)]
+    gpu, cpu = both(sc, g, src, 3000, dets=dets)
+    compare(gpu, cpu)
+    assert cpu.counter("detector_hits") > 0
