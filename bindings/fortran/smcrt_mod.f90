@@ -33,6 +33,12 @@ module smcrt_mod
         SMCRT_FLAG_RENDER_SOURCE = 4, SMCRT_FLAG_TEST_KERNEL = 8, SMCRT_FLAG_END_EARLY = 16, &
         SMCRT_FLAG_RECORD_PHOTONS = 32
     integer, parameter :: SMCRT_NCOUNTERS = 16
+    ! smcrt_symmetry (escape function, kernelsMod.f90:85-1460)
+    integer(c_int32_t), parameter :: SMCRT_SYM_NONE = 0, SMCRT_SYM_PRISM = 1, SMCRT_SYM_FLIPPED = 2, &
+        SMCRT_SYM_UNIFORM_SLAB = 3, SMCRT_SYM_NONE_ROTATIONAL = 4, SMCRT_SYM_ROTATIONAL_360 = 5
+    ! inverse MCRT flags (kernelsMod.f90:1462-1787)
+    integer(c_int32_t), parameter :: SMCRT_INVERSE_FIND_MUS = 1, SMCRT_INVERSE_FIND_MUA = 2, &
+        SMCRT_INVERSE_FIND_G = 4, SMCRT_INVERSE_FIND_N = 8, SMCRT_INVERSE_APPLY_TRIAL = 16
 
     type, bind(C) :: smcrt_sdf_node
         integer(c_int32_t) :: kind = 0, layer = 0, op = 0, first_child = 0, n_children = 0
@@ -97,6 +103,18 @@ module smcrt_mod
         type(c_ptr) :: counters = c_null_ptr, records = c_null_ptr
     end type smcrt_device_tallies
 
+    type, bind(C) :: smcrt_escape_config          ! the [symmetry] table
+        integer(c_int32_t) :: symmetry = 0, n(3) = 10
+        real(c_double)     :: max(3) = 1._c_double, pos(3) = 0._c_double
+        real(c_double)     :: dir(3) = [0._c_double, 0._c_double, 1._c_double], rotation = 0._c_double
+    end type smcrt_escape_config
+
+    type, bind(C) :: smcrt_inverse_config         ! the [inverse] table
+        integer(c_int32_t) :: layer, flags, max_steps = 1000, reserved = 0
+        real(c_double)     :: max_step_size = 1._c_double, grad_step_size = 1e-4_c_double, accuracy = 0.01_c_double
+        integer(c_int64_t) :: seed = 123456789
+    end type smcrt_inverse_config
+
     type, bind(C) :: smcrt_kernel_times
         real(c_double)     :: transport_ms = 0._c_double, deposit_ms = 0._c_double
         integer(c_int64_t) :: launches = 0, reserved = 0
@@ -155,6 +173,55 @@ module smcrt_mod
             type(smcrt_run_config), intent(in) :: cfg
             type(smcrt_tallies), intent(inout) :: io
         end function smcrt_run
+
+        ! the escape function's batched launch cells (kernelsMod.f90:533-642): one launch for
+        ! every origin; det_totals(n_dets, n_origins) accumulates total_dect per origin
+        integer(c_int) function smcrt_run_origins(scene, src, origins, n_origins, cfg, det_totals, io) &
+                bind(C, name="smcrt_run_origins")
+            import :: c_int, c_ptr, c_double, c_int64_t, smcrt_source, smcrt_run_config, smcrt_tallies
+            type(c_ptr), value                 :: scene
+            type(smcrt_source), intent(in)     :: src
+            real(c_double), intent(in)         :: origins(3, *)
+            integer(c_int64_t), value          :: n_origins
+            type(smcrt_run_config), intent(in) :: cfg
+            real(c_double), intent(inout)      :: det_totals(*)
+            type(smcrt_tallies), intent(inout) :: io
+        end function smcrt_run_origins
+
+        integer(c_int) function smcrt_scene_classify(scene, points, n, layer, kappa) bind(C, name="smcrt_scene_classify")
+            import :: c_int, c_ptr, c_double, c_int64_t, c_int32_t
+            type(c_ptr), value             :: scene
+            real(c_double), intent(in)     :: points(3, *)
+            integer(c_int64_t), value      :: n
+            integer(c_int32_t), intent(out) :: layer(*)
+            real(c_double), intent(out)    :: kappa(*)
+        end function smcrt_scene_classify
+
+        ! escape_Function (kernelsMod.f90:85-530): escape_sym(n_dets, n0, n1, n2) and
+        ! escape(n_dets, nxg, nyg, nzg), real(sp) as iarray.f90:18
+        integer(c_int) function smcrt_escape_run(scene, src, cfg, run, escape_sym, escape, io) &
+                bind(C, name="smcrt_escape_run")
+            import :: c_int, c_ptr, c_float, smcrt_source, smcrt_escape_config, smcrt_run_config, smcrt_tallies
+            type(c_ptr), value                    :: scene
+            type(smcrt_source), intent(in)        :: src
+            type(smcrt_escape_config), intent(in) :: cfg
+            type(smcrt_run_config), intent(in)    :: run
+            real(c_float), intent(out)            :: escape_sym(*), escape(*)
+            type(smcrt_tallies), intent(inout)    :: io
+        end function smcrt_escape_run
+
+        ! inverse_MCRT (kernelsMod.f90:1462-1751): steps = gradDescentData(max_steps, 5)
+        integer(c_int) function smcrt_inverse_run(scene, src, cfg, run, targets, steps, io) &
+                bind(C, name="smcrt_inverse_run")
+            import :: c_int, c_ptr, c_double, smcrt_source, smcrt_inverse_config, smcrt_run_config
+            type(c_ptr), value                     :: scene
+            type(smcrt_source), intent(in)         :: src
+            type(smcrt_inverse_config), intent(in) :: cfg
+            type(smcrt_run_config), intent(in)     :: run
+            real(c_double), intent(in)             :: targets(*)
+            real(c_double), intent(out)            :: steps(*)
+            type(c_ptr), value                     :: io
+        end function smcrt_inverse_run
 
         integer(c_int) function smcrt_run_device(scene, src, cfg, dev, stream) bind(C, name="smcrt_run_device")
             import :: c_int, c_ptr, smcrt_source, smcrt_run_config, smcrt_device_tallies

@@ -21,7 +21,8 @@ pytestmark = pytest.mark.skipif(not os.path.exists(FC), reason="no Fortran compi
 TYPES = {"smcrt_sdf_node": abi.SdfNode, "smcrt_grid": abi.Grid, "smcrt_source": abi.Source,
          "smcrt_spectrum": abi.Spectrum,
          "smcrt_detector": abi.Detector, "smcrt_run_config": abi.RunConfig, "smcrt_tallies": abi.Tallies,
-         "smcrt_device_tallies": abi.DeviceTallies, "smcrt_kernel_times": abi.KernelTimes}
+         "smcrt_device_tallies": abi.DeviceTallies, "smcrt_kernel_times": abi.KernelTimes,
+         "smcrt_escape_config": abi.EscapeConfig, "smcrt_inverse_config": abi.InverseConfig}
 
 
 def _build_module(tmp):
