@@ -73,6 +73,17 @@ __device__ __forceinline__ uint64_t d2u(double x) { return (uint64_t)__double_as
 __device__ __forceinline__ double u2d(uint64_t u) { return __longlong_as_double((long long)u); }
 
 // natural log: fdlibm e_log.c algorithm (identical operation sequence to the oracle)
+#ifdef SMCRT_ABL_FAST_MATH  // timing ablation only: fp32 hardware log/sin/cos, not bit-exact
+__device__ __forceinline__ double det_log(double x) { return (double)__logf((float)x); }
+__device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
+  float fs, fc;
+  __sincosf((float)x, &fs, &fc);
+  *s = fs; *c = fc;
+}
+#define SMCRT_HAVE_FAST_MATH 1
+#endif
+
+#ifndef SMCRT_HAVE_FAST_MATH
 __device__ inline double det_log(double x) {
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
                two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
@@ -175,6 +186,8 @@ __device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
 
 
 // atan (fdlibm s_atan.c), for the fibre detector's acceptance angle (detectors.f90:386).
+#endif  // SMCRT_HAVE_FAST_MATH
+
 __device__ inline double det_atan(double x) {
   const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
                             1.57079632679489655800e+00};

@@ -1385,6 +1385,20 @@ int smcrt_run_origins(smcrt_scene* s, const smcrt_source* src, const double* ori
   return st;
 }
 
+#ifdef SMCRT_DIAG
+// Diagnostic builds only (not in include/smcrt.h): read and clear the kernel's lane-state
+// occupancy (72) and per-phase s_memtime sums (9).
+int smcrt_diag_read(unsigned long long* out) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), sizeof(unsigned long long) * 72));
+  HIPCHK(hipMemcpyFromSymbol(out + 72, HIP_SYMBOL(g_diag_t), sizeof(unsigned long long) * 9));
+  unsigned long long z[72] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof z));
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_t), z, sizeof(unsigned long long) * 9));
+  return SMCRT_OK;
+}
+#endif
+
 int smcrt_scene_info(const smcrt_scene* s, smcrt_grid* grid, int32_t* n_top, int32_t* n_dets) {
   if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
   if (grid) *grid = s->grid;
