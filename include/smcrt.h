@@ -513,8 +513,12 @@ int smcrt_job_info(const smcrt_job* job, smcrt_job_desc* desc);
 int smcrt_job_scene(const smcrt_job* job, smcrt_sdf_node* nodes, int32_t* top, smcrt_detector* dets);
 /* The metadata dict (the values parse_* and finalise set) as TOML text, for NRRD headers. */
 int smcrt_job_metadata(const smcrt_job* job, char* buf, int32_t cap);
-/* default_MCRT (kernelsMod.f90:14-82) without checkpoint loading: run_MCRT on `device`, then
- * finalise (:2321-2416). Writes, under outdir (the reference's fileplace):
+/* default_MCRT (kernelsMod.f90:14-82): run_MCRT on `device`, then finalise (:2321-2416).
+ * Photons run in batches of checkpoint_every_n; after each, <checkpoint_file> (relative to
+ * outdir) is rewritten with the tally of the photons done so far (writer.f90:426-457). With
+ * load_checkpoint, the checkpoint's input file (next to this one) is run for its remaining
+ * photons with iseed*101 from zeroed tallies, as the reference's second setup() leaves it.
+ * Writes, under outdir (the reference's fileplace):
  *   jmean/<fluence>, normalised;
  *   emission/<render_source_name>, normalised;
  *   absorb/absorb.nrrd;

@@ -10,10 +10,12 @@
 //   default_MCRT / finalise                                       src/kernelsMod.f90:14-82, 2321-2416
 // Host code only; part of libsmcrt.so's C ABI (include/smcrt.h).
 #include <algorithm>
+#include <cctype>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <sstream>
 #include <string>
 #include <sys/stat.h>
@@ -878,36 +880,88 @@ extern "C" {
 // then finalise's normalisation and writes (:2321-2416) under `outdir` (the reference's
 // fileplace): jmean/<fluence>, emission/<render_source_name>, absorb/absorb.nrrd,
 // detectors/detector_<i>.dat. `io` (may be NULL) receives the tallies as well.
-int smcrt_job_run(smcrt_job* J, int32_t device, const char* outdir, double* nscatt_out) {
-  if (!J || !outdir) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
-  if (J->loadckpt) return ffail(SMCRT_ERR_UNSUPPORTED, "load_checkpoint is not supported by smcrt_job_run");
+int smcrt_job_run(smcrt_job* J0, int32_t device, const char* outdir, double* nscatt_out) {
+  if (!J0 || !outdir) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  smcrt_job* J = J0;
+  std::unique_ptr<smcrt_job> ck;  // the checkpoint's job (load_checkpoint)
+  if (J0->loadckpt) {  // default_MCRT, kernelsMod.f90:51-71
+    std::ifstream f(J0->ckptfile, std::ios::binary);
+    if (!f) return ffail(SMCRT_ERR_INVALID_ARG, "cannot read checkpoint " + J0->ckptfile);
+    std::string l1, l2;
+    std::getline(f, l1);
+    std::getline(f, l2);
+    const size_t p1 = l1.find('='), p2 = l2.find('=');
+    if (p1 == std::string::npos || p2 == std::string::npos)
+      return ffail(SMCRT_ERR_INVALID_ARG, "bad checkpoint header in " + J0->ckptfile);
+    std::string tf = l1.substr(p1 + 1);
+    while (!tf.empty() && std::isspace((unsigned char)tf.back())) tf.pop_back();
+    const int64_t run_before = std::strtoll(l2.c_str() + p2 + 1, nullptr, 10);
+    // parse_params("res/"//tomlfile): the checkpoint's file, next to this job's input file
+    if (!tf.empty() && tf[0] != '/') {
+      const size_t sl = J0->toml_path.rfind('/');
+      if (sl != std::string::npos) tf = J0->toml_path.substr(0, sl + 1) + tf;
+    }
+    smcrt_job* raw = nullptr;
+    const int ls = smcrt_job_load_mode(tf.c_str(), SMCRT_JOB_DEFAULT, &raw);
+    if (ls) return ls;
+    ck.reset(raw);
+    J = raw;
+    // The reference reads the checkpoint's jmean, then its second setup() reallocates and
+    // zeroes the tallies (setup.f90:28-30, 154-185), so the run restarts from zero with
+    // the remaining photons and a new seed; that is kept here.
+    J->iseed = J->iseed * 101;
+    J->nphotons = J->nphotons - run_before;
+    if (J->nphotons < 0) return ffail(SMCRT_ERR_INVALID_ARG, "checkpoint has more photons than the job");
+  }
   smcrt_scene* scene = nullptr;
   int st = smcrt_scene_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(),
                               &J->grid, J->dets.empty() ? nullptr : J->dets.data(), (int32_t)J->dets.size(), device,
                               &scene);
   if (st) return st;
   const size_t nv = (size_t)J->grid.nx * J->grid.ny * J->grid.nz;
-  std::vector<float> jmean(nv, 0.f), absorb(nv, 0.f), emission(nv, 0.f);
+  std::vector<double> jm(nv, 0.0), ab(nv, 0.0), em(nv, 0.0);
   int64_t nb = 0;
   smcrt_scene_det_bins(scene, &nb);
   std::vector<double> det_bins((size_t)std::max<int64_t>(1, nb), 0.0);
   double nscatt = 0.0;
   smcrt_tallies io;
   std::memset(&io, 0, sizeof(io));
-  io.jmean = jmean.data(); io.absorb = absorb.data(); io.emission = emission.data();
+  io.jmean_f64 = jm.data(); io.absorb_f64 = ab.data(); io.emission_f64 = em.data();
   io.det_bins = det_bins.data(); io.nscatt = &nscatt;
   smcrt_run_config cfg;
   std::memset(&cfg, 0, sizeof(cfg));
-  cfg.n_photons = (uint64_t)J->nphotons;
-  cfg.first_photon = 0;
   cfg.seed = (uint64_t)J->iseed;
   cfg.flags = SMCRT_FLAG_PATHLENGTH | (J->render_source ? SMCRT_FLAG_RENDER_SOURCE : 0);
-  st = smcrt_run(scene, &J->src, &cfg, &io);
+  // checkpoint every checkpoint_every_n photons (run_MCRT, kernelsMod.f90:1865): the GPU
+  // runs batches of that size; after each, photons [0, j) are complete and jmean holds
+  // exactly their tally, written with the reference's checkpoint layout (writer.f90:426-457)
+  const int64_t every = J->ckptfreq > 0 ? J->ckptfreq : J->nphotons;
+  std::vector<float> tmp;
+  for (int64_t done = 0; done < J->nphotons && !st;) {
+    const int64_t n = std::min<int64_t>(every, J->nphotons - done);
+    cfg.n_photons = (uint64_t)n;
+    cfg.first_photon = (uint64_t)done;
+    st = smcrt_run(scene, &J->src, &cfg, &io);
+    done += n;
+    if (!st && done % every == 0 && J->ckptfreq > 0) {
+      tmp.resize(nv);
+      for (size_t i = 0; i < nv; ++i) tmp[i] = (float)jm[i];
+      const size_t sl = J->toml_path.rfind('/');
+      const std::string tname = sl == std::string::npos ? J->toml_path : J->toml_path.substr(sl + 1);
+      std::string cpath = J->ckptfile;
+      if (!cpath.empty() && cpath[0] != '/') cpath = std::string(outdir) + "/" + cpath;
+      if (!mkdirs(outdir)) st = ffail(SMCRT_ERR_INVALID_ARG, std::string("cannot create ") + outdir);
+      else st = smcrt_write_checkpoint(cpath.c_str(), tname.c_str(), done, tmp.data(), &J->grid, 1, nullptr, 0);
+    }
+  }
   smcrt_scene_destroy(scene);
   if (st) return st;
   if (nscatt_out) *nscatt_out = nscatt;
+  std::vector<float> jmean(nv), absorb(nv), emission(nv);
+  for (size_t i = 0; i < nv; ++i) {
+    jmean[i] = (float)jm[i]; absorb[i] = (float)ab[i]; emission[i] = (float)em[i];
+  }
   return finalise_writes(J, outdir, jmean, absorb, emission, det_bins);
-  return SMCRT_OK;
 }
 
 int smcrt_job_escape_config(const smcrt_job* J, smcrt_escape_config* out) {

@@ -200,7 +200,9 @@ def test_job_run_scat_test(tmp_path, kats):
     d = j.desc
     with Engine(builders.setup_scat_test(10.0), d.grid) as eng:
         r = eng.run(d.source, d.n_photons, seed=d.seed)
-    assert np.array_equal(output.normalise_fluence(r.jmean.astype(np.float32), d.grid, d.n_photons), data)
+    # (the job runs checkpoint_every_n-photon batches: fp64 sums in another order)
+    np.testing.assert_allclose(output.normalise_fluence(r.jmean.astype(np.float32), d.grid, d.n_photons), data,
+                               rtol=1e-6, atol=0)
 
 
 # ------------------------- the escape / inverse build variants --------
@@ -310,3 +312,41 @@ def test_job_run_inverse(tmp_path):
     assert np.all(g[:, 4] == g[0, 4]) and g[0, 4] < 0
     t = j.run_inverse(apply_trial=True)
     assert np.array_equal(t[:, :4], g[:, :4]) and len(set(t[:, 4])) > 1
+
+
+@pytest.mark.gpu
+def test_job_checkpoint_write_and_resume(tmp_path):
+    """run_MCRT's checkpoints (kernelsMod.f90:1865, writer.f90:426-457) hold exactly the
+    tally of photons [0, j); default_MCRT's load_checkpoint (:51-71) reruns the remaining
+    photons with iseed*101 from zeroed tallies (the reference's second setup() zeroes them)."""
+    from rsmcrt_amd import output
+    from rsmcrt_amd.engine import Engine
+    base = open(res("scat_test.toml")).read()
+    t1 = base.replace("nphotons = 100000", "nphotons = 30000").replace("checkpoint_every_n=10000",
+                                                                       "checkpoint_every_n=20000")
+    assert t1 != base
+    (tmp_path / "ck.toml").write_text(t1)
+    out = tmp_path / "run1"
+    j = Job(str(tmp_path / "ck.toml"))
+    j.run(out)
+    raw = (out / "check.ckpt").read_bytes()
+    hdr = b"tomlfile=ck.toml\nphotons_run=20000\n"
+    assert raw.startswith(hdr)
+    ck = np.frombuffer(raw[len(hdr):], dtype=np.float32)
+    d = j.desc
+    with Engine(builders.setup_scat_test(10.0), d.grid) as eng:
+        r = eng.run(d.source, 20000, seed=d.seed)
+    np.testing.assert_allclose(ck, r.jmean.astype(np.float32).reshape(-1), rtol=1e-6, atol=0)
+    # resume: load_checkpoint = true, pointing at that file
+    t2 = t1.replace("load_checkpoint=false", "load_checkpoint=true").replace(
+        'checkpoint_file="check.ckpt"', f'checkpoint_file="{out / "check.ckpt"}"')
+    assert "load_checkpoint=true" in t2
+    (tmp_path / "resume.toml").write_text(t2)
+    out2 = tmp_path / "run2"
+    Job(str(tmp_path / "resume.toml")).run(out2)
+    from tests.test_writers import read_nrrd_like_reference
+    data, _ = read_nrrd_like_reference(out2 / "jmean" / "fluence.nrrd")
+    with Engine(builders.setup_scat_test(10.0), d.grid) as eng:
+        r2 = eng.run(d.source, 10000, seed=d.seed * 101)
+    np.testing.assert_allclose(output.normalise_fluence(r2.jmean.astype(np.float32), d.grid, 10000), data,
+                               rtol=1e-6, atol=0)
