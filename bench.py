@@ -95,18 +95,19 @@ def cpu_baseline(sc, g, src, seconds, eng, threads):
                                       "photons_compared": n}
 
 
-def pmc_traffic(batch, grid, steps_kernel="transport_kernel<true>"):
-    """HBM bytes per transport launch from the committed rocprofv3 PMC summary of this
-    exact configuration (tools/profile.sh -> profiles/transport_traffic.json), else None."""
+def pmc_summary(batch, grid):
+    """Per-launch PMC values of the transport kernel (HBM bytes, VALU/SALU instructions)
+    from the committed rocprofv3 summary of this exact configuration (tools/profile.sh +
+    tools/prof_summary.py -> profiles/transport_traffic.json), else {}."""
     p = os.path.join(ROOT, "profiles", "transport_traffic.json")
     try:
         with open(p) as f:
             t = json.load(f)
     except (OSError, ValueError):
-        return None, None
+        return {}
     if t.get("batch") != batch or t.get("grid") != grid:
-        return None, None
-    return t.get("hbm_bytes_per_launch"), t.get("source")
+        return {}
+    return t
 
 
 def main():
@@ -203,7 +204,18 @@ def main():
         # §8(d): the reference's fp32 read+write per atomic; here one 8-B deposit record)
         alg_bytes = 8.0 * dep_per_launch
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(B, args.grid)
+        pmc = pmc_summary(B, args.grid)
+        traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), pmc.get("source")
+        # The kernel's binding resource is VALU issue: wave-instructions per launch (PMC
+        # SQ_INSTS_VALU of the same command) / the live launch time, against the chip's issue
+        # peak of one wave64 VALU instruction per 4 cycles per SIMD (1024 SIMDs, 2.4 GHz).
+        valu_peak = 1024 * 2.4e9 / 4 / 1e9
+        valu = None
+        if pmc.get("valu_insts_per_launch"):
+            va = pmc["valu_insts_per_launch"] / (kern_ms * 1e-3) / 1e9
+            valu = {"bound": "valu", "achieved": va, "peak": valu_peak, "unit": "G wave-instr/s", "frac": va / valu_peak,
+                    "valu_insts_per_launch": pmc["valu_insts_per_launch"],
+                    "salu_insts_per_launch": pmc.get("salu_insts_per_launch"), "source": traffic_src}
         out = {
             "metric": "photon packets/sec (128^3 jmean grid, path-length deposition)",
             "value": photons / elapsed,
@@ -231,6 +243,7 @@ def main():
                          "deposit_fold_ms_per_launch": dep_ms,
                          "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) / world / launches,
                          "binding_resource": "fp64 VALU issue + divergence (see DESIGN.md), not HBM"},
+            "valu_roofline": valu,
             "cpu_baseline": None,
         }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -88,6 +88,8 @@ def main():
             with open(a.traffic, "w") as f:
                 json.dump({"batch": a.batch, "grid": a.grid, "kernel": k,
                            "hbm_bytes_per_launch": out[k]["hbm_bytes_per_dispatch"],
+                           "valu_insts_per_launch": out[k].get("SQ_INSTS_VALU"),
+                           "salu_insts_per_launch": out[k].get("SQ_INSTS_SALU"),
                            "avg_ms": out[k]["avg_ms_last"], "source": os.path.relpath(a.dir)}, f, indent=1)
     if a.json:
         with open(a.json, "w") as f:
