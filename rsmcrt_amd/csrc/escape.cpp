@@ -10,7 +10,9 @@
 // operation for operation (fp64 arithmetic on fp32 escapeSymmetry values, fp32 results).
 #include <cmath>
 #include <cstring>
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/smcrt.h"
@@ -446,9 +448,14 @@ int smcrt_escape_map(const smcrt_escape_config* cfg, const smcrt_grid* g, int32_
   if (g->nx < 1 || g->ny < 1 || g->nz < 1) return set_error(SMCRT_ERR_INVALID_ARG, "bad grid");
   if (n_dets == 0) return SMCRT_OK;
   const SymArr E{escape_sym, n_dets, S.n0, S.n1};
+  // every fluence cell is independent: z-slabs on host threads (results do not depend on
+  // the split)
+  unsigned nt = std::thread::hardware_concurrency();
+  nt = std::max(1u, std::min({nt, 16u, (unsigned)g->nz}));
+  auto slab = [&](int32_t o0, int32_t o1) {
   for (int32_t m = 1; m <= g->nx; ++m)
     for (int32_t n = 1; n <= g->ny; ++n)
-      for (int32_t o = 1; o <= g->nz; ++o) {
+      for (int32_t o = o0; o < o1; ++o) {
         // fluence-grid cell centre taken onto the symmetry grid, :681-696 / 1118-1128
         const double y = ((((double)n - 0.5) / g->ny) * 2.0 * g->ymax) - g->ymax;
         const double x = ((((double)m - 0.5) / g->nx) * 2.0 * g->xmax) - g->xmax;
@@ -460,6 +467,14 @@ int smcrt_escape_map(const smcrt_escape_config* cfg, const smcrt_grid* g, int32_
         if (is_cyl(S.kind)) map_cyl(S, E, p, out);
         else map_cart(S, E, p, out);
       }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) {
+    const int32_t o0 = 1 + (int32_t)((int64_t)g->nz * t / nt), o1 = 1 + (int32_t)((int64_t)g->nz * (t + 1) / nt);
+    if (t + 1 == nt) slab(o0, o1);
+    else th.emplace_back(slab, o0, o1);
+  }
+  for (auto& x : th) x.join();
   return SMCRT_OK;
 }
 
