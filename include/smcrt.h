@@ -435,8 +435,10 @@ int smcrt_scene_get_optprops(const smcrt_scene* scene, int32_t top_index, int32_
  * steps: max_steps*5 doubles, gradDescentData(maxNumSteps, 5) in Fortran order: guesses of
  * mus, mua, g, n then the error of step i at steps[(c-1)*max_steps + (i-1)]. run->n_photons
  * photons per step, each step from photon first_photon (the reference reseeds every
- * run_MCRT). The layer's original properties are restored at the end. io (may be NULL)
- * accumulates the tallies of all steps. */
+ * run_MCRT). The layer's original properties are restored at the end. A step whose
+ * properties repeat an earlier step's bits reuses that step's error (runs are deterministic),
+ * so the reference's mode costs two runs. io (may be NULL) accumulates the tallies of the
+ * steps actually run. */
 int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_inverse_config* cfg,
                       const smcrt_run_config* run, const double* targets, double* steps, smcrt_tallies* io);
 

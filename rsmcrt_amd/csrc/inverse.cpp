@@ -83,6 +83,16 @@ int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_i
   int64_t nb = 0;
   if ((st = smcrt_scene_det_bins(scene, &nb))) return st;
   int changed = 0;
+  // A step is a deterministic function of the layer's properties (every run restarts the
+  // same photon streams, :1850): a step whose properties repeat an earlier step's bits has
+  // that step's error. In the reference's own mode every step after the first reruns one
+  // scene (:1630-1631), so this turns maxNumSteps runs into two.
+  struct Memo {
+    double p[4];
+    double err;
+  };
+  std::vector<Memo> memo;
+  double cur[4] = {orig[0], orig[1], orig[2], orig[3]};  // the properties the scene holds
   for (int64_t i = 1; i <= M && !st; ++i) {
     if (i >= 2) (void)R.next();  // ran = ran2(): always <= 1, the explore branch (:1620-1622)
     double* row = steps;
@@ -90,15 +100,27 @@ int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_i
     row[(1) * M + (i - 1)] = fmua ? R.next() * (muau - mual) + mual : mua;
     row[(2) * M + (i - 1)] = fg ? R.next() * (gu - gl) + gl : hgg;
     row[(3) * M + (i - 1)] = fn ? R.next() * (nu - nl) + nl : n;
+    double want[4] = {cur[0], cur[1], cur[2], cur[3]};
     if (apply) {
-      st = smcrt_scene_set_optprops(scene, idx, row[i - 1], row[M + i - 1], row[2 * M + i - 1], row[3 * M + i - 1]);
-      changed = 1;
-    } else if (i >= 2 && !changed) {
+      want[0] = row[i - 1]; want[1] = row[M + i - 1]; want[2] = row[2 * M + i - 1]; want[3] = row[3 * M + i - 1];
+    } else if (i >= 2) {
       // trialOptProp = mono(mus, mua, hgg, n) from the original getters (:1630-1631)
-      st = smcrt_scene_set_optprops(scene, idx, mus, mua, hgg, n);
+      want[0] = mus; want[1] = mua; want[2] = hgg; want[3] = n;
+    }
+    bool hit = false;
+    for (const Memo& m : memo)
+      if (std::memcmp(m.p, want, sizeof want) == 0) {
+        row[4 * M + (i - 1)] = m.err;
+        hit = true;
+        break;
+      }
+    if (hit) continue;
+    if (std::memcmp(want, cur, sizeof cur) != 0) {
+      st = smcrt_scene_set_optprops(scene, idx, want[0], want[1], want[2], want[3]);
+      if (st) break;
+      std::memcpy(cur, want, sizeof cur);
       changed = 1;
     }
-    if (st) break;
     bins.assign((size_t)std::max<int64_t>(nb, 1), 0.0);
     smcrt_tallies t;
     if (io) t = *io;
@@ -125,6 +147,10 @@ int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_i
     }
     if (st) break;
     row[4 * M + (i - 1)] = -err / counter;
+    Memo m;
+    std::memcpy(m.p, cur, sizeof cur);
+    m.err = row[4 * M + (i - 1)];
+    memo.push_back(m);
   }
   if (changed) {  // restore the layer
     const int rst = smcrt_scene_set_optprops(scene, idx, orig[0], orig[1], orig[2], orig[3]);
