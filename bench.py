@@ -122,6 +122,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share, <= 16")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
+    ap.add_argument("--sync-fold", action="store_true", help="diagnostic: each step waits for its own fold")
     ap.add_argument("--source", default="point", choices=["point", "uniform"],
                     help="diagnostic: uniform = parallelogram source over the z=0.99 plane")
     args = ap.parse_args()
@@ -148,6 +149,10 @@ def main():
         from rsmcrt_amd import scene as _scene
         src = _scene.uniform_source((-1.0, -1.0, 0.99), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
     run_flags = 0 if args.no_deposit else abi.FLAG_PATHLENGTH
+    if not args.sync_fold:
+        # the deposit fold of step k runs beside step k+1's transport kernel; the fence
+        # before the reduce makes jmean complete inside the timed region
+        run_flags |= abi.FLAG_ASYNC_FOLD
     eng = Engine(sc, g, device=torch.cuda.current_device())
     nv = g.nx * g.ny * g.nz
     jmean = torch.zeros(nv, dtype=torch.float64, device=dev)
@@ -166,6 +171,7 @@ def main():
 
     for s in range(args.warmup):
         step(s)
+    eng.fence(stream.cuda_stream)
     torch.cuda.synchronize()
     eng.set_timing(True)
     eng.kernel_times()  # reset
@@ -178,6 +184,7 @@ def main():
     t0 = time.perf_counter()
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
+    eng.fence(stream.cuda_stream)
     if world > 1:
         shard.reduce_tallies((jmean, absorb, nscatt, counters), dist)
     torch.cuda.synchronize()

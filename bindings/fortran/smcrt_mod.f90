@@ -31,7 +31,7 @@ module smcrt_mod
     ! run flags
     integer(c_int32_t), parameter :: SMCRT_FLAG_PATHLENGTH = 1, SMCRT_FLAG_SURVIVAL_BIAS = 2, &
         SMCRT_FLAG_RENDER_SOURCE = 4, SMCRT_FLAG_TEST_KERNEL = 8, SMCRT_FLAG_END_EARLY = 16, &
-        SMCRT_FLAG_RECORD_PHOTONS = 32
+        SMCRT_FLAG_RECORD_PHOTONS = 32, SMCRT_FLAG_ASYNC_FOLD = 64
     integer, parameter :: SMCRT_NCOUNTERS = 16
     ! smcrt_symmetry (escape function, kernelsMod.f90:85-1460)
     integer(c_int32_t), parameter :: SMCRT_SYM_NONE = 0, SMCRT_SYM_PRISM = 1, SMCRT_SYM_FLIPPED = 2, &

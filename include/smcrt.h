@@ -199,7 +199,9 @@ enum {
   SMCRT_FLAG_TEST_KERNEL = 1u << 3,   /* test_kernel semantics (kernelsMod.f90:2069-2182): no re-emission,
                                          initial layer mask ds<=0, scatter-order moments */
   SMCRT_FLAG_END_EARLY = 1u << 4,     /* test_kernel end_early: stop after the 4th scatter */
-  SMCRT_FLAG_RECORD_PHOTONS = 1u << 5 /* fill smcrt_tallies.records (debug/parity) */
+  SMCRT_FLAG_RECORD_PHOTONS = 1u << 5, /* fill smcrt_tallies.records (debug/parity) */
+  SMCRT_FLAG_ASYNC_FOLD = 1u << 6      /* smcrt_run_device: the jmean fold may finish after later work
+                                          on the stream; jmean is complete after smcrt_scene_fence */
 };
 
 typedef struct smcrt_run_config {
@@ -333,6 +335,11 @@ int smcrt_run_origins(smcrt_scene* scene, const smcrt_source* src, const double*
  * its kappa (0 when outside), evaluated on the scene's device: the launch-cell test of the
  * escape function (kernelsMod.f90:589-603). `kappa` may be NULL. */
 int smcrt_scene_classify(smcrt_scene* scene, const double* points, int64_t n, int32_t* layer, double* kappa);
+
+/* Make `stream` wait for every deposit fold in flight (SMCRT_FLAG_ASYNC_FOLD launches): jmean
+ * is complete in `stream` order after this call. The fold of one launch then runs beside
+ * the next launch's transport kernel (two record-log slots). */
+int smcrt_scene_fence(smcrt_scene* scene, void* stream);
 
 /* Per-kernel device time (ms) of the launches made since the previous query, from HIP
  * events recorded on the launch stream around each kernel group while timing is enabled

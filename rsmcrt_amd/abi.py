@@ -55,6 +55,7 @@ FLAG_RENDER_SOURCE = 1 << 2
 FLAG_TEST_KERNEL = 1 << 3
 FLAG_END_EARLY = 1 << 4
 FLAG_RECORD_PHOTONS = 1 << 5
+FLAG_ASYNC_FOLD = 1 << 6
 
 # counters
 COUNTER_NAMES = [
@@ -193,5 +194,5 @@ EXPORTED_SYMBOLS = [
     "smcrt_scene_info", "smcrt_run_origins", "smcrt_scene_classify", "smcrt_escape_sym_dims", "smcrt_escape_cells",
     "smcrt_escape_map", "smcrt_escape_run", "smcrt_scene_get_optprops", "smcrt_inverse_run", "smcrt_job_load_mode",
     "smcrt_job_escape_config", "smcrt_job_inverse_config", "smcrt_job_targets", "smcrt_job_run_escape",
-    "smcrt_job_run_inverse",
+    "smcrt_job_run_inverse", "smcrt_scene_fence",
 ]

@@ -681,24 +681,31 @@ struct smcrt_scene {
   uint32_t hist_tiles = 0;  // fused tile histogram in the transport kernel (0: bin_hist kernel)
   // binned jmean deposition (deposit.h)
   uint32_t n_tiles = 0;
-  unsigned long long* d_pool = nullptr;    // record log, cap records
-  unsigned long long* d_sorted = nullptr;  // tile-sorted records
-  uint32_t* d_chunk_fill = nullptr;
-  uint32_t* d_dep_ctl = nullptr;      // [0] chunks taken [1] overflow [2] pieces [3] records
+  // Two record-log slots, used by alternate launches: the fold of launch k (on fstream)
+  // reads its slot while launch k+1's transport kernel fills the other.
+  unsigned long long* d_pool[2] = {nullptr, nullptr};  // record log, cap records
+  unsigned long long* d_sorted = nullptr;  // tile-sorted records (folds are serial on fstream)
+  uint32_t* d_chunk_fill[2] = {nullptr, nullptr};
+  uint32_t* d_dep_ctl[2] = {nullptr, nullptr};  // [0] chunks taken [1] overflow [2] pieces [3] records
   uint32_t* d_tile_count = nullptr;  // n_tiles
   uint32_t* d_tile_start = nullptr;  // n_tiles
-  uint32_t* d_bin_counts = nullptr;  // [n_tiles][BIN_BLOCKS]
+  uint32_t* d_bin_counts[2] = {nullptr, nullptr};  // [n_tiles][BIN_BLOCKS]
+  hipStream_t fstream = nullptr;  // the deposit folds
+  hipEvent_t ev_t = nullptr;      // a transport launch finished (fstream waits on it)
+  hipEvent_t ev_f[2] = {nullptr, nullptr};  // the fold of slot i finished
+  bool f_pending[2] = {false, false};
+  int slot = 0, last_slot = -1;
   size_t scatter_lds = 0;
   Piece* d_pieces = nullptr;
   uint64_t pool_chunks = 0, max_pieces = 0;
   double rpp_est = 1024.0;           // deposit records per photon, refined from past launches
   bool rpp_measured = false;
-  uint32_t* h_ctl = nullptr;         // pinned copy of dep_ctl of the last launch
-  hipEvent_t ctl_ev = nullptr;
-  bool ctl_pending = false;
+  uint32_t* h_ctl = nullptr;         // pinned copies of dep_ctl, 8 words per slot ([4] = photons)
+  hipEvent_t ctl_ev[2] = {nullptr, nullptr};
+  bool ctl_pending[2] = {false, false};
   bool force_atomic = false;  // SMCRT_DEPOSIT=atomic
-  // smcrt_scene_kernel_times: event triples (before transport, after transport, after
-  // the deposit fold) of the launches since the last harvest
+  // smcrt_scene_kernel_times: event quads (before / after transport on the launch stream,
+  // before / after the deposit fold on fstream) of the launches since the last harvest
   bool timing = false;
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
@@ -721,12 +728,13 @@ constexpr uint64_t CALIB_PHOTONS = 1ull << 18;  // first binned launch of a scen
 // Fold the recorded event triples into the sums (waits for them).
 static hipError_t harvest_times(smcrt_scene* s) {
   for (size_t i = 0; i < s->tev_used; ++i) {
-    hipEvent_t* e = &s->tev[3 * i];
-    hipError_t err = hipEventSynchronize(e[2]);
+    hipEvent_t* e = &s->tev[4 * i];
+    hipError_t err = hipEventSynchronize(e[1]);
+    if (err == hipSuccess) err = hipEventSynchronize(e[3]);
     if (err != hipSuccess) return err;
     float a = 0.f, b = 0.f;
     if ((err = hipEventElapsedTime(&a, e[0], e[1])) != hipSuccess) return err;
-    if ((err = hipEventElapsedTime(&b, e[1], e[2])) != hipSuccess) return err;
+    if ((err = hipEventElapsedTime(&b, e[2], e[3])) != hipSuccess) return err;
     s->t_transport += a; s->t_deposit += b; s->t_launches += 1;
   }
   s->tev_used = 0;
@@ -777,11 +785,18 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
+  if (s->fstream) (void)hipStreamSynchronize(s->fstream);
   void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
-                  s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_dep_ctl, s->d_tile_count,
-                  s->d_tile_start, s->d_bin_counts, s->d_pieces};
-  if (s->ctl_ev) (void)hipEventDestroy(s->ctl_ev);
+                  s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1],
+                  s->d_dep_ctl[0], s->d_dep_ctl[1], s->d_tile_count, s->d_tile_start, s->d_bin_counts[0],
+                  s->d_bin_counts[1], s->d_pieces};
+  for (int i = 0; i < 2; ++i) {
+    if (s->ctl_ev[i]) (void)hipEventDestroy(s->ctl_ev[i]);
+    if (s->ev_f[i]) (void)hipEventDestroy(s->ev_f[i]);
+  }
+  if (s->ev_t) (void)hipEventDestroy(s->ev_t);
+  if (s->fstream) (void)hipStreamDestroy(s->fstream);
   for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
   if (s->h_ctl) (void)hipHostFree(s->h_ctl);
   for (void* p : ptrs)
@@ -908,18 +923,24 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     const char* fa = std::getenv("SMCRT_DEPOSIT");
     s->force_atomic = fa && std::string(fa) == "atomic";
     if (s->n_tiles) {
-      if ((st = dalloc(&s->d_dep_ctl, 4)) || (st = dalloc(&s->d_tile_count, s->n_tiles)) ||
-          (st = dalloc(&s->d_tile_start, s->n_tiles)) ||
-          (st = dalloc(&s->d_bin_counts, (size_t)s->n_tiles * BIN_BLOCKS)))
+      if ((st = dalloc(&s->d_dep_ctl[0], 4)) || (st = dalloc(&s->d_dep_ctl[1], 4)) ||
+          (st = dalloc(&s->d_tile_count, s->n_tiles)) || (st = dalloc(&s->d_tile_start, s->n_tiles)) ||
+          (st = dalloc(&s->d_bin_counts[0], (size_t)s->n_tiles * BIN_BLOCKS)) ||
+          (st = dalloc(&s->d_bin_counts[1], (size_t)s->n_tiles * BIN_BLOCKS)))
         return cleanup_fail(st);
       s->scatter_lds = scatter_lds_bytes(s->n_tiles);
       if (hipFuncSetAttribute((const void*)bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)s->scatter_lds) != hipSuccess)
         return cleanup_fail(fail(SMCRT_ERR_HIP, "bin_scatter LDS attribute"));
-      if (hipHostMalloc((void**)&s->h_ctl, 8 * sizeof(uint32_t)) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ctl_ev, hipEventDisableTiming) != hipSuccess)
-        return cleanup_fail(fail(SMCRT_ERR_HIP, "pinned/event allocation failed"));
-      std::memset(s->h_ctl, 0, 8 * sizeof(uint32_t));
+      if (hipHostMalloc((void**)&s->h_ctl, 16 * sizeof(uint32_t)) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ctl_ev[0], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ctl_ev[1], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ev_f[0], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ev_f[1], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&s->ev_t, hipEventDisableTiming) != hipSuccess ||
+          hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup_fail(fail(SMCRT_ERR_HIP, "pinned/event/stream allocation failed"));
+      std::memset(s->h_ctl, 0, 16 * sizeof(uint32_t));
     }
   }
   int per_cu = 0, cus = 0;
@@ -1003,14 +1024,26 @@ extern "C" {
 
 // Refine the records-per-photon estimate from the last binned launch, if it has landed.
 static void refine_rpp(smcrt_scene* s) {
-  if (s->ctl_pending && hipEventQuery(s->ctl_ev) == hipSuccess) {
-    s->ctl_pending = false;
-    if (s->h_ctl[4] > 0) {
-      const double rpp = (double)(s->h_ctl[3] + s->h_ctl[1]) / (double)s->h_ctl[4];
-      s->rpp_est = std::max(1.0, rpp);
-      s->rpp_measured = true;
+  for (int i = 0; i < 2; ++i) {
+    const int sl = s->last_slot < 0 ? i : (s->last_slot + 1 + i) & 1;  // the older slot first
+    if (s->ctl_pending[sl] && hipEventQuery(s->ctl_ev[sl]) == hipSuccess) {
+      s->ctl_pending[sl] = false;
+      const uint32_t* h = s->h_ctl + 8 * sl;
+      if (h[4] > 0) {
+        const double rpp = (double)(h[3] + h[1]) / (double)h[4];
+        s->rpp_est = std::max(1.0, rpp);
+        s->rpp_measured = true;
+      }
     }
   }
+}
+
+// Wait (host) for every fold in flight: before the shared fold buffers are reallocated.
+static hipError_t drain_folds(smcrt_scene* s) {
+  if (!s->fstream) return hipSuccess;
+  const hipError_t e = hipStreamSynchronize(s->fstream);
+  s->f_pending[0] = s->f_pending[1] = false;
+  return e;
 }
 
 // Records the record pool must hold for one launch of n photons.
@@ -1026,21 +1059,29 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   // grow with 25% headroom so launch-to-launch jitter of the estimate never reallocates
   // (a reallocation synchronises the device)
   chunks = std::min<uint64_t>(chunks + chunks / 4, MAX_POOL_RECORDS / CHUNK_RECORDS);
-  const void* old[] = {s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_pieces};
-  for (const void* p : old)
-    if (p) (void)hipFree((void*)p);
-  s->d_pool = s->d_sorted = nullptr; s->d_chunk_fill = nullptr; s->d_pieces = nullptr; s->pool_chunks = 0;
+  // the launches and folds in flight (on any stream) use these buffers
+  (void)hipDeviceSynchronize();
+  (void)drain_folds(s);
+  auto release = [&]() {
+    void* old[] = {s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1], s->d_pieces};
+    for (void* p : old)
+      if (p) (void)hipFree(p);
+    s->d_pool[0] = s->d_pool[1] = s->d_sorted = nullptr;
+    s->d_chunk_fill[0] = s->d_chunk_fill[1] = nullptr;
+    s->d_pieces = nullptr;
+    s->pool_chunks = 0;
+  };
+  release();
   const uint64_t cap = chunks * CHUNK_RECORDS;
   // pieces <= records / piece size + one partial piece per tile (deposit.h bin_scan)
   const uint64_t pieces = std::min<uint64_t>(cap / MIN_PIECE_RECORDS, REDUCE_PIECES + 1) + s->n_tiles + 1;
-  if (hipMalloc((void**)&s->d_pool, cap * 8) != hipSuccess || hipMalloc((void**)&s->d_sorted, cap * 8) != hipSuccess ||
-      hipMalloc((void**)&s->d_chunk_fill, chunks * 4) != hipSuccess ||
+  if (hipMalloc((void**)&s->d_pool[0], cap * 8) != hipSuccess || hipMalloc((void**)&s->d_pool[1], cap * 8) != hipSuccess ||
+      hipMalloc((void**)&s->d_sorted, cap * 8) != hipSuccess ||
+      hipMalloc((void**)&s->d_chunk_fill[0], chunks * 4) != hipSuccess ||
+      hipMalloc((void**)&s->d_chunk_fill[1], chunks * 4) != hipSuccess ||
       hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) != hipSuccess) {
     (void)hipGetLastError();
-    const void* bad[] = {s->d_pool, s->d_sorted, s->d_chunk_fill, s->d_pieces};
-    for (const void* p : bad)
-      if (p) (void)hipFree((void*)p);
-    s->d_pool = s->d_sorted = nullptr; s->d_chunk_fill = nullptr; s->d_pieces = nullptr;
+    release();
     return false;
   }
   s->pool_chunks = chunks;
@@ -1048,27 +1089,32 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   return true;
 }
 
-static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hipStream_t stream) {
+// One transport launch on `stream` into record slot `sl` (binned), then its deposit fold on
+// s->fstream, ordered after the launch by an event. The fold of the previous launch may still
+// run while this transport kernel does: they touch different slots (and jmean is only
+// written by folds, which are serial on fstream).
+static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hipStream_t stream, int sl) {
+  const bool binned = K.rec_pool != nullptr;
+  if (binned && s->f_pending[sl]) HIPCHK(hipStreamWaitEvent(stream, s->ev_f[sl], 0));  // slot free
   HIPCHK(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), stream));
   // this launch's cold parameters: a ring slot, written in stream order before the kernel
   KCold* C = s->d_cold + (s->cold_seq++ % COLD_SLOTS);
   HIPCHK(hipMemcpyAsync(C, &Ch, sizeof(KCold), hipMemcpyHostToDevice, stream));
-  const bool binned = K.rec_pool != nullptr;
   if (binned) {
-    HIPCHK(hipMemsetAsync(s->d_dep_ctl, 0, 4 * sizeof(uint32_t), stream));
+    HIPCHK(hipMemsetAsync(s->d_dep_ctl[sl], 0, 4 * sizeof(uint32_t), stream));
     if (K.hist_tiles)
-      HIPCHK(hipMemsetAsync(s->d_bin_counts, 0, (size_t)s->n_tiles * BIN_BLOCKS * sizeof(uint32_t), stream));
+      HIPCHK(hipMemsetAsync(s->d_bin_counts[sl], 0, (size_t)s->n_tiles * BIN_BLOCKS * sizeof(uint32_t), stream));
   }
   hipEvent_t* ev = nullptr;
   if (s->timing) {
     if (s->tev_used == MAX_TIMED) HIPCHK(harvest_times(s));
-    if (3 * (s->tev_used + 1) > s->tev.size())
-      for (int i = 0; i < 3; ++i) {
+    if (4 * (s->tev_used + 1) > s->tev.size())
+      for (int i = 0; i < 4; ++i) {
         hipEvent_t e;
         HIPCHK(hipEventCreate(&e));
         s->tev.push_back(e);
       }
-    ev = &s->tev[3 * s->tev_used++];
+    ev = &s->tev[4 * s->tev_used++];
     HIPCHK(hipEventRecord(ev[0], stream));
   }
   const uint64_t waves_needed = (Ch.n_photons + 63) / 64;
@@ -1087,27 +1133,37 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
   if (binned) {
+    hipStream_t fs = s->fstream;
+    HIPCHK(hipEventRecord(s->ev_t, stream));
+    HIPCHK(hipStreamWaitEvent(fs, s->ev_t, 0));
+    if (ev) HIPCHK(hipEventRecord(ev[2], fs));
     const uint32_t nch = (uint32_t)s->pool_chunks;
     const uint64_t nv = (uint64_t)s->grid.nx * s->grid.ny * s->grid.nz;
     if (!K.hist_tiles)  // else the transport kernel built the counts
-      hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, stream, s->d_pool, s->d_chunk_fill,
-                         s->d_dep_ctl, nch, s->n_tiles, s->d_bin_counts);
-    hipLaunchKernelGGL(bin_rowscan, dim3(s->n_tiles), dim3(BIN_BLOCKS), 0, stream, s->d_bin_counts,
+      hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_pool[sl], s->d_chunk_fill[sl],
+                         s->d_dep_ctl[sl], nch, s->n_tiles, s->d_bin_counts[sl]);
+    hipLaunchKernelGGL(bin_rowscan, dim3(s->n_tiles), dim3(BIN_BLOCKS), 0, fs, s->d_bin_counts[sl],
                        s->d_tile_count);
-    hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, stream, s->d_tile_count, s->n_tiles, s->d_tile_start,
-                       s->d_pieces, s->d_dep_ctl);
-    hipLaunchKernelGGL(bin_scatter, dim3(BIN_BLOCKS), dim3(BIN_THREADS), s->scatter_lds, stream, s->d_pool,
-                       s->d_chunk_fill, s->d_dep_ctl, nch, s->n_tiles, s->d_tile_start, s->d_bin_counts,
+    hipLaunchKernelGGL(bin_scan, dim3(1), dim3(1024), 0, fs, s->d_tile_count, s->n_tiles, s->d_tile_start,
+                       s->d_pieces, s->d_dep_ctl[sl]);
+    hipLaunchKernelGGL(bin_scatter, dim3(BIN_BLOCKS), dim3(BIN_THREADS), s->scatter_lds, fs, s->d_pool[sl],
+                       s->d_chunk_fill[sl], s->d_dep_ctl[sl], nch, s->n_tiles, s->d_tile_start, s->d_bin_counts[sl],
                        s->d_sorted, (uint64_t)s->pool_chunks * CHUNK_RECORDS);
-    hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, stream, s->d_sorted, s->d_pieces, s->d_dep_ctl, nv,
+    hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, fs, s->d_sorted, s->d_pieces, s->d_dep_ctl[sl], nv,
                        Ch.jmean);
     HIPCHK(hipGetLastError());
     // remember how many records this launch produced (read back lazily, never waited for)
-    HIPCHK(hipMemcpyAsync(s->h_ctl, s->d_dep_ctl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipEventRecord(s->ctl_ev, stream));
-    s->ctl_pending = true;
+    HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl, s->d_dep_ctl[sl], 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
+    HIPCHK(hipEventRecord(s->ctl_ev[sl], fs));
+    s->ctl_pending[sl] = true;
+    if (ev) HIPCHK(hipEventRecord(ev[3], fs));
+    HIPCHK(hipEventRecord(s->ev_f[sl], fs));
+    s->f_pending[sl] = true;
+    s->last_slot = sl;
+  } else if (ev) {  // no fold: an empty interval
+    HIPCHK(hipEventRecord(ev[2], stream));
+    HIPCHK(hipEventRecord(ev[3], stream));
   }
-  if (ev) HIPCHK(hipEventRecord(ev[2], stream));
 #ifdef SMCRT_DIAG
   {
     unsigned long long h[72];
@@ -1211,7 +1267,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.key0 = (uint32_t)cfg->seed;
   K.key1 = (uint32_t)(cfg->seed >> 32);
   Ch.jmean = dt.jmean; Ch.absorb = dt.absorb; Ch.emission = dt.emission;
-  Ch.chunk_fill = s->d_chunk_fill; Ch.dep_ctl = s->d_dep_ctl; Ch.bin_counts = s->d_bin_counts;
+  Ch.chunk_fill = nullptr; Ch.dep_ctl = nullptr; Ch.bin_counts = nullptr;  // (per slot, below)
   Ch.det_bins = dt.det_bins; Ch.nscatt = dt.nscatt; Ch.moments = dt.moments;
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = s->d_queue;
@@ -1236,8 +1292,10 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
         const double usable = (double)(s->pool_chunks * CHUNK_RECORDS) - (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
         n = std::min<uint64_t>(n, (uint64_t)std::max(65536.0, usable / (s->rpp_est * POOL_SLACK)));
         // (taken after ensure_pool: it may have reallocated the pool)
-        K.rec_pool = s->d_pool;
-        Ch.chunk_fill = s->d_chunk_fill;  // (ensure_pool may have reallocated them)
+        K.rec_pool = s->d_pool[s->slot];
+        Ch.chunk_fill = s->d_chunk_fill[s->slot];  // (ensure_pool may have reallocated them)
+        Ch.dep_ctl = s->d_dep_ctl[s->slot];
+        Ch.bin_counts = s->d_bin_counts[s->slot];
         K.n_chunks = (uint32_t)s->pool_chunks;
         K.hist_tiles = s->hist_tiles;
       }
@@ -1245,16 +1303,24 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
     Ch.n_photons = n;
     Ch.first_photon = orun ? done : cfg->first_photon + done;  // (origins: the global queue index)
     Ch.records = dt.records ? dt.records + done : nullptr;
-    if (K.rec_pool) s->h_ctl[4] = 0;
-    int st = launch_one(s, K, Ch, xsrc, stream);
+    const int sl = s->slot;
+    if (K.rec_pool) {
+      // (the slot's previous readback must land before its photon count is replaced)
+      if (s->ctl_pending[sl]) { HIPCHK(hipEventSynchronize(s->ctl_ev[sl])); refine_rpp(s); }
+      s->h_ctl[8 * sl + 4] = (uint32_t)std::min<uint64_t>(n, 0xFFFFFFFFull);
+    }
+    int st = launch_one(s, K, Ch, xsrc, stream, sl);
     if (st) return st;
-    if (K.rec_pool) s->h_ctl[4] = (uint32_t)std::min<uint64_t>(n, 0xFFFFFFFFull);
+    if (K.rec_pool) s->slot ^= 1;
     if (calibrate && K.rec_pool) {
-      HIPCHK(hipEventSynchronize(s->ctl_ev));
+      HIPCHK(hipEventSynchronize(s->ctl_ev[sl]));
       refine_rpp(s);
     }
     done += n;
   }
+  // the tallies are complete in `stream` order at return, unless the caller defers the folds
+  if (!(cfg->flags & SMCRT_FLAG_ASYNC_FOLD) && s->last_slot >= 0 && s->f_pending[s->last_slot])
+    HIPCHK(hipStreamWaitEvent(stream, s->ev_f[s->last_slot], 0));
   return SMCRT_OK;
 }
 
@@ -1434,6 +1500,16 @@ int smcrt_scene_classify(smcrt_scene* s, const double* points, int64_t n, int32_
   if (d_pts) (void)hipFree(d_pts);
   if (d_lay) (void)hipFree(d_lay);
   return st;
+}
+
+int smcrt_scene_fence(smcrt_scene* s, void* stream) {
+  g_last_error.clear();
+  if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  if (s->last_slot >= 0 && s->f_pending[s->last_slot])  // folds are serial: the last covers all
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->ev_f[s->last_slot], 0));
+  return SMCRT_OK;
 }
 
 int smcrt_scene_set_timing(smcrt_scene* s, int32_t enable) {

@@ -53,6 +53,7 @@ def load_library(path: str = LIB_PATH):
         L.smcrt_run_device.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.RunConfig),
                                        C.POINTER(abi.DeviceTallies), C.c_void_p]
         L.smcrt_scene_set_timing.argtypes = [C.c_void_p, C.c_int32]
+        L.smcrt_scene_fence.argtypes = [C.c_void_p, C.c_void_p]
         L.smcrt_scene_kernel_times.argtypes = [C.c_void_p, C.POINTER(abi.KernelTimes)]
         L.smcrt_normalise_fluence.argtypes = [C.POINTER(C.c_float), C.POINTER(abi.Grid), C.c_uint64]
         L.smcrt_scene_info.argtypes = [C.c_void_p, C.POINTER(abi.Grid), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -209,6 +210,10 @@ class Engine:
         """Asynchronous launch into caller-owned device buffers on `stream` (hipStream_t)."""
         _check(load_library().smcrt_run_device(self._h, C.byref(source), C.byref(cfg), C.byref(dev),
                                                C.c_void_p(stream)))
+
+    def fence(self, stream: int = 0):
+        """Make `stream` wait for the deposit folds of FLAG_ASYNC_FOLD launches."""
+        _check(load_library().smcrt_scene_fence(self._h, C.c_void_p(stream)))
 
     def set_timing(self, enable: bool = True):
         """Record HIP events around each kernel group of later launches."""

@@ -421,3 +421,33 @@ def test_general_emitter_with_detectors():
     gpu, cpu = both(sc, g, src, 3000, dets=dets)
     compare(gpu, cpu)
     assert cpu.counter("detector_hits") > 0
+
+
+def test_async_fold_pipeline():
+    """FLAG_ASYNC_FOLD launches on a caller stream (the bench's mode: the fold of launch k runs
+    beside launch k+1's transport kernel in the other record slot) + a fence give the same
+    tallies as one synchronous run of the same photons."""
+    import torch
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(64, 64, 64, 1, 1, 1)
+    src = scene.point_source()
+    nv = 64 ** 3
+    dev = torch.device("cuda", 0)
+    jm = torch.zeros(nv, dtype=torch.float64, device=dev)
+    ab = torch.zeros(nv, dtype=torch.float64, device=dev)
+    ctr = torch.zeros(abi.NCOUNTERS, dtype=torch.int64, device=dev)
+    dt = abi.DeviceTallies()
+    dt.jmean, dt.absorb, dt.counters = jm.data_ptr(), ab.data_ptr(), ctr.data_ptr()
+    stream = torch.cuda.current_stream()
+    n, k = 300_000, 5
+    with Engine(sc, g) as eng:
+        for i in range(k):
+            eng.run_device(src, Engine.config(n, seed=SEED, flags=abi.FLAG_PATHLENGTH | abi.FLAG_ASYNC_FOLD,
+                                              first_photon=i * n), dt, stream.cuda_stream)
+        eng.fence(stream.cuda_stream)
+        torch.cuda.synchronize()
+        ref = eng.run(src, n * k, seed=SEED)
+    np.testing.assert_allclose(jm.cpu().numpy().reshape(64, 64, 64), ref.jmean, rtol=1e-10, atol=1e-300)
+    assert np.array_equal(ab.cpu().numpy().reshape(64, 64, 64), ref.absorb)
+    c = ctr.cpu().numpy()
+    assert int(c[abi.CTR["deposits"]]) == ref.counter("deposits") and int(c[abi.CTR["photons"]]) == n * k
