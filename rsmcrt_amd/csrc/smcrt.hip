@@ -59,7 +59,7 @@ __device__ unsigned long long g_diag[72];
 __device__ unsigned long long g_diag_t[9];
 #endif
 
-template <bool LDS_FACES, int GM, bool XSRC>
+template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
 #ifndef SMCRT_WAVES_PER_EU
 #define SMCRT_WAVES_PER_EU 3
 #endif
@@ -206,7 +206,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       const bool tap = (L.st >= ST_N1 && L.st <= ST_N4);
       const int32_t capi = fres ? L.new_layer : (tap ? L.Ls : 0);
       const int32_t capj = fres ? L.old_layer : 0;
-      R = eval_sdfs(nodes, prog, K.n_prog, eval_query(L), test_kernel && L.st == ST_LAYER, capi, capj);
+      const bool mask_le = test_kernel && L.st == ST_LAYER;
+      const uint64_t evm = __ballot(have);
+      if (COOP && (uint32_t)__popcll(evm) <= (uint32_t)K.coop_lanes) {  // a sparse wave: one lane at a time
+        const V3 q = eval_query(L);
+        uint64_t m = evm;
+        while (m) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          const V3 ql = v3(__shfl(q.x, l, 64), __shfl(q.y, l, 64), __shfl(q.z, l, 64));
+          const EvalOut o = eval_sdfs_coop(nodes, prog, K.n_prog, K.n_top, ql, __shfl((int)mask_le, l, 64) != 0,
+                                           __shfl(capi, l, 64), __shfl(capj, l, 64));
+          if (lane_id == l) R = o;
+        }
+      } else {
+        R = eval_sdfs(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
+      }
       // packet%cnts counts the evaluations of tauint2's ds/dsNew arrays only (inttau2.f90:67,83,
       // 138,183,219,232): not the initial layer search, the Fresnel ds lookups or calcNormal.
       const bool counted = L.st == ST_H0 || L.st == ST_H1 || L.st == ST_H3 || L.st == ST_M1 || L.st == ST_G0;
@@ -564,8 +579,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   if (binned) close_log(K, C, W, overflow, whist);
 
 #ifdef SMCRT_DIAG
-  if (lane_id == 0)
+  if (lane_id == 0) {
     for (int i = 0; i < 9; ++i) atomicAdd(&g_diag_t[i], t_acc[i]);
+    unsigned long long tw = 0;
+    for (int i = 0; i < 9; ++i) tw += t_acc[i];
+    atomicMax(&g_diag[68], (unsigned long long)w_iters);  // the longest wave: iterations, ticks
+    atomicMax(&g_diag[69], tw);
+    atomicAdd(&g_diag[70], 1ull);  // waves
+  }
 #endif
   // ---- per-wave counter reduction ------------------------------------------------------
   unsigned long long* const counters = C->counters;
@@ -653,6 +674,7 @@ struct smcrt_scene {
   smcrt_sdf_node* d_nodes = nullptr;
   ProgOp* d_prog = nullptr;
   int n_prog = 0;
+  int coop_lanes = 0;
   double inv2[3] = {0.0, 0.0, 0.0};
   int grid_mode = 0;  // transport_kernel<*, GM>: 1 = every 2*max a power of two, 2 = and every n too
   int32_t fe[3] = {0, 0, 0};
@@ -742,12 +764,16 @@ static hipError_t harvest_times(smcrt_scene* s) {
 }
 
 // The transport kernel instantiation for this scene (LDS faces? power-of-two grid?).
+// Scenes with many tops (coop_lanes > 0) and a plain source get the instantiation with the
+// cooperative tail EVAL; it costs registers (scratch spills), so small scenes never pay for it.
 static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
-#define TK(F, G) {(const void*)transport_kernel<F, G, false>, (const void*)transport_kernel<F, G, true>}
-  static const void* const fns[2][3][2] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
+#define TK(F, G)                                                                                         \
+  {(const void*)transport_kernel<F, G, false, false>, (const void*)transport_kernel<F, G, true, false>, \
+   (const void*)transport_kernel<F, G, false, true>}
+  static const void* const fns[2][3][3] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
                                            {TK(true, 0), TK(true, 1), TK(true, 2)}};
 #undef TK
-  return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : 0];
+  return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : (s->coop_lanes > 0 ? 2 : 0)];
 }
 
 // Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
@@ -879,8 +905,10 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     return t[0] == 1.0 && t[1] == 0.0 && t[2] == 0.0 && t[4] == 0.0 && t[5] == 1.0 && t[6] == 0.0 &&
            t[8] == 0.0 && t[9] == 0.0 && t[10] == 1.0;
   };
+  std::vector<int32_t> top_first((size_t)n_top + 1, 0);
   for (int32_t i = 0; i < n_top; ++i) {
     const smcrt_sdf_node& nd = nodes[top[i]];
+    top_first[i] = (int32_t)prog.size();
     if (nd.kind != SMCRT_SDF_MODEL) {
       prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0, translate_only(top[i]), 0});
     } else {
@@ -891,6 +919,12 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     }
   }
   s->n_prog = (int)prog.size();
+  top_first[n_top] = s->n_prog;
+  for (int32_t i = 0; i <= n_top; ++i)  // eval_sdfs_coop's table of each top's first op
+    prog.push_back(ProgOp{top_first[i], PROG_TOP, 0, 0, 0.0, 0, 0});
+  // A sparse wave evaluates its lanes' SDF arrays one lane at a time across the wave when
+  // that is cheaper than the serial per-lane chain over all n_top tops (transport.h).
+  s->coop_lanes = n_top >= 8 ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
   // n*p/(2*max) may be computed as n*p*inv exactly when 2*max is a power of two
   const double maxes[3] = {grid->xmax, grid->ymax, grid->zmax};
   for (int a = 0; a < 3; ++a) {
@@ -1171,6 +1205,7 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
     HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)));
     unsigned long long lt = 0;
     for (int i = 0; i < 64; ++i) lt += h[i];
+    std::fprintf(stderr, "[diag] waves %llu, longest wave %llu trips %llu ticks\n", h[70], h[68], h[69]);
     std::fprintf(stderr, "[diag] trips %llu dda %llu eval %llu p7 %llu | lane-trips %llu:", h[64], h[65], h[66],
                  h[67], lt);
     for (int i = 0; i < 64; ++i)
@@ -1248,6 +1283,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.nodes = s->d_nodes;
   K.prog = s->d_prog;
   K.n_prog = s->n_prog;
+  K.coop_lanes = s->coop_lanes;
   K.inv2x = s->inv2[0]; K.inv2y = s->inv2[1]; K.inv2z = s->inv2[2];
   K.fex = s->fe[0]; K.fey = s->fe[1]; K.fez = s->fe[2];
   K.props = s->d_props;

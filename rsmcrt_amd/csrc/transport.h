@@ -85,6 +85,7 @@ struct KParams {
   const smcrt_detector* __restrict__ dets;
   const int64_t* __restrict__ det_off;
   int32_t n_prog, n_top, n_dets;
+  int32_t coop_lanes;  // cooperative EVAL when at most this many lanes need one (0 = never)
   int32_t nx, ny, nz;
   uint32_t flags;
   double xmax, ymax, zmax;
@@ -863,6 +864,61 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
       if (i == capj) r.vb = d;
     }
   }
+  return r;
+}
+
+// Cooperative EVAL: the whole wave evaluates the SDF array for one lane's query point `q`.
+// Lane j runs the programs of tops j+1, j+65, ... (prog[n_prog + i].node holds the first op
+// of top i+1, prog[n_prog + n_top].node == n_prog), then the wave reduces the partials. Used
+// in a launch's tail, where a wave has only a few live photons and eval_sdfs' serial chain of
+// dependent scalar loads and fp64 ops over every top is pure latency (one sphere ~1000
+// cycles). Results equal eval_sdfs': min/abs-min are exact, maxloc ties go to the lowest top
+// index as eval_sdfs' strict compares do, and the captured values come from the owning lane.
+// (minv may differ from eval_sdfs' in the sign of a zero; it is only ever tested with > 0.)
+__device__ __attribute__((noinline)) EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restrict__ nodes,
+                                                           const ProgOp* __restrict__ prog, int32_t n_prog,
+                                                           int32_t n_top, V3 q, bool mask_le, int32_t capi,
+                                                           int32_t capj) {
+  const int32_t lane = (int32_t)(threadIdx.x & 63);
+  double minabs = __builtin_inf(), minv = __builtin_inf(), best = -__builtin_inf();
+  double va = 0.0, vb = 0.0;
+  int32_t loc = 0;
+  for (int32_t i = lane; i < n_top; i += 64) {
+    const int32_t b = prog[n_prog + i].node, e = prog[n_prog + i + 1].node;
+    if (b == e) continue;  // an empty model never completes its ds(i)
+    double acc = 0.0;
+    for (int32_t ip = b; ip < e; ++ip) {
+      const ProgOp op = prog[ip];
+      const double v = sdf_prim(nodes + op.node, q, op.translate_only != 0);
+      if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
+      else acc = csg(op.op, acc, v, op.k);
+    }
+    const double d = acc;
+    const int32_t t = i + 1;
+    const double a = fabs(d);
+    if (a < minabs) minabs = a;
+    if (d < minv) minv = d;
+    const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+    if (neg && (loc == 0 || d > best)) { best = d; loc = t; }
+    if (t == capi) va = d;
+    if (t == capj) vb = d;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double m2 = __shfl_xor(minabs, off, 64);
+    if (m2 < minabs) minabs = m2;
+    const double v2 = __shfl_xor(minv, off, 64);
+    if (v2 < minv) minv = v2;
+    const double b2 = __shfl_xor(best, off, 64);
+    const int32_t l2 = __shfl_xor(loc, off, 64);
+    if (l2 != 0 && (loc == 0 || b2 > best || (b2 == best && l2 < loc))) { best = b2; loc = l2; }
+  }
+  EvalOut r;
+  r.minabs = minabs;
+  r.minv = minv;
+  r.maxloc = loc;
+  r.va = capi > 0 ? __shfl(va, (capi - 1) & 63, 64) : 0.0;
+  r.vb = capj > 0 ? __shfl(vb, (capj - 1) & 63, 64) : 0.0;
   return r;
 }
 

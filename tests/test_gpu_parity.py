@@ -451,3 +451,30 @@ def test_async_fold_pipeline():
     assert np.array_equal(ab.cpu().numpy().reshape(64, 64, 64), ref.absorb)
     c = ctr.cpu().numpy()
     assert int(c[abi.CTR["deposits"]]) == ref.counter("deposits") and int(c[abi.CTR["photons"]]) == n * k
+
+
+def test_coop_eval_models_and_many_tops():
+    """The cooperative tail EVAL (transport.h eval_sdfs_coop, used for scenes with >= 8 tops):
+    smooth-union and intersection models among 13 tops, several at once over the same query
+    point, Fresnel everywhere (n differs per layer), and a small batch so most EVALs run in
+    sparse waves. Must equal the oracle's serial maxloc/minval bit for bit."""
+    from rsmcrt_amd.scene import Scene, box, cylinder, invert, model, mono, sphere, translate
+    sdfs = []
+    for i in range(10):
+        x, y, z = (-0.6 + 0.13 * i, 0.25 * ((i % 3) - 1), 0.2 * ((i % 4) - 1.5))
+        sdfs.append(sphere(0.08 + 0.01 * (i % 3), mono(3.0, 0.1, 0.8, 1.2 + 0.02 * i), len(sdfs) + 1,
+                           transform=invert(translate((x, y, z)))))
+    opt_m = mono(5.0, 0.2, 0.5, 1.45)
+    sdfs.append(model([sphere(0.2, opt_m, len(sdfs) + 1, transform=invert(translate((0.0, 0.0, 0.5)))),
+                       cylinder((0.0, -0.3, 0.5), (0.0, 0.3, 0.5), 0.08, opt_m, len(sdfs) + 1)],
+                      abi.OP_SMOOTH_UNION, 0.05))
+    sdfs.append(model([sphere(0.25, opt_m, len(sdfs) + 1, transform=invert(translate((0.0, 0.5, -0.5)))),
+                       box((0.3, 0.3, 0.3), opt_m, len(sdfs) + 1, transform=invert(translate((0.1, 0.5, -0.5))))],
+                      abi.OP_INTERSECTION, 0.0))
+    sdfs.append(box((2.0, 2.0, 2.0), mono(0.5, 0.01, 0.0, 1.0), len(sdfs) + 1))
+    sc = Scene(sdfs)
+    assert sc.n_top == 13
+    src = scene.uniform_source((-1.0, -1.0, 0.999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, scene.grid(40, 40, 40, 1, 1, 1), src, 1500)
+    compare(gpu, cpu)
+    assert cpu.counter("fresnel") > 0
