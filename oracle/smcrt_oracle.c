@@ -14,10 +14,12 @@
  *   SDF primitives        src/sdfs/sdfs.f90:494-735, src/sdfs/sdf_base.f90:146-190
  *   CSG operators         src/sdfs/sdfModifiers.f90:428-491
  *   Fresnel               src/surfaces.f90:14-127
- *   emitters              src/photon.f90:311-359 (point), 566-649 (uniform), 652-710 (pencil)
+ *   emitters              src/photon.f90:159-1043 (every source: point, uniform, pencil,
+ *                         circular, focus, annulus, dslit, aperture, slm, ...)
+ *   source spectra        src/piecewise.f90 (constant, 1-D and 2-D piecewise)
  *   scatter               src/photon.f90:1045-1103
  *   detectors             src/detectors/detector_base.f90:137-235, detectors.f90:147-469,
- *                         src/geometryMod.f90:217-270
+ *                         src/geometryMod.f90:217-270 (circle, annulus, camera, fibre)
  *
  * Parity pinning: the Fortran reference cannot be built here without stand-ins for its
  * un-vendored dependencies (toml-f, fortran_utilities, stdlib — fpm.toml:8-16), so this

@@ -4,7 +4,7 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 for w in m1 m0 m2 m3 m4 m5; do
-  timeout -k 10 240 python -u bench.py --workload $w --steps ${STEPS:-3} --warmup 1 --cpu-seconds ${CPU_S:-8} \
+  timeout -k 10 240 python -u bench.py --workload $w --steps ${STEPS:-2} --warmup 1 --cpu-seconds ${CPU_S:-8} \
     > gpurun_out/wl_$w.json 2> gpurun_out/wl_$w.err
   echo "$w done"
 done
