@@ -73,7 +73,7 @@ def workload(name, grid_n):
         return (builders.skin_layers(), scene.grid(n, n, n, 0.05, 0.05, 0.05),
                 scene.pencil_source((0.0, 0.0, 0.0499), (0.0, 0.0, -1.0)), dets,
                 f"M5 (build-defined) skin: layered boxes with Fresnel at every interface, pencil beam, circle + "
-                f"annulus reflectance detectors, {n}^3 grid", 2_000_000)
+                f"annulus reflectance detectors, {n}^3 grid", 8_000_000)
     raise ValueError(name)
 
 
@@ -244,6 +244,7 @@ def main():
     ap.add_argument("--sync-fold", action="store_true", help="diagnostic: each step waits for its own fold")
     ap.add_argument("--source", default="default", choices=["default", "uniform"],
                     help="diagnostic: uniform = parallelogram source over the z=0.99 plane")
+    ap.add_argument("--no-dets", action="store_true", help="diagnostic: the workload's scene without its detectors")
     ap.add_argument("--esc-nr", type=int, default=20)
     ap.add_argument("--esc-nz", type=int, default=10)
     args = ap.parse_args()
@@ -270,6 +271,8 @@ def main():
     from rsmcrt_amd.engine import Engine
 
     sc, g, src, dets, desc, default_batch = workload(args.workload, args.grid)
+    if args.no_dets:
+        dets = []
     if args.source == "uniform":
         from rsmcrt_amd import scene as _scene
         src = _scene.uniform_source((-1.0, -1.0, 0.99), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
