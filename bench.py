@@ -41,7 +41,7 @@ def workload(name, grid_n):
         n = grid_n or 200
         return (builders.setup_scat_test(10.0), scene.grid(n, n, n, 1.0, 1.0, 1.0), scene.point_source(), [],
                 f"M0 scat_test (res/scat_test.toml): sphere r=1 tau=10 g=0 in 2^3 box, point source, {n}^3 grid "
-                "(setupGeometry.f90:409-435)", 4_000_000)
+                "(setupGeometry.f90:409-435)", 3_000_000)
     if name == "m1":
         n = grid_n or 128
         return (builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0), scene.grid(n, n, n, 1.0, 1.0, 1.0),
