@@ -1063,6 +1063,10 @@ static void refine_rpp(smcrt_scene* s) {
     if (s->ctl_pending[sl] && hipEventQuery(s->ctl_ev[sl]) == hipSuccess) {
       s->ctl_pending[sl] = false;
       const uint32_t* h = s->h_ctl + 8 * sl;
+      static const bool pool_log = std::getenv("SMCRT_POOL_LOG") != nullptr;  // diagnostics
+      if (pool_log)
+        std::fprintf(stderr, "[pool] slot %d: %u photons, %u records, %u overflowed, %u of %llu chunks\n", sl, h[4],
+                     h[3], h[1], h[0], (unsigned long long)s->pool_chunks);
       if (h[4] > 0) {
         const double rpp = (double)(h[3] + h[1]) / (double)h[4];
         s->rpp_est = std::max(1.0, rpp);
