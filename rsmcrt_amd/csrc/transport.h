@@ -875,7 +875,7 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
 // cycles). Results equal eval_sdfs': min/abs-min are exact, maxloc ties go to the lowest top
 // index as eval_sdfs' strict compares do, and the captured values come from the owning lane.
 // (minv may differ from eval_sdfs' in the sign of a zero; it is only ever tested with > 0.)
-__device__ __attribute__((noinline)) EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restrict__ nodes,
+__device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restrict__ nodes,
                                                            const ProgOp* __restrict__ prog, int32_t n_prog,
                                                            int32_t n_top, V3 q, bool mask_le, int32_t capi,
                                                            int32_t capj) {
