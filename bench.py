@@ -121,6 +121,12 @@ def cpu_baseline(sc, g, src, dets, seconds, eng, threads, seed, chunk):
     for r in results[1:]:
         res.merge(r)
     assert res.n_photons == n
+    base = {"value": n / dt, "unit": "photon packets/s", "cores": threads, "kind": "port",
+            "sample": f"photons [0,{n}) of the same workload, oracle/ C restatement (gcc -O2) on {threads} host "
+                      f"thread{'s' if threads > 1 else ''} for {dt:.1f} s",
+            "seconds": round(dt, 2)}
+    if eng is None:
+        return base, None
     gpu = eng.run(src, n, seed=seed)
     fc, fg = res.normalised_fluence(), gpu.normalised_fluence()
     rmse = float(np.sqrt(np.mean((fg - fc) ** 2)))
@@ -131,10 +137,7 @@ def cpu_baseline(sc, g, src, dets, seconds, eng, threads, seed, chunk):
     if dets:
         db = float(np.max(np.abs(gpu.det_bins - res.det_bins)) / max(1e-300, float(np.max(np.abs(res.det_bins)))))
         agree["det_bins_max_rel_diff_vs_cpu"] = db
-    return {"value": n / dt, "unit": "photon packets/s", "cores": threads, "kind": "port",
-            "sample": f"photons [0,{n}) of the same workload, oracle/ C restatement (gcc -O2) on {threads} host "
-                      f"threads for {dt:.1f} s",
-            "seconds": round(dt, 2)}, agree
+    return base, agree
 
 
 def pmc_summary(name, batch, grid):
@@ -150,6 +153,65 @@ def pmc_summary(name, batch, grid):
     if t.get("workload", "m1") != name or t.get("batch") != batch or t.get("grid") != grid:
         return {}
     return t
+
+
+# fp64 operations (add/sub, mul, div, sqrt; abs/min/max not counted) of one evaluation of each
+# SDF primitive as geometry.h writes it (sdfs.f90:494-735), of its transform (translation
+# only: 3 adds; general vec_dot_mat: 9 mul + 9 add) and of each CSG fold (sdfModifiers.f90)
+SDF_FLOP = {1: 7, 2: 10, 3: 12, 4: 45, 5: 6, 6: 29, 7: 30, 8: 50, 9: 20, 10: 5}
+CSG_FLOP = {0: 0, 1: 8, 2: 1, 3: 1}
+FP64_PEAK_TFLOPS = 78.6  # MI355X fp64 vector, spec
+
+
+def flop_per_eval(sc):
+    """fp64 FLOP of one evaluation of the whole SDF array (every top, models folded)."""
+    tot = 0
+    for t in sc.top:
+        nd = sc.nodes[t]
+        kids = [nd] if nd.kind != 11 else [sc.nodes[nd.first_child + c] for c in range(nd.n_children)]
+        for i, c in enumerate(kids):
+            tr = list(c.transform)
+            ident = tr[0] == 1 and tr[5] == 1 and tr[10] == 1 and not any(tr[k] for k in (1, 2, 4, 6, 8, 9))
+            tot += SDF_FLOP.get(c.kind, 0) + (3 if ident else 18)
+            if nd.kind == 11 and i > 0:
+                tot += CSG_FLOP.get(nd.op, 0)
+    return tot
+
+
+def fp64_roofline(sc, sdf_evals_per_launch, kern_ms):
+    """the SDF march's fp64 FLOP/s = SDF evaluations (packet%cnts, device
+    counter) x FLOP per evaluation, over the transport kernel's launch time."""
+    n_top = max(1, len(sc.top))
+    flop = sdf_evals_per_launch / n_top * flop_per_eval(sc)
+    ach = flop / (kern_ms * 1e-3) / 1e12
+    return {"bound": "fp64-valu", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / FP64_PEAK_TFLOPS, "sdf_flop_per_launch": flop, "flop_per_array_eval": flop_per_eval(sc)}
+
+
+# Issue cycles per wave64 VALU instruction on one SIMD-32 (profiles/r01_valu_rates.txt for
+# fp64, MI355X_MICROARCH.md for 32-bit: 2 cycles with >= 2 waves per SIMD)
+VALU_CYCLES = {"f64_addmulfma": 5.0, "f64_trans": 17.0, "int64": 8.0, "other_32bit": 2.0}
+SIMDS, CLOCK_HZ = 1024, 2.4e9
+
+
+def valu_roofline(pmc, kern_ms):
+    """VALU issue utilisation of the transport kernel from the PMC instruction mix of the
+    committed profile of this configuration: sum over classes of (instructions x issue
+    cycles) / (1024 SIMDs x 2.4 GHz x the live launch time)."""
+    tot = pmc.get("valu_insts_per_launch")
+    if not tot:
+        return None
+    cls = pmc.get("valu_classes") or {}
+    f64 = sum(cls.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64"))
+    tr = cls.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+    i64 = cls.get("SQ_INSTS_VALU_INT64", 0.0)
+    rest = max(0.0, tot - f64 - tr - i64)
+    mix = {"f64_addmulfma": f64, "f64_trans": tr, "int64": i64, "other_32bit": rest}
+    cycles = sum(mix[k] * VALU_CYCLES[k] for k in mix)
+    avail = SIMDS * CLOCK_HZ * kern_ms * 1e-3
+    return {"bound": "valu-issue", "achieved": cycles / avail, "peak": 1.0, "unit": "fraction of SIMD issue cycles",
+            "frac": cycles / avail, "valu_insts_per_launch": tot, "mix": mix, "issue_cycles": VALU_CYCLES,
+            "salu_insts_per_launch": pmc.get("salu_insts_per_launch"), "source": pmc.get("source")}
 
 
 def escape_bench(args):
@@ -237,7 +299,8 @@ def main():
                                                         "escape: photons per cell)")
     ap.add_argument("--grid", type=int, default=0, help="grid cells per axis (0 = workload default)")
     ap.add_argument("--seed", type=int, default=123456789)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu1-seconds", type=float, default=8.0, help="the 1-core CPU leg (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share, <= 16")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
@@ -268,7 +331,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from rsmcrt_amd import abi, shard
-    from rsmcrt_amd.engine import Engine
+    from rsmcrt_amd.engine import Comm, Engine
 
     sc, g, src, dets, desc, default_batch = workload(args.workload, args.grid)
     if args.no_dets:
@@ -282,6 +345,13 @@ def main():
         # before the reduce makes jmean complete inside the timed region
         run_flags |= abi.FLAG_ASYNC_FOLD
     eng = Engine(sc, g, dets, device=torch.cuda.current_device())
+    comm = None
+    if world > 1:
+        # the engine's own RCCL communicator (smcrt_comm_init_rank): rank 0's id reaches the
+        # other ranks through the torch process group, then libsmcrt reduces its tallies
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm(uid[0], world, rank, torch.cuda.current_device())
     nv = g.nx * g.ny * g.nz
     jmean = torch.zeros(nv, dtype=torch.float64, device=dev)
     absorb = torch.zeros(nv, dtype=torch.float64, device=dev)
@@ -311,7 +381,7 @@ def main():
     eng.kernel_times()  # reset
     c0 = counters.clone()
     if world > 1:
-        dist.all_reduce(c0)
+        dist.all_reduce(c0)  # (the timed reduce sums `counters` over ranks: subtract the sum)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -319,8 +389,8 @@ def main():
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
     eng.fence(stream.cuda_stream)
-    if world > 1:
-        shard.reduce_tallies((jmean, absorb, nscatt, counters, det_bins), dist)
+    if comm is not None:  # ONE packed RCCL all-reduce of every tally, inside libsmcrt
+        eng.reduce_device_tallies(comm, dt_, root=-1, stream=stream.cuda_stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -332,35 +402,33 @@ def main():
     log(f"[bench] {args.workload}: {args.steps} timed steps in {elapsed:.2f} s")
     kt = eng.kernel_times()  # HIP events around each kernel group, on the launch stream
     eng.set_timing(False)
-    launches = max(1, kt["launches"])
-    kern_ms = kt["transport_ms"] / launches
-    dep_ms = kt["deposit_ms"] / launches
+    ms_per_step = elapsed * 1e3 / args.steps
+    launches = kt["launches"]
+    kern_ms = kt["transport_ms"] / launches if launches > 0 else 0.0
+    dep_ms = kt["deposit_ms"] / launches if launches > 0 else 0.0
+    timing_src = "HIP events around each transport launch (smcrt_scene_kernel_times)"
+    if not kern_ms > 0.0:  # no launch was timed: fall back to the wall time per step (flagged)
+        launches = max(1, launches)
+        kern_ms = ms_per_step * args.steps / launches
+        timing_src = "FALLBACK: wall time per step (the event timing returned no launches)"
     cdelta = (counters - c0).cpu().numpy()  # all ranks, timed steps only
     photons = world * args.steps * B
 
     out = None
     if rank == 0:
-        deposits = float(cdelta[abi.CTR["deposits"]]) / world  # per rank, over the timed steps
+        per_rank = 1.0 / world
+        deposits = float(cdelta[abi.CTR["deposits"]]) * per_rank  # per rank, over the timed steps
         dep_per_launch = deposits / launches
         # algorithmic HBM bytes of the transport kernel: 8 B per jmean deposit (SURVEY.md
         # §8(d): the reference's fp32 read+write per atomic; here one 8-B deposit record)
         alg_bytes = 8.0 * dep_per_launch
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         pmc = pmc_summary(args.workload, B, g.nx)
-        traffic, traffic_src = pmc.get("hbm_bytes_per_launch"), pmc.get("source")
-        # The kernel's binding resource is VALU issue: wave-instructions per launch (PMC
-        # SQ_INSTS_VALU of the same command) / the live launch time, against the chip's issue
-        # peak of one wave64 VALU instruction per 4 cycles per SIMD (1024 SIMDs, 2.4 GHz).
-        valu_peak = 1024 * 2.4e9 / 4 / 1e9
-        valu = None
-        if pmc.get("valu_insts_per_launch"):
-            va = pmc["valu_insts_per_launch"] / (kern_ms * 1e-3) / 1e9
-            valu = {"bound": "valu", "achieved": va, "peak": valu_peak, "unit": "G wave-instr/s", "frac": va / valu_peak,
-                    "valu_insts_per_launch": pmc["valu_insts_per_launch"],
-                    "salu_insts_per_launch": pmc.get("salu_insts_per_launch"), "source": traffic_src}
+        traffic, traffic_src = pmc.get("step_hbm_bytes_per_launch"), pmc.get("source")
         metric = "photon packets/sec (128^3 jmean grid, path-length deposition)"
         if args.workload != "m1" or g.nx != 128:
             metric = f"photon packets/sec ({args.workload}, {g.nx}x{g.ny}x{g.nz} jmean grid, path-length deposition)"
+        sdf_evals = float(cdelta[abi.CTR["sdf_evals"]]) * per_rank
         out = {
             "metric": metric,
             "value": photons / elapsed,
@@ -368,7 +436,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
+            "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -376,28 +444,41 @@ def main():
             "data": "synthetic (Philox photon streams; scenes from setupGeometry.f90 / SURVEY §8(d))",
             "config": {"workload": desc,
                        "grid": [g.nx, g.ny, g.nz], "photons_per_step_per_gpu": B, "photons_timed": photons,
-                       "parallelism": f"photon-index shards x{world} + RCCL all-reduce of tallies"},
+                       "parallelism": f"photon-index shards x{world}" + (
+                           " + one packed RCCL all-reduce of the tallies in libsmcrt" if world > 1 else "")},
+            # SURVEY §8(d)'s HBM view of the deposition: 8 B per jmean deposit (the reference's
+            # fp32 read+write per atomic) / the transport kernel's launch time. `traffic` is the
+            # PMC HBM bytes of the whole step (transport + deposit folds) per launch.
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": traffic,
-                         "kernel": "transport_kernel", "avg_launch_ms": kern_ms,
-                         "launches_timed": kt["launches"],
+                         "kernel": "transport_kernel", "avg_launch_ms": kern_ms, "timing": timing_src,
+                         "launches_timed": launches,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "traffic_source": traffic_src,
+                         "traffic_by_kernel": pmc.get("hbm_bytes_per_launch_by_kernel"),
+                         "traffic_over_algorithmic": (traffic / alg_bytes) if traffic and alg_bytes else None,
                          "deposits_per_photon": deposits / (args.steps * B),
                          "deposit_fold_ms_per_launch": dep_ms,
-                         "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) / world / launches,
-                         "sdf_evals_per_photon": float(cdelta[abi.CTR["sdf_evals"]]) / world / (args.steps * B),
-                         "binding_resource": "fp64 VALU issue + divergence (see DESIGN.md), not HBM"},
-            "valu_roofline": valu,
+                         "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) * per_rank / launches,
+                         "sdf_evals_per_photon": sdf_evals / (args.steps * B),
+                         "note": "the transport kernel is bound by fp64 VALU issue and divergence, not by "
+                                 "HBM: see valu_roofline / fp64_roofline and DESIGN.md §4.2"},
+            "fp64_roofline": fp64_roofline(sc, sdf_evals / launches, kern_ms),
+            "valu_roofline": valu_roofline(pmc, kern_ms),
             "cpu_baseline": None,
         }
     if rank == 0 and world == 1 and not args.no_cpu:
-        log(f"[bench] CPU leg: {args.cpu_seconds} s on the oracle restatement")
+        threads = args.cpu_threads or cpu_threads()
+        log(f"[bench] CPU leg: {args.cpu_seconds} s on {threads} threads + {args.cpu1_seconds} s on 1 core")
         chunk = max(50, min(2000, B // 1000))
-        base, agree = cpu_baseline(sc, g, src, dets, args.cpu_seconds, eng, args.cpu_threads or cpu_threads(),
-                                   args.seed, chunk)
+        base, agree = cpu_baseline(sc, g, src, dets, args.cpu_seconds, eng, threads, args.seed, chunk)
         out["cpu_baseline"] = base
         out["parity"] = agree
+        if args.cpu1_seconds > 0:
+            one, _ = cpu_baseline(sc, g, src, dets, args.cpu1_seconds, None, 1, args.seed, max(50, chunk // 8))
+            out["cpu_baseline_1core"] = one
+            out["gpu_over_cpu_1core"] = out["value"] / one["value"]
+        out["gpu_over_cpu"] = out["value"] / base["value"]
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()

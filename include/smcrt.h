@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SMCRT_ABI_VERSION 2
+#define SMCRT_ABI_VERSION 3
 
 typedef enum smcrt_status {
   SMCRT_OK = 0,
@@ -444,10 +444,77 @@ int smcrt_scene_get_optprops(const smcrt_scene* scene, int32_t top_index, int32_
  * photons per step, each step from photon first_photon (the reference reseeds every
  * run_MCRT). The layer's original properties are restored at the end. A step whose
  * properties repeat an earlier step's bits reuses that step's error (runs are deterministic),
- * so the reference's mode costs two runs. io (may be NULL) accumulates the tallies of the
- * steps actually run. */
+ * so the reference's mode costs two runs when io is NULL. With io (may be NULL) every step
+ * runs and io accumulates all max_steps runs, as the reference's jmean does. */
 int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_inverse_config* cfg,
                       const smcrt_run_config* run, const double* targets, double* steps, smcrt_tallies* io);
+
+/* ---- multi-GPU: photon shards + ONE packed RCCL reduction (SURVEY §8(b) n_gpus, §8(e)) --
+ * The reference splits `do j = 1, nphotons` statically over OpenMP threads
+ * (kernelsMod.f90:1859) and means to sum the tallies onto the root with mpi_reduce
+ * (kernelsMod.f90:2351-2357). Here photon index ranges are split over GPUs; since a photon's
+ * Philox stream is keyed by its global index, N GPUs compute exactly the photons one GPU
+ * would. The only exchange is one reduction of a packed fp64 buffer per run, over RCCL
+ * (xGMI between the GPUs of a node). RCCL (librccl.so.1) is loaded on first use; without it
+ * these calls return SMCRT_ERR_RCCL.
+ *
+ * Packed layout (fp64 elements, in this order; a grid or the detector block is present only
+ * when its bit is set in `fields`, the scalar block always):
+ *   jmean[n_voxels] | absorb[n_voxels] | emission[n_voxels] | det_bins[n_det_bins] |
+ *   nscatt | moments[24] | counters[SMCRT_NCOUNTERS]
+ * Counters travel as doubles: exact while every total stays below 2^53. */
+enum {
+  SMCRT_PACK_JMEAN = 1u << 0,
+  SMCRT_PACK_ABSORB = 1u << 1,
+  SMCRT_PACK_EMISSION = 1u << 2,
+  SMCRT_PACK_DET_BINS = 1u << 3
+};
+typedef struct smcrt_pack_layout {
+  int64_t n_voxels;    /* nx*ny*nz */
+  int64_t n_det_bins;  /* smcrt_scene_det_bins */
+  uint32_t fields;     /* SMCRT_PACK_* */
+  int32_t reserved;
+} smcrt_pack_layout;
+
+/* Doubles in a packed buffer of this layout. Host only. */
+int smcrt_pack_size(const smcrt_pack_layout* layout, int64_t* n_doubles);
+/* Host tallies -> packed buffer (grids from the fp64 arrays when given, else from the fp32
+ * ones; a NULL tally packs zeros). Host only. */
+int smcrt_pack_host(const smcrt_pack_layout* layout, const smcrt_tallies* t, double* buf);
+/* Packed buffer -> host tallies, ACCUMULATED like smcrt_run's (fp32 grids get
+ * (float)((double)old + value)). Host only. */
+int smcrt_unpack_host(const smcrt_pack_layout* layout, const double* buf, smcrt_tallies* t);
+
+/* One process per GPU (torchrun / mpirun): rank 0 makes an id and hands it to every rank
+ * (out of band); each rank then joins on its device. */
+#define SMCRT_UNIQUE_ID_BYTES 128
+typedef struct smcrt_comm smcrt_comm;
+int smcrt_comm_unique_id(uint8_t* id /* SMCRT_UNIQUE_ID_BYTES */);
+int smcrt_comm_init_rank(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, smcrt_comm** out);
+void smcrt_comm_destroy(smcrt_comm* comm);
+/* Sum every rank's device tallies (smcrt_run_device's buffers) over `comm` with ONE packed
+ * collective on `stream`: an all-reduce when root < 0 (every rank gets the sums), else a
+ * reduce onto rank `root` (the mpi_reduce of kernelsMod.f90:2353-2357; the other ranks'
+ * buffers are left as they were). The fields are the non-NULL pointers of `dev` (records are
+ * not reduced); every rank must pass the same set. Asynchronous on `stream`. */
+int smcrt_reduce_device_tallies(smcrt_scene* scene, smcrt_comm* comm, smcrt_device_tallies* dev, int32_t root,
+                                void* stream);
+
+/* One process, several GPUs: smcrt_run with n_gpus. smcrt_multi_create
+ * uploads the scene to each of `devices` (NULL: devices 0 .. n_devices-1; n_devices <= 0:
+ * every visible device); smcrt_multi_run gives device g the photons
+ * [first + g*N/n, first + (g+1)*N/n) and sums the devices' tallies onto the first device with
+ * one packed RCCL reduce, then accumulates them into `io` as smcrt_run does. Results do not
+ * depend on the number of devices (up to the fp64 summation order of jmean). */
+typedef struct smcrt_multi smcrt_multi;
+int smcrt_multi_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t* top, int32_t n_top,
+                       const smcrt_grid* grid, const smcrt_detector* dets, int32_t n_dets,
+                       const int32_t* devices, int32_t n_devices, smcrt_multi** out);
+int smcrt_multi_info(const smcrt_multi* multi, int32_t* n_devices);
+/* The scene on device slot i (0 <= i < n_devices), e.g. for smcrt_scene_set_optprops. */
+smcrt_scene* smcrt_multi_scene(smcrt_multi* multi, int32_t i);
+int smcrt_multi_run(smcrt_multi* multi, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io);
+void smcrt_multi_destroy(smcrt_multi* multi);
 
 /* ---- output formats (src/writer.f90), host-side, no GPU needed ------------------------
  * Written byte for byte as the reference writes them, so its readers
@@ -522,18 +589,25 @@ int smcrt_job_info(const smcrt_job* job, smcrt_job_desc* desc);
 int smcrt_job_scene(const smcrt_job* job, smcrt_sdf_node* nodes, int32_t* top, smcrt_detector* dets);
 /* The metadata dict (the values parse_* and finalise set) as TOML text, for NRRD headers. */
 int smcrt_job_metadata(const smcrt_job* job, char* buf, int32_t cap);
-/* default_MCRT (kernelsMod.f90:14-82): run_MCRT on `device`, then finalise (:2321-2416).
- * Photons run in batches of checkpoint_every_n; after each, <checkpoint_file> (relative to
- * outdir) is rewritten with the tally of the photons done so far (writer.f90:426-457). With
- * load_checkpoint, the checkpoint's input file (next to this one) is run for its remaining
- * photons with iseed*101 from zeroed tallies, as the reference's second setup() leaves it.
+/* default_MCRT (kernelsMod.f90:14-82): run_MCRT on `device` (SMCRT_ALL_DEVICES: every
+ * visible GPU through smcrt_multi_run), then finalise (:2321-2416).
+ * Photons run in batches of checkpoint_every_n; after each, <checkpoint_file> is rewritten
+ * with the tally of the photons done so far (writer.f90:426-457). With load_checkpoint,
+ * <checkpoint_file> is read back, and its input file (next to this one) is run for its
+ * remaining photons with iseed*101 from zeroed tallies, as the reference's second setup()
+ * leaves it. A relative <checkpoint_file> is taken relative to outdir for both the write
+ * and the read (the reference uses one CWD-relative name for both, kernelsMod.f90:54,1863).
  * Writes, under outdir (the reference's fileplace):
  *   jmean/<fluence>, normalised;
  *   emission/<render_source_name>, normalised;
  *   absorb/absorb.nrrd;
  *   detectors/detector_<i>.dat.
  * `nscatt` (may be NULL) receives the total scatter count. */
+#define SMCRT_ALL_DEVICES (-1)
 int smcrt_job_run(smcrt_job* job, int32_t device, const char* outdir, double* nscatt);
+/* smcrt_job_run over an explicit list of GPUs (photon shards + one RCCL reduce per batch). */
+int smcrt_job_run_devices(smcrt_job* job, const int32_t* devices, int32_t n_devices, const char* outdir,
+                          double* nscatt);
 
 /* The parsed [symmetry] / [inverse] tables and the detectors' inverseTarget values
  * (parse_detectors.f90:102, -1 when absent; desc.n_dets of them). */

@@ -5,7 +5,7 @@ against the library's own view of them.
 """
 import ctypes as C
 
-SMCRT_ABI_VERSION = 2
+SMCRT_ABI_VERSION = 3
 
 # smcrt_status
 OK = 0
@@ -180,6 +180,16 @@ class JobDesc(C.Structure):
                 ("source", Source), ("experiment", C.c_char * 64), ("source_name", C.c_char * 32)]
 
 
+# packed tally layout of the multi-GPU reduction (include/smcrt.h)
+PACK_JMEAN, PACK_ABSORB, PACK_EMISSION, PACK_DET_BINS = 1, 2, 4, 8
+UNIQUE_ID_BYTES = 128
+ALL_DEVICES = -1
+
+
+class PackLayout(C.Structure):
+    _fields_ = [("n_voxels", C.c_int64), ("n_det_bins", C.c_int64), ("fields", C.c_uint32), ("reserved", C.c_int32)]
+
+
 class KernelTimes(C.Structure):
     _fields_ = [("transport_ms", C.c_double), ("deposit_ms", C.c_double), ("launches", C.c_int64),
                 ("reserved", C.c_int64)]
@@ -195,4 +205,7 @@ EXPORTED_SYMBOLS = [
     "smcrt_escape_map", "smcrt_escape_run", "smcrt_scene_get_optprops", "smcrt_inverse_run", "smcrt_job_load_mode",
     "smcrt_job_escape_config", "smcrt_job_inverse_config", "smcrt_job_targets", "smcrt_job_run_escape",
     "smcrt_job_run_inverse", "smcrt_scene_fence",
+    "smcrt_pack_size", "smcrt_pack_host", "smcrt_unpack_host", "smcrt_comm_unique_id", "smcrt_comm_init_rank",
+    "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_multi_create", "smcrt_multi_info",
+    "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_destroy", "smcrt_job_run_devices",
 ]

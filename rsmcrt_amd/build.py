@@ -13,7 +13,7 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libsmcrt.so")
-SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp")]
+SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp", "multi.hip")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("transport.h", "detmath.h", "geometry.h", "deposit.h",
                                                          "hosterr.h", "toml.h", "mat4.h", "srcplan.h", "png.h", "scene_internal.h")] + [
     os.path.join(ROOT, "include", "smcrt.h")]
@@ -41,7 +41,7 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
-    cmd = [hipcc(), *FLAGS, "-o", LIB + ".tmp", *SOURCES, "-lz"]
+    cmd = [hipcc(), *FLAGS, "-o", LIB + ".tmp", *SOURCES, "-lz", "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

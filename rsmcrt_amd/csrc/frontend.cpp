@@ -880,13 +880,22 @@ extern "C" {
 // then finalise's normalisation and writes (:2321-2416) under `outdir` (the reference's
 // fileplace): jmean/<fluence>, emission/<render_source_name>, absorb/absorb.nrrd,
 // detectors/detector_<i>.dat. `io` (may be NULL) receives the tallies as well.
-int smcrt_job_run(smcrt_job* J0, int32_t device, const char* outdir, double* nscatt_out) {
+// `devices` empty: one scene on `device`; else one smcrt_multi over those GPUs (photon shards
+// + one RCCL reduce per checkpoint batch).
+static int job_run_impl(smcrt_job* J0, int32_t device, const std::vector<int32_t>& devices, const char* outdir,
+                        double* nscatt_out) {
   if (!J0 || !outdir) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
   smcrt_job* J = J0;
   std::unique_ptr<smcrt_job> ck;  // the checkpoint's job (load_checkpoint)
+  // state%ckptfile names the checkpoint for both the write and the read
+  // (kernelsMod.f90:54,1863); a relative name is resolved against outdir on both sides
+  auto ckpt_path = [&](const std::string& name) {
+    return (!name.empty() && name[0] != '/') ? std::string(outdir) + "/" + name : name;
+  };
   if (J0->loadckpt) {  // default_MCRT, kernelsMod.f90:51-71
-    std::ifstream f(J0->ckptfile, std::ios::binary);
-    if (!f) return ffail(SMCRT_ERR_INVALID_ARG, "cannot read checkpoint " + J0->ckptfile);
+    const std::string cin = ckpt_path(J0->ckptfile);
+    std::ifstream f(cin, std::ios::binary);
+    if (!f) return ffail(SMCRT_ERR_INVALID_ARG, "cannot read checkpoint " + cin);
     std::string l1, l2;
     std::getline(f, l1);
     std::getline(f, l2);
@@ -914,14 +923,19 @@ int smcrt_job_run(smcrt_job* J0, int32_t device, const char* outdir, double* nsc
     if (J->nphotons < 0) return ffail(SMCRT_ERR_INVALID_ARG, "checkpoint has more photons than the job");
   }
   smcrt_scene* scene = nullptr;
-  int st = smcrt_scene_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(),
-                              &J->grid, J->dets.empty() ? nullptr : J->dets.data(), (int32_t)J->dets.size(), device,
-                              &scene);
+  smcrt_multi* multi = nullptr;
+  const smcrt_detector* dp = J->dets.empty() ? nullptr : J->dets.data();
+  int st = devices.empty()
+               ? smcrt_scene_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(),
+                                    &J->grid, dp, (int32_t)J->dets.size(), device, &scene)
+               : smcrt_multi_create(J->nodes.data(), (int32_t)J->nodes.size(), J->top.data(), (int32_t)J->top.size(),
+                                    &J->grid, dp, (int32_t)J->dets.size(), devices.data(), (int32_t)devices.size(),
+                                    &multi);
   if (st) return st;
   const size_t nv = (size_t)J->grid.nx * J->grid.ny * J->grid.nz;
   std::vector<double> jm(nv, 0.0), ab(nv, 0.0), em(nv, 0.0);
   int64_t nb = 0;
-  smcrt_scene_det_bins(scene, &nb);
+  smcrt_scene_det_bins(scene ? scene : smcrt_multi_scene(multi, 0), &nb);
   std::vector<double> det_bins((size_t)std::max<int64_t>(1, nb), 0.0);
   double nscatt = 0.0;
   smcrt_tallies io;
@@ -941,20 +955,20 @@ int smcrt_job_run(smcrt_job* J0, int32_t device, const char* outdir, double* nsc
     const int64_t n = std::min<int64_t>(every, J->nphotons - done);
     cfg.n_photons = (uint64_t)n;
     cfg.first_photon = (uint64_t)done;
-    st = smcrt_run(scene, &J->src, &cfg, &io);
+    st = scene ? smcrt_run(scene, &J->src, &cfg, &io) : smcrt_multi_run(multi, &J->src, &cfg, &io);
     done += n;
     if (!st && done % every == 0 && J->ckptfreq > 0) {
       tmp.resize(nv);
       for (size_t i = 0; i < nv; ++i) tmp[i] = (float)jm[i];
       const size_t sl = J->toml_path.rfind('/');
       const std::string tname = sl == std::string::npos ? J->toml_path : J->toml_path.substr(sl + 1);
-      std::string cpath = J->ckptfile;
-      if (!cpath.empty() && cpath[0] != '/') cpath = std::string(outdir) + "/" + cpath;
+      const std::string cpath = ckpt_path(J->ckptfile);
       if (!mkdirs(outdir)) st = ffail(SMCRT_ERR_INVALID_ARG, std::string("cannot create ") + outdir);
       else st = smcrt_write_checkpoint(cpath.c_str(), tname.c_str(), done, tmp.data(), &J->grid, 1, nullptr, 0);
     }
   }
   smcrt_scene_destroy(scene);
+  smcrt_multi_destroy(multi);
   if (st) return st;
   if (nscatt_out) *nscatt_out = nscatt;
   std::vector<float> jmean(nv), absorb(nv), emission(nv);
@@ -962,6 +976,25 @@ int smcrt_job_run(smcrt_job* J0, int32_t device, const char* outdir, double* nsc
     jmean[i] = (float)jm[i]; absorb[i] = (float)ab[i]; emission[i] = (float)em[i];
   }
   return finalise_writes(J, outdir, jmean, absorb, emission, det_bins);
+}
+
+int smcrt_job_run(smcrt_job* J, int32_t device, const char* outdir, double* nscatt_out) {
+  if (device == SMCRT_ALL_DEVICES) {
+    int32_t n = 0;
+    const int st = smcrt_device_count(&n);
+    if (st) return st;
+    if (n < 1) return ffail(SMCRT_ERR_NO_DEVICE, "no HIP device");
+    std::vector<int32_t> all((size_t)n);
+    for (int32_t i = 0; i < n; ++i) all[(size_t)i] = i;
+    return job_run_impl(J, 0, all, outdir, nscatt_out);
+  }
+  return job_run_impl(J, device, {}, outdir, nscatt_out);
+}
+
+int smcrt_job_run_devices(smcrt_job* J, const int32_t* devices, int32_t n_devices, const char* outdir,
+                          double* nscatt_out) {
+  if (!devices || n_devices < 1) return ffail(SMCRT_ERR_INVALID_ARG, "no devices given");
+  return job_run_impl(J, 0, std::vector<int32_t>(devices, devices + n_devices), outdir, nscatt_out);
 }
 
 int smcrt_job_escape_config(const smcrt_job* J, smcrt_escape_config* out) {

@@ -108,12 +108,15 @@ int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_i
       want[0] = mus; want[1] = mua; want[2] = hgg; want[3] = n;
     }
     bool hit = false;
-    for (const Memo& m : memo)
-      if (std::memcmp(m.p, want, sizeof want) == 0) {
-        row[4 * M + (i - 1)] = m.err;
-        hit = true;
-        break;
-      }
+    // (with caller tallies every step runs, so `io` accumulates maxNumSteps runs as the
+    // reference's jmean does over its run_MCRT calls)
+    if (!io)
+      for (const Memo& m : memo)
+        if (std::memcmp(m.p, want, sizeof want) == 0) {
+          row[4 * M + (i - 1)] = m.err;
+          hit = true;
+          break;
+        }
     if (hit) continue;
     if (std::memcmp(want, cur, sizeof cur) != 0) {
       st = smcrt_scene_set_optprops(scene, idx, want[0], want[1], want[2], want[3]);

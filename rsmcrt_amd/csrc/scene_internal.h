@@ -1,5 +1,5 @@
 // scene_internal.h — library-internal accessors of smcrt_scene (defined in smcrt.hip) for
-// the host drivers (inverse.cpp). Not part of the C ABI.
+// the host drivers (inverse.cpp, multi.hip). Not part of the C ABI.
 #pragma once
 #include <stdint.h>
 
@@ -10,4 +10,7 @@ namespace smcrt {
 int scene_node_optprops(const smcrt_scene* s, int32_t top, double out[4]);
 // doubles of detector data detector d owns
 int scene_det_size(const smcrt_scene* s, int32_t d, int64_t* n);
+// the HIP device and the scene's own launch stream (a hipStream_t), for the multi-GPU driver
+int scene_device(const smcrt_scene* s);
+void* scene_stream(const smcrt_scene* s);
 }  // namespace smcrt

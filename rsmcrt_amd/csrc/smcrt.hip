@@ -1048,6 +1048,9 @@ int smcrt::scene_node_optprops(const smcrt_scene* s, int32_t i, double out[4]) {
   return SMCRT_OK;
 }
 
+int smcrt::scene_device(const smcrt_scene* s) { return s->device; }
+void* smcrt::scene_stream(const smcrt_scene* s) { return (void*)s->stream; }
+
 int smcrt::scene_det_size(const smcrt_scene* s, int32_t d, int64_t* n) {
   if (!s || d < 0 || d >= s->n_dets) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or detector");
   *n = (d + 1 < s->n_dets ? s->h_det_off[d + 1] : s->det_total) - s->h_det_off[d];
@@ -1376,8 +1379,13 @@ int smcrt_run_device(smcrt_scene* s, const smcrt_source* src, const smcrt_run_co
 }  // extern "C"
 
 // smcrt_run's body; `orun` (batched origins) is set by smcrt_run_origins. Caller holds s->mu.
-static int run_sync(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io,
+static int run_sync(smcrt_scene* s, const smcrt_source* src, const smcrt_run_config* cfg_in, smcrt_tallies* io,
                     const OriginRun* orun) {
+  // A synchronous run returns complete tallies: its folds always join s->stream before the
+  // copies, whatever the caller's flags say (SMCRT_FLAG_ASYNC_FOLD is for smcrt_run_device).
+  smcrt_run_config cfg_local = *cfg_in;
+  cfg_local.flags &= ~(uint32_t)SMCRT_FLAG_ASYNC_FOLD;
+  const smcrt_run_config* cfg = &cfg_local;
   const int64_t nv = (int64_t)s->grid.nx * s->grid.ny * s->grid.nz;
   const bool want[3] = {io->jmean || io->jmean_f64, io->absorb || io->absorb_f64, io->emission || io->emission_f64};
   if (!s->d_grids && (want[0] || want[1] || want[2])) {

@@ -73,6 +73,26 @@ def load_library(path: str = LIB_PATH):
         L.smcrt_escape_run.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.EscapeConfig),
                                        C.POINTER(abi.RunConfig), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                        C.POINTER(abi.Tallies)]
+        L.smcrt_pack_size.argtypes = [C.POINTER(abi.PackLayout), C.POINTER(C.c_int64)]
+        L.smcrt_pack_host.argtypes = [C.POINTER(abi.PackLayout), C.POINTER(abi.Tallies), C.POINTER(C.c_double)]
+        L.smcrt_unpack_host.argtypes = [C.POINTER(abi.PackLayout), C.POINTER(C.c_double), C.POINTER(abi.Tallies)]
+        L.smcrt_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+        L.smcrt_comm_init_rank.argtypes = [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32,
+                                           C.POINTER(C.c_void_p)]
+        L.smcrt_comm_destroy.argtypes = [C.c_void_p]
+        L.smcrt_comm_destroy.restype = None
+        L.smcrt_reduce_device_tallies.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.DeviceTallies), C.c_int32,
+                                                  C.c_void_p]
+        L.smcrt_multi_create.argtypes = [C.POINTER(abi.SdfNode), C.c_int32, C.POINTER(C.c_int32), C.c_int32,
+                                         C.POINTER(abi.Grid), C.POINTER(abi.Detector), C.c_int32,
+                                         C.POINTER(C.c_int32), C.c_int32, C.POINTER(C.c_void_p)]
+        L.smcrt_multi_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32)]
+        L.smcrt_multi_scene.argtypes = [C.c_void_p, C.c_int32]
+        L.smcrt_multi_scene.restype = C.c_void_p
+        L.smcrt_multi_run.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.RunConfig),
+                                      C.POINTER(abi.Tallies)]
+        L.smcrt_multi_destroy.argtypes = [C.c_void_p]
+        L.smcrt_multi_destroy.restype = None
         if L.smcrt_abi_version() != abi.SMCRT_ABI_VERSION:
             raise SmcrtError("libsmcrt.so ABI version mismatch")
         _lib = L
@@ -211,6 +231,12 @@ class Engine:
         _check(load_library().smcrt_run_device(self._h, C.byref(source), C.byref(cfg), C.byref(dev),
                                                C.c_void_p(stream)))
 
+    def reduce_device_tallies(self, comm: "Comm", dev: abi.DeviceTallies, root: int = -1, stream: int = 0):
+        """Sum this rank's device tallies over `comm` with one packed RCCL collective
+        (all-reduce for root < 0, else reduce onto rank `root`), asynchronously on `stream`."""
+        _check(load_library().smcrt_reduce_device_tallies(self._h, comm._h, C.byref(dev), int(root),
+                                                          C.c_void_p(stream)))
+
     def fence(self, stream: int = 0):
         """Make `stream` wait for the deposit folds of FLAG_ASYNC_FOLD launches."""
         _check(load_library().smcrt_scene_fence(self._h, C.c_void_p(stream)))
@@ -224,3 +250,105 @@ class Engine:
         t = abi.KernelTimes()
         _check(load_library().smcrt_scene_kernel_times(self._h, C.byref(t)))
         return {"transport_ms": t.transport_ms, "deposit_ms": t.deposit_ms, "launches": t.launches}
+
+
+def pack_layout(grid, n_det_bins: int, fields: int) -> abi.PackLayout:
+    lay = abi.PackLayout()
+    lay.n_voxels, lay.n_det_bins, lay.fields = grid.nx * grid.ny * grid.nz, int(n_det_bins), int(fields)
+    return lay
+
+
+def pack_result(res: Result, fields: int) -> np.ndarray:
+    """A host Result as the packed fp64 buffer of the multi-GPU reduction (smcrt_pack_host)."""
+    L = load_library()
+    lay = pack_layout(res.grid, sum(res.det_sizes), fields)
+    n = C.c_int64()
+    _check(L.smcrt_pack_size(C.byref(lay), C.byref(n)))
+    buf = np.zeros(n.value)
+    t = res.tallies()
+    _check(L.smcrt_pack_host(C.byref(lay), C.byref(t), buf.ctypes.data_as(C.POINTER(C.c_double))))
+    return buf
+
+
+def unpack_into(res: Result, buf: np.ndarray, fields: int) -> Result:
+    """Accumulate a packed buffer into a host Result (smcrt_unpack_host)."""
+    L = load_library()
+    lay = pack_layout(res.grid, sum(res.det_sizes), fields)
+    b = np.ascontiguousarray(buf, dtype=np.float64)
+    t = res.tallies()
+    _check(L.smcrt_unpack_host(C.byref(lay), b.ctypes.data_as(C.POINTER(C.c_double)), C.byref(t)))
+    return res
+
+
+class Comm:
+    """An RCCL communicator of one process per GPU (smcrt_comm_init_rank). Rank 0 makes the
+    id with `unique_id()`; the caller hands it to the other ranks out of band."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * abi.UNIQUE_ID_BYTES)()
+        _check(load_library().smcrt_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, n_ranks: int, rank: int, device: int):
+        buf = (C.c_uint8 * abi.UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check(load_library().smcrt_comm_init_rank(buf, int(n_ranks), int(rank), int(device), C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().smcrt_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class MultiEngine:
+    """One process driving several GPUs (smcrt_multi_*): photon shards per device, one packed
+    RCCL reduce per run. `run` has Engine.run's semantics (without photon records)."""
+
+    def __init__(self, scene, grid, dets=(), devices=None):
+        L = load_library()
+        self.scene, self.grid, self.dets = scene, grid, list(dets)
+        self._nodes = scene.node_array()
+        self._top = scene.top_array()
+        self._darr = detector_array(self.dets)
+        devs = None if devices is None else (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        _check(L.smcrt_multi_create(self._nodes, len(scene.nodes), self._top, scene.n_top, C.byref(grid),
+                                    self._darr, len(self.dets), devs, len(devices) if devices else 0, C.byref(h)))
+        self._h = h
+        n = C.c_int32()
+        _check(L.smcrt_multi_info(h, C.byref(n)))
+        self.n_devices = n.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load_library().smcrt_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def run(self, source, n_photons, seed=123456789, flags=abi.FLAG_PATHLENGTH, first_photon=0,
+            result: Result | None = None) -> Result:
+        res = result if result is not None else Result(self.grid, self.dets, n_photons)
+        res.n_photons += int(n_photons)
+        cfg = Engine.config(n_photons, seed, flags, first_photon)
+        t = res.tallies()
+        _check(load_library().smcrt_multi_run(self._h, C.byref(source), C.byref(cfg), C.byref(t)))
+        return res

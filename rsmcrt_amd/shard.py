@@ -15,6 +15,16 @@ def first_photon(step: int, rank: int, world: int, batch: int, base: int = 0) ->
 
 
 def reduce_tallies(tensors, dist, group=None) -> None:
-    """Sum tally buffers over ranks in place (RCCL over xGMI on GPUs, gloo on CPU)."""
-    for t in tensors:
-        dist.all_reduce(t, group=group)
+    """Sum tally buffers over ranks in place with ONE collective: the tensors are packed into
+    one fp64 buffer (integer counters travel as doubles, exact below 2^53), all-reduced, and
+    copied back. On GPUs the engine's own smcrt_reduce_device_tallies does the same inside
+    libsmcrt over RCCL; this torch form serves gloo (CPU) process groups."""
+    import torch
+    flat = [t.reshape(-1) for t in tensors]
+    buf = torch.cat([f.to(torch.float64) for f in flat])
+    dist.all_reduce(buf, group=group)
+    at = 0
+    for f in flat:
+        n = f.numel()
+        f.copy_(buf[at:at + n].to(f.dtype))
+        at += n

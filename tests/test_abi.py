@@ -63,6 +63,7 @@ STRUCTS = {
     "smcrt_tallies": (abi.Tallies, ["jmean", "jmean_f64", "det_bins", "counters", "records"]),
     "smcrt_device_tallies": (abi.DeviceTallies, ["jmean", "det_bins", "records"]),
     "smcrt_kernel_times": (abi.KernelTimes, ["transport_ms", "deposit_ms", "launches"]),
+    "smcrt_pack_layout": (abi.PackLayout, ["n_voxels", "n_det_bins", "fields"]),
     "smcrt_escape_config": (abi.EscapeConfig, ["symmetry", "n", "max", "pos", "dir", "rotation"]),
     "smcrt_inverse_config": (abi.InverseConfig, ["layer", "flags", "max_steps", "max_step_size", "accuracy", "seed"]),
 }

@@ -337,12 +337,12 @@ def test_job_checkpoint_write_and_resume(tmp_path):
     with Engine(builders.setup_scat_test(10.0), d.grid) as eng:
         r = eng.run(d.source, 20000, seed=d.seed)
     np.testing.assert_allclose(ck, r.jmean.astype(np.float32).reshape(-1), rtol=1e-6, atol=0)
-    # resume: load_checkpoint = true, pointing at that file
-    t2 = t1.replace("load_checkpoint=false", "load_checkpoint=true").replace(
-        'checkpoint_file="check.ckpt"', f'checkpoint_file="{out / "check.ckpt"}"')
-    assert "load_checkpoint=true" in t2
+    # resume: load_checkpoint = true with the same relative checkpoint_file, which names the
+    # file under the output directory for the read as for the write
+    t2 = t1.replace("load_checkpoint=false", "load_checkpoint=true")
+    assert "load_checkpoint=true" in t2 and 'checkpoint_file="check.ckpt"' in t2
     (tmp_path / "resume.toml").write_text(t2)
-    out2 = tmp_path / "run2"
+    out2 = out
     Job(str(tmp_path / "resume.toml")).run(out2)
     from tests.test_writers import read_nrrd_like_reference
     data, _ = read_nrrd_like_reference(out2 / "jmean" / "fluence.nrrd")

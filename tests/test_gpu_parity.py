@@ -478,3 +478,74 @@ def test_coop_eval_models_and_many_tops():
     gpu, cpu = both(sc, scene.grid(40, 40, 40, 1, 1, 1), src, 1500)
     compare(gpu, cpu)
     assert cpu.counter("fresnel") > 0
+
+
+def test_sync_run_ignores_async_fold_flag():
+    """smcrt_run is synchronous: a caller that passes FLAG_ASYNC_FOLD (meant for
+    smcrt_run_device) still gets complete tallies, and back-to-back runs do not race the
+    previous run's fold (run_sync masks the flag)."""
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(64, 64, 64, 1, 1, 1)
+    src = scene.point_source()
+    with Engine(sc, g) as eng:
+        a = eng.run(src, 400_000, seed=SEED, flags=abi.FLAG_PATHLENGTH | abi.FLAG_ASYNC_FOLD)
+        b = eng.run(src, 400_000, seed=SEED, flags=abi.FLAG_PATHLENGTH | abi.FLAG_ASYNC_FOLD)
+        c = eng.run(src, 400_000, seed=SEED)
+    for r in (a, b):
+        np.testing.assert_allclose(r.jmean, c.jmean, rtol=1e-12, atol=1e-300)
+        assert r.counters_dict() == c.counters_dict()
+
+
+def test_multi_device_run_matches_single():
+    """smcrt_multi_run (photon shards over the visible GPUs + one packed RCCL reduce onto the
+    first) gives smcrt_run's result: counters, absorb and detector bins bit-exact, jmean to
+    the fp64 summation order of the folds (which is not fixed run to run either). On a
+    one-GPU box this is the n_devices = 1 path through RCCL."""
+    from rsmcrt_amd.engine import MultiEngine
+    sc = builders.skin_layers()
+    g = scene.grid(64, 64, 64, 0.05, 0.05, 0.05)
+    src = scene.pencil_source((0.0, 0.0, 0.0499), (0.0, 0.0, -1.0))
+    dets = [scene.circle_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.05, 50)]
+    with MultiEngine(sc, g, dets) as me:
+        assert me.n_devices >= 1
+        a = me.run(src, 200_000, seed=SEED, first_photon=17)
+        me.run(src, 50_000, seed=SEED, first_photon=200_017, result=a)
+    with Engine(sc, g, dets) as eng:
+        b = eng.run(src, 250_000, seed=SEED, first_photon=17)
+    assert a.counters_dict() == b.counters_dict()
+    assert np.array_equal(a.absorb, b.absorb)
+    assert np.array_equal(a.det_bins, b.det_bins)
+    np.testing.assert_allclose(a.jmean, b.jmean, rtol=1e-12, atol=1e-300)
+    assert a.nscatt[0] == b.nscatt[0]
+
+
+def test_reduce_device_tallies_one_rank():
+    """smcrt_reduce_device_tallies on a one-rank communicator (the multi-process path bench.py
+    takes under torchrun): the packed all-reduce leaves every field as it was, counters
+    included (they travel as doubles)."""
+    import torch
+    from rsmcrt_amd.engine import Comm
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(32, 32, 32, 1, 1, 1)
+    src = scene.point_source()
+    dev = torch.device("cuda", 0)
+    nv = 32 ** 3
+    jm = torch.zeros(nv, dtype=torch.float64, device=dev)
+    ab = torch.zeros(nv, dtype=torch.float64, device=dev)
+    ns = torch.zeros(1, dtype=torch.float64, device=dev)
+    ctr = torch.zeros(abi.NCOUNTERS, dtype=torch.int64, device=dev)
+    dt = abi.DeviceTallies()
+    dt.jmean, dt.absorb, dt.nscatt, dt.counters = jm.data_ptr(), ab.data_ptr(), ns.data_ptr(), ctr.data_ptr()
+    stream = torch.cuda.current_stream()
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    with Engine(sc, g) as eng:
+        eng.run_device(src, Engine.config(100_000, seed=SEED), dt, stream.cuda_stream)
+        torch.cuda.synchronize()
+        before = (jm.clone(), ab.clone(), ns.clone(), ctr.clone())
+        for root in (-1, 0):
+            eng.reduce_device_tallies(comm, dt, root=root, stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+    comm.close()
+    for x, y in zip((jm, ab, ns, ctr), before):
+        assert torch.equal(x, y)
+    assert int(ctr[abi.CTR["photons"]]) == 100_000

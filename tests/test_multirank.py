@@ -47,6 +47,77 @@ def _worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
+def _packed_worker(rank, world, port, out_dir):
+    """The library's packed layout (smcrt_pack_host / smcrt_unpack_host, the buffer
+    smcrt_reduce_device_tallies and smcrt_multi_run reduce over RCCL) reduced with ONE gloo
+    all-reduce."""
+    from oracle import pyoracle as O
+    from rsmcrt_amd import engine
+    from rsmcrt_amd.tallies import Result
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+        g = scene.grid(GRID, GRID, GRID, 1.0, 1.0, 1.0)
+        dets = [scene.circle_dect((0.0, 0.0, 0.9), (0.0, 0.0, 1.0), 1, 1.0, 20)]
+        res = Result(g, dets)
+        for s in range(STEPS):
+            O.run(sc, g, scene.point_source(), BATCH, dets=dets,
+                  first_photon=shard.first_photon(s, rank, world, BATCH), result=res)
+        fields = abi.PACK_JMEAN | abi.PACK_ABSORB | abi.PACK_DET_BINS
+        buf = torch.from_numpy(engine.pack_result(res, fields))
+        dist.all_reduce(buf)  # the one collective
+        if rank == 0:
+            tot = engine.unpack_into(Result(g, dets), buf.numpy(), fields)
+            np.savez(os.path.join(out_dir, "packed.npz"), jmean=tot.jmean, absorb=tot.absorb, det=tot.det_bins,
+                     nscatt=tot.nscatt, counters=tot.counters, n=buf.numel())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_packed_layout_matches_single_rank(tmp_path, lib_path):
+    from oracle import pyoracle as O
+    world = 2
+    mp.spawn(_packed_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = np.load(tmp_path / "packed.npz")
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(GRID, GRID, GRID, 1.0, 1.0, 1.0)
+    dets = [scene.circle_dect((0.0, 0.0, 0.9), (0.0, 0.0, 1.0), 1, 1.0, 20)]
+    ref = O.run(sc, g, scene.point_source(), STEPS * world * BATCH, dets=dets)
+    # layout: 2 grids + 21 detector bins + nscatt + 24 moments + 16 counters
+    assert int(got["n"]) == 2 * GRID ** 3 + 21 + 1 + 24 + abi.NCOUNTERS
+    assert np.array_equal(got["counters"], ref.counters)
+    assert np.array_equal(got["absorb"], ref.absorb)
+    np.testing.assert_allclose(got["jmean"], ref.jmean, rtol=1e-12, atol=0)
+    np.testing.assert_allclose(got["det"], ref.det_bins, rtol=1e-12, atol=0)
+    assert got["nscatt"][0] == ref.nscatt[0] and ref.counter("detector_hits") > 0
+
+
+def test_pack_roundtrip_host(lib_path):
+    """smcrt_pack_host -> smcrt_unpack_host accumulates every field (no GPU)."""
+    from rsmcrt_amd import engine
+    from rsmcrt_amd.tallies import Result
+    g = scene.grid(5, 4, 3, 1.0, 1.0, 1.0)
+    dets = [scene.circle_dect((0.0, 0.0, 0.9), (0.0, 0.0, 1.0), 1, 1.0, 7)]
+    r = Result(g, dets)
+    rng = np.random.default_rng(1)
+    r.jmean[...] = rng.random(r.jmean.shape)
+    r.emission[...] = rng.random(r.jmean.shape)
+    r.det_bins[...] = rng.random(r.det_bins.shape)
+    r.nscatt[0], r.moments[...] = 12.5, rng.random(24)
+    r.counters[...] = np.arange(abi.NCOUNTERS, dtype=np.uint64) * np.uint64(10 ** 12)
+    fields = abi.PACK_JMEAN | abi.PACK_EMISSION | abi.PACK_DET_BINS
+    buf = engine.pack_result(r, fields)
+    assert buf.size == 2 * 60 + 8 + 1 + 24 + abi.NCOUNTERS
+    out = Result(g, dets)
+    engine.unpack_into(out, buf, fields)
+    engine.unpack_into(out, buf, fields)
+    assert np.array_equal(out.jmean, 2 * r.jmean) and np.array_equal(out.emission, 2 * r.emission)
+    assert not out.absorb.any()  # not packed
+    assert np.array_equal(out.det_bins, 2 * r.det_bins) and out.nscatt[0] == 25.0
+    assert np.array_equal(out.counters, 2 * r.counters)
+
+
 def test_shard_ranges_disjoint_and_complete():
     for world in (1, 2, 4, 8):
         seen = []

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--traffic", help="write profiles/transport_traffic.json-style file here")
     ap.add_argument("--batch", type=int, default=4_000_000)
     ap.add_argument("--grid", type=int, default=128)
+    ap.add_argument("--workload", default="m1")
     a = ap.parse_args()
     out = {}
     tr = find(a.dir, "trace", "kernel_trace") or os.path.join(a.dir, "kernel_trace.csv")
@@ -85,11 +86,20 @@ def main():
     if a.traffic:
         k = next((k for k in out if k.startswith("transport_kernel") and "hbm_bytes_per_dispatch" in out[k]), None)
         if k:
+            # the whole step: the transport kernel plus the deposit-fold kernels that follow each
+            # of its launches (same dispatch count), per launch
+            step = {kk: out[kk]["hbm_bytes_per_dispatch"] for kk in out
+                    if (kk == k or kk.startswith("bin_") or kk.startswith("dda_") or kk.startswith("fold_"))
+                    and "hbm_bytes_per_dispatch" in out[kk]}
+            classes = {c: out[k][c] for c in out[k] if c.startswith("SQ_INSTS_VALU_")}
             with open(a.traffic, "w") as f:
-                json.dump({"batch": a.batch, "grid": a.grid, "kernel": k,
+                json.dump({"workload": a.workload, "batch": a.batch, "grid": a.grid, "kernel": k,
                            "hbm_bytes_per_launch": out[k]["hbm_bytes_per_dispatch"],
+                           "step_hbm_bytes_per_launch": sum(step.values()),
+                           "hbm_bytes_per_launch_by_kernel": step,
                            "valu_insts_per_launch": out[k].get("SQ_INSTS_VALU"),
                            "salu_insts_per_launch": out[k].get("SQ_INSTS_SALU"),
+                           "valu_classes": classes,
                            "avg_ms": out[k]["avg_ms_last"], "source": os.path.relpath(a.dir)}, f, indent=1)
     if a.json:
         with open(a.json, "w") as f:
