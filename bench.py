@@ -214,6 +214,56 @@ def valu_roofline(pmc, kern_ms):
             "salu_insts_per_launch": pmc.get("salu_insts_per_launch"), "source": pmc.get("source")}
 
 
+def reference_pinned(device):
+    """Spatial tallies of the HIP path against targets the reference itself holds (labelled
+    reference-pinned, separate from the GPU == port parity above; tests/test_reference_targets.py
+    holds the acceptance rules): the RI-mismatch absorb-depth fits of
+    tools/validateRIMismatch.py:28-46 (res/validation2.toml, validation3.toml, 1e6 photons)
+    and the fibre collection efficiency of tools/validateFibreDect.py:25 (1e6 photons)."""
+    import numpy as np
+    from rsmcrt_amd import scene as S
+    from rsmcrt_amd.engine import Engine
+    from rsmcrt_amd.job import Job
+    from tests import refval
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats.json")) as f:
+        kats = json.load(f)
+    out = {}
+
+    def job_scene(j):
+        sc = S.Scene([])
+        sc.nodes = [j.nodes[i] for i in range(j.desc.n_nodes)]
+        sc.top = list(j.top[:j.desc.n_top])
+        return sc
+
+    for which in ("validation2", "validation3"):
+        j = Job(os.path.join(ROOT, "tests", "golden", "res", f"{which}.toml"))
+        d = j.desc
+        g = S.grid(5, 5, d.grid.nz, d.grid.xmax, d.grid.ymax, d.grid.zmax)
+        with Engine(job_scene(j), g, device=device) as eng:
+            r = eng.run(d.source, d.n_photons, seed=d.seed)
+        sums = r.absorb.sum(axis=(1, 2))
+        dz = 2 * g.zmax / g.nz
+        depths, fit = refval.ri_fit(kats, which)
+        sim = refval.to_reference_units(sums, d.n_photons, dz)
+        sig = refval.to_reference_units(np.sqrt(np.maximum(sums, 1.0)), d.n_photons, dz)
+        ok, rep = refval.compare_profile(sim, fit, depths, sig)
+        out[f"{which}_absorb_depth_vs_fit"] = {"photons": d.n_photons, "rel_rms": rep["rel_rms"],
+                                               "integral_ratio": rep["integral_ratio"], "bins": rep["bins"],
+                                               "bins_outside_4sigma_plus_5pct": len(rep["failed"]), "pass": ok}
+    j = Job(os.path.join(ROOT, "tests", "golden", "res", "validateFibreDect.toml"))
+    d = j.desc
+    g = S.grid(20, 20, 20, d.grid.xmax, d.grid.ymax, d.grid.zmax)
+    with Engine(job_scene(j), g, j.detectors, device=device) as eng:
+        r = eng.run(d.source, d.n_photons, seed=d.seed)
+    a, p = refval.fibre_expected(kats)
+    eff = np.array([r.detector(i).sum() / d.n_photons for i in range(10)])
+    ok, z = refval.fibre_check(eff, p, d.n_photons)
+    out["fibre_collection_efficiency"] = {"photons": d.n_photons, "max_abs_z": float(np.max(np.abs(z))),
+                                          "max_rel_err": float(np.max(np.abs(eff - p) / p)), "pass": ok}
+    out["source"] = "tools/validateRIMismatch.py:28-46, tools/validateFibreDect.py:25 (reference_kats.json)"
+    return out
+
+
 def escape_bench(args):
     """Escape function on res/default.toml's scene and detectors (a 50x62x64 scattering box,
     11 annulus detectors) with its 360rotational symmetry on a reduced symmetry grid. The GPU
@@ -303,6 +353,7 @@ def main():
     ap.add_argument("--cpu1-seconds", type=float, default=8.0, help="the 1-core CPU leg (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = this process's CPU share, <= 16")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-ref", action="store_true", help="skip the reference-pinned spatial checks")
     ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
     ap.add_argument("--sync-fold", action="store_true", help="diagnostic: each step waits for its own fold")
     ap.add_argument("--source", default="default", choices=["default", "uniform"],
@@ -479,6 +530,9 @@ def main():
             out["cpu_baseline_1core"] = one
             out["gpu_over_cpu_1core"] = out["value"] / one["value"]
         out["gpu_over_cpu"] = out["value"] / base["value"]
+    if rank == 0 and world == 1 and not args.no_ref:
+        log("[bench] reference-pinned spatial checks (validation2/3 absorb depth, fibre efficiency)")
+        out.setdefault("parity", {})["reference_pinned"] = reference_pinned(torch.cuda.current_device())
     if rank == 0:
         print(json.dumps(out), flush=True)
     eng.close()
