@@ -347,6 +347,257 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
   }
 }
 
+// =============================================================================================
+// Tile buckets: the transport kernel files each record straight into a bucket of its tile,
+// so the fold reads every record once and writes nothing back (16 B of HBM traffic per
+// deposit: the record's write and its read; the sorted path above moves 40 B).
+//
+// A bucket is BUCKET_RECORDS consecutive pool slots that hold records of one tile only.
+// Every wave keeps, in LDS, one open bucket per tile (id + fill) and takes bucket ids from a
+// wave-private batch of BUCKET_BATCH ids (one returning atomic per batch). A deposit is an
+// LDS add-and-return on its tile's fill plus one 8-B store; only the deposit that fills a
+// bucket takes the rare slow path (claim the next id, record the full bucket).
+// The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
+constexpr uint32_t BUCKET_SHIFT = 8;
+constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
+constexpr uint32_t BUCKET_BATCH = 64;                    // ids a wave takes at a time
+constexpr uint32_t BUCKET_NONE = 0xFFFFFFFFu;            // no bucket open for the tile yet
+constexpr uint32_t BUCKET_EXHAUSTED = 0xFFFFFFFEu;       // pool full: the tile's deposits use atomics
+constexpr uint32_t TILE_INVALID = 0xFFFFFFFFu;           // bucket_tile of an id never used
+constexpr uint32_t FILL_EXHAUSTED = 0x40000000u;         // fill of an exhausted tile: always "over"
+constexpr uint32_t MAX_DIRECT_TILES = 512;               // 8 B of LDS per tile per wave
+constexpr uint32_t MIN_PIECE_BUCKETS = MIN_PIECE_RECORDS / BUCKET_RECORDS;
+
+// Wave-uniform batch of bucket ids [next, end) (scalar registers).
+struct BucketLog {
+  uint32_t next, end;
+};
+
+// Per-wave LDS state: bf[t] = records in tile t's open bucket (BUCKET_RECORDS: none open),
+// bi[t] = its id. Call in wave-uniform control flow.
+__device__ __forceinline__ void init_buckets(uint32_t* bf, uint32_t* bi, uint32_t n_tiles) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t t = lane; t < n_tiles; t += 64) {
+    bf[t] = BUCKET_RECORDS;
+    bi[t] = BUCKET_NONE;
+  }
+}
+
+__device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __restrict__ C, BucketLog& W,
+                                                      bool over, uint32_t pos, uint32_t t, unsigned long long rec,
+                                                      uint32_t vox, double val, uint32_t& overflow, uint32_t* bf,
+                                                      uint32_t* bi) {
+  const int lane = threadIdx.x & 63;
+  // The deposit that found its tile's fill at exactly BUCKET_RECORDS claims the next bucket;
+  // the others of this instruction that overflowed the same tile follow it into the new one.
+  const bool claim = over && pos == BUCKET_RECORDS;
+  const uint64_t cm = __ballot(claim);
+  const uint32_t nc = (uint32_t)__popcll(cm);
+  uint32_t next = uniform(W.next), end = uniform(W.end);
+  if (nc > end - next) {  // batch used up: retire its unused ids, take a new batch
+    const uint32_t id = next + lane;
+    if (id < end && id < K.n_buckets) C->bucket_tile[id] = TILE_INVALID;
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(C->dep_ctl, BUCKET_BATCH);
+    base = uniform(__shfl(base, 0, 64));
+    next = base;
+    end = base + BUCKET_BATCH;
+  }
+  if (claim) {
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+    const uint32_t nb = next + rank;
+    const uint32_t old = __hip_atomic_load(bi + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (old < K.n_buckets) C->bucket_fill[old] = BUCKET_RECORDS;  // the full bucket
+    if (nb < K.n_buckets) {
+      C->bucket_tile[nb] = t;
+      atomicAdd(C->tile_nb + t, 1u);
+      __hip_atomic_store(bi + t, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      atomicSub(bf + t, BUCKET_RECORDS);  // -> the number that overflowed into it
+    } else {
+      __hip_atomic_store(bi + t, BUCKET_EXHAUSTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(bf + t, FILL_EXHAUSTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+  }
+  W.next = next + nc;
+  W.end = end;
+  __builtin_amdgcn_wave_barrier();
+  bool spill = false;
+  if (over) {
+    const uint32_t b = __hip_atomic_load(bi + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (b < K.n_buckets && pos - BUCKET_RECORDS < BUCKET_RECORDS) {
+      K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos - BUCKET_RECORDS)] = rec;
+    } else {  // pool exhausted: stay correct with fp64 atomics
+      atomic_add_nr(C->jmean + vox, val);
+      spill = true;
+    }
+  }
+  overflow += (uint32_t)__popcll(__ballot(spill));
+}
+
+__device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __restrict__ C, BucketLog& W, bool dep,
+                                              uint32_t vox, double val, uint32_t& overflow, uint32_t* bf,
+                                              uint32_t* bi) {
+  if (!__ballot(dep)) return;
+  const uint32_t t = vox >> TILE_SHIFT;
+  const unsigned long long rec = pack_record(vox, val);
+  uint32_t pos = 0;
+  if (dep) pos = atomicAdd(bf + t, 1u);
+  const bool over = dep && pos >= BUCKET_RECORDS;
+  if (dep && !over) {
+    const uint32_t b = __hip_atomic_load(bi + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + pos] = rec;
+  }
+  if (__ballot(over)) bucket_slow(K, C, W, over, pos, t, rec, vox, val, overflow, bf, bi);
+}
+
+// End of the kernel for one wave: record the fill of every open bucket and retire the unused
+// ids of the batch; add the wave's record and overflow counts.
+__device__ __forceinline__ void close_buckets(const KParams& K, const KCold* __restrict__ C, const BucketLog& W,
+                                              uint32_t records, uint32_t overflow, const uint32_t* bf,
+                                              const uint32_t* bi) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t t = lane; t < K.bucket_tiles; t += 64) {
+    const uint32_t b = bi[t];
+    if (b < K.n_buckets) C->bucket_fill[b] = bf[t] < BUCKET_RECORDS ? bf[t] : BUCKET_RECORDS;
+  }
+  const uint32_t id = W.next + lane;
+  if (id < W.end && id < K.n_buckets) C->bucket_tile[id] = TILE_INVALID;
+  if (lane == 0) {
+    if (records) atomicAdd(C->dep_ctl + 3, records);
+    if (overflow) atomicAdd(C->dep_ctl + 1, overflow);
+  }
+}
+
+// ---- bk_scan: bucket offsets per tile and the reduce pieces (one block) --------------------
+// tile_nb[t] buckets of tile t -> tile_start[t] (exclusive scan), cursor[t] = tile_start[t];
+// pieces of at most `pb` buckets of one tile. dep_ctl[2] = pieces.
+__global__ __launch_bounds__(1024) void bk_scan(const uint32_t* __restrict__ tile_nb, uint32_t n_tiles,
+                                                uint32_t* __restrict__ tile_start, uint32_t* __restrict__ cursor,
+                                                Piece* __restrict__ pieces, uint32_t* __restrict__ dep_ctl) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t per = (n_tiles + blockDim.x - 1) / blockDim.x;
+  const uint32_t t0 = threadIdx.x * per < n_tiles ? threadIdx.x * per : n_tiles;
+  const uint32_t t1 = t0 + per < n_tiles ? t0 + per : n_tiles;
+  uint32_t s = 0;
+  for (uint32_t t = t0; t < t1; ++t) s += tile_nb[t];
+  uint32_t all_s, all_np;
+  uint32_t off = block_exscan(s, wsum, &all_s);
+  const uint32_t want = all_s / REDUCE_PIECES + 1;
+  const uint32_t pb = want > MIN_PIECE_BUCKETS ? want : MIN_PIECE_BUCKETS;
+  uint32_t np = 0;
+  for (uint32_t t = t0; t < t1; ++t) np += (tile_nb[t] + pb - 1) / pb;
+  uint32_t pc = block_exscan(np, wsum, &all_np);
+  if (threadIdx.x == 0) dep_ctl[2] = all_np;
+  for (uint32_t t = t0; t < t1; ++t) {
+    const uint32_t c = tile_nb[t];
+    tile_start[t] = off;
+    cursor[t] = off;
+    for (uint32_t k = 0; k < c; k += pb) {
+      Piece p;
+      p.tile = t; p.start = off + k; p.count = (c - k) < pb ? (c - k) : pb; p.pad = 0;
+      pieces[pc++] = p;
+    }
+    off += c;
+  }
+}
+
+// ---- bk_place: bucket ids in tile order ------------------------------------------------------
+// Block b takes a contiguous range of ids in passes of BIN_THREADS * 8: LDS ranks per tile,
+// one global reservation per (pass, tile), then the ids are written to order[].
+__global__ __launch_bounds__(BIN_THREADS) void bk_place(const uint32_t* __restrict__ bucket_tile,
+                                                        const uint32_t* __restrict__ dep_ctl, uint32_t n_buckets,
+                                                        uint32_t n_tiles, uint32_t* __restrict__ cursor,
+                                                        uint32_t* __restrict__ order) {
+  __shared__ uint32_t cnt[MAX_DIRECT_TILES];
+  __shared__ uint32_t base[MAX_DIRECT_TILES];
+  const uint32_t used = dep_ctl[0] < n_buckets ? dep_ctl[0] : n_buckets;
+  const uint32_t per = (used + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = blockIdx.x * per;
+  const uint32_t b1 = b0 + per < used ? b0 + per : used;
+  constexpr int PER_THREAD = 8;
+  for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) cnt[t] = 0;
+  __syncthreads();
+  for (uint32_t p = b0; p < b1; p += BIN_THREADS * PER_THREAD) {
+    uint32_t tile[PER_THREAD], rank[PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < PER_THREAD; ++k) {
+      const uint32_t i = p + threadIdx.x + k * BIN_THREADS;
+      tile[k] = i < b1 ? bucket_tile[i] : TILE_INVALID;
+      rank[k] = tile[k] < n_tiles ? atomicAdd(&cnt[tile[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
+      const uint32_t c = cnt[t];
+      base[t] = c ? atomicAdd(cursor + t, c) : 0u;
+      cnt[t] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER_THREAD; ++k) {
+      const uint32_t i = p + threadIdx.x + k * BIN_THREADS;
+      if (tile[k] < n_tiles) order[base[tile[k]] + rank[k]] = i;
+    }
+    __syncthreads();
+  }
+}
+
+// ---- bk_reduce: one piece (buckets of one tile) per block, fp64 LDS sums into jmean --------
+// (blockDim.x must be 1024)
+constexpr uint32_t REDUCE_STAGE_BUCKETS = 256;
+__global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __restrict__ pool,
+                                                  const uint32_t* __restrict__ order,
+                                                  const uint32_t* __restrict__ bucket_fill,
+                                                  const Piece* __restrict__ pieces,
+                                                  const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
+                                                  double* __restrict__ jmean) {
+  __shared__ double acc[TILE_VOXELS];
+  __shared__ uint32_t ids[REDUCE_STAGE_BUCKETS], fills[REDUCE_STAGE_BUCKETS];
+  const uint32_t n_pieces = dep_ctl[2];
+  for (uint32_t pi = blockIdx.x; pi < n_pieces; pi += gridDim.x) {
+    const Piece p = pieces[pi];
+    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) acc[i] = 0.0;
+    for (uint32_t k0 = 0; k0 < p.count; k0 += REDUCE_STAGE_BUCKETS) {
+      const uint32_t kn = p.count - k0 < REDUCE_STAGE_BUCKETS ? p.count - k0 : REDUCE_STAGE_BUCKETS;
+      __syncthreads();
+      if (threadIdx.x < kn) {
+        const uint32_t b = order[p.start + k0 + threadIdx.x];
+        ids[threadIdx.x] = b;
+        fills[threadIdx.x] = bucket_fill[b];
+      }
+      __syncthreads();
+      const uint32_t slots = kn << BUCKET_SHIFT;
+      uint32_t s = threadIdx.x;
+      for (; s + 7 * 1024 < slots; s += 8 * 1024) {  // 8 loads in flight per thread
+        unsigned long long x[8];
+        bool v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t j = s + k * 1024, kb = j >> BUCKET_SHIFT, r = j & (BUCKET_RECORDS - 1);
+          v[k] = r < fills[kb];
+          x[k] = v[k] ? pool[((uint64_t)ids[kb] << BUCKET_SHIFT) + r] : 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (v[k]) atomicAdd(&acc[(uint32_t)(x[k] >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x[k]));
+      }
+      for (; s < slots; s += 1024) {
+        const uint32_t kb = s >> BUCKET_SHIFT, r = s & (BUCKET_RECORDS - 1);
+        if (r < fills[kb]) {
+          const unsigned long long x = pool[((uint64_t)ids[kb] << BUCKET_SHIFT) + r];
+          atomicAdd(&acc[(uint32_t)(x >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x));
+        }
+      }
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)p.tile << TILE_SHIFT;
+    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) {
+      const double a = acc[i];
+      if (a != 0.0 && base + i < n_voxels) atomic_add_nr(jmean + base + i, a);
+    }
+    __syncthreads();
+  }
+}
+
 // ---- bin_reduce: one tile piece per block, fp64 LDS sums added into jmean ----------------
 // (blockDim.x must be 1024)
 __global__ __launch_bounds__(1024) void bin_reduce(const unsigned long long* __restrict__ sorted,

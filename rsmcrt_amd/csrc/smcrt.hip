@@ -98,8 +98,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   }
   double* const startp = sh_dyn + hist_off + threadIdx.x;  // [3][256] when n_dets > 0
   if (K.n_dets) hist_off += 3 * 256;
-  uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * K.hist_tiles;
-  for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
+  // per-wave deposit state: the sorted path's tile histogram (hist_tiles words) or the
+  // bucketed path's open bucket per tile (fill | id: 2 * bucket_tiles words)
+  const uint32_t wave_words = K.bucket_tiles ? 2 * K.bucket_tiles : K.hist_tiles;
+  uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * wave_words;
+  uint32_t* const bfill = whist;
+  uint32_t* const bid = whist + K.bucket_tiles;
+  if (K.bucket_tiles) init_buckets(bfill, bid, K.bucket_tiles);
+  else
+    for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
 #pragma unroll
   for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
 #pragma unroll
@@ -117,6 +124,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   const bool binned = K.rec_pool != nullptr;  // (set only when jmean is tallied)
   RecLog W;
   W.chunk = LOG_NONE; W.fill = 0;
+  BucketLog WB;
+  WB.next = WB.end = 0;
   uint32_t overflow = 0;
   uint32_t w_dep = 0, w_sdf = 0, w_iters = 0;  // wave totals (scalar registers)
   uint64_t chunk_base = 0;  // wave-uniform photon chunk
@@ -396,7 +405,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 #ifdef SMCRT_ABL_NO_EMIT  // timing ablation only: deposits are computed but dropped
         if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, C, W, dep, vox, val, overflow, whist); }
 #else
-        if (binned) emit_deposits(K, C, W, dep, vox, val, overflow, whist);
+        if (binned) {
+          if (K.bucket_tiles) emit_bucketed(K, C, WB, dep, vox, val, overflow, bfill, bid);
+          else emit_deposits(K, C, W, dep, vox, val, overflow, whist);
+        }
 #endif
         else if (dep) {
           double* const jm = C->jmean;
@@ -576,7 +588,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     }
   }
 
-  if (binned) close_log(K, C, W, overflow, whist);
+  if (binned) {
+    if (K.bucket_tiles) close_buckets(K, C, WB, w_dep - overflow, overflow, bfill, bid);
+    else close_log(K, C, W, overflow, whist);
+  }
 
 #ifdef SMCRT_DIAG
   if (lane_id == 0) {
@@ -701,12 +716,17 @@ struct smcrt_scene {
   bool lds_faces = false;
   size_t face_bytes = 0;
   uint32_t hist_tiles = 0;  // fused tile histogram in the transport kernel (0: bin_hist kernel)
+  bool bucketed = false;    // records go straight into per-tile buckets (deposit.h); else sorted path
   // binned jmean deposition (deposit.h)
   uint32_t n_tiles = 0;
   // Two record-log slots, used by alternate launches: the fold of launch k (on fstream)
   // reads its slot while launch k+1's transport kernel fills the other.
   unsigned long long* d_pool[2] = {nullptr, nullptr};  // record log, cap records
   unsigned long long* d_sorted = nullptr;  // tile-sorted records (folds are serial on fstream)
+  // bucketed path: per slot the tile of each bucket id (bucket fills use d_chunk_fill, the
+  // per-tile bucket counts d_bin_counts); shared by the serial folds: ids in tile order
+  uint32_t* d_bucket_tile[2] = {nullptr, nullptr};
+  uint32_t* d_order = nullptr;
   uint32_t* d_chunk_fill[2] = {nullptr, nullptr};
   uint32_t* d_dep_ctl[2] = {nullptr, nullptr};  // [0] chunks taken [1] overflow [2] pieces [3] records
   uint32_t* d_tile_count = nullptr;  // n_tiles
@@ -726,6 +746,7 @@ struct smcrt_scene {
   hipEvent_t ctl_ev[2] = {nullptr, nullptr};
   bool ctl_pending[2] = {false, false};
   bool force_atomic = false;  // SMCRT_DEPOSIT=atomic
+  uint64_t pool_cap_chunks = 0;  // SMCRT_POOL_CAP (records; tests of pool exhaustion): 0 = none
   // smcrt_scene_kernel_times: event quads (before / after transport on the launch stream,
   // before / after the deposit fold on fstream) of the launches since the last harvest
   bool timing = false;
@@ -777,10 +798,12 @@ static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
 }
 
 // Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
-static size_t transport_lds(const smcrt_scene* s, uint32_t hist_tiles) {
+static size_t transport_lds(const smcrt_scene* s, uint32_t wave_words) {
   return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
-         (size_t)4 * hist_tiles * sizeof(uint32_t);
+         (size_t)4 * wave_words * sizeof(uint32_t);
 }
+// LDS words per wave of the deposit state (deposit.h): open buckets or the tile histogram.
+static uint32_t wave_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_tiles : s->hist_tiles; }
 
 static TopProps make_props(const smcrt_sdf_node& nd) {
   TopProps p;  // init_mono, opticalProperties.f90:107-125
@@ -816,7 +839,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1],
                   s->d_dep_ctl[0], s->d_dep_ctl[1], s->d_tile_count, s->d_tile_start, s->d_bin_counts[0],
-                  s->d_bin_counts[1], s->d_pieces};
+                  s->d_bin_counts[1], s->d_pieces, s->d_bucket_tile[0], s->d_bucket_tile[1], s->d_order};
   for (int i = 0; i < 2; ++i) {
     if (s->ctl_ev[i]) (void)hipEventDestroy(s->ctl_ev[i]);
     if (s->ev_f[i]) (void)hipEventDestroy(s->ev_f[i]);
@@ -956,6 +979,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     s->n_tiles = (tiles <= MAX_TILES && nv < 0xFFFFFFFFull) ? (uint32_t)tiles : 0;
     const char* fa = std::getenv("SMCRT_DEPOSIT");
     s->force_atomic = fa && std::string(fa) == "atomic";
+    if (const char* pc = std::getenv("SMCRT_POOL_CAP"))
+      s->pool_cap_chunks = std::max<uint64_t>(1, std::strtoull(pc, nullptr, 10) / CHUNK_RECORDS);
     if (s->n_tiles) {
       if ((st = dalloc(&s->d_dep_ctl[0], 4)) || (st = dalloc(&s->d_dep_ctl[1], 4)) ||
           (st = dalloc(&s->d_tile_count, s->n_tiles)) || (st = dalloc(&s->d_tile_start, s->n_tiles)) ||
@@ -983,7 +1008,11 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   {
     const char* fh = std::getenv("SMCRT_FUSED_HIST");
     const bool fuse = !(fh && std::string(fh) == "0");
-    s->hist_tiles = (fuse && s->n_tiles > 0 && s->n_tiles <= MAX_FUSED_HIST_TILES) ? s->n_tiles : 0;
+    // SMCRT_DEPOSIT=sorted (or a disabled fused histogram) keeps the sorted record path
+    const char* dm = std::getenv("SMCRT_DEPOSIT");
+    const bool sorted = (dm && std::string(dm) == "sorted") || !fuse;
+    s->bucketed = !sorted && s->n_tiles > 0 && s->n_tiles <= MAX_DIRECT_TILES;
+    s->hist_tiles = (!s->bucketed && fuse && s->n_tiles > 0 && s->n_tiles <= MAX_FUSED_HIST_TILES) ? s->n_tiles : 0;
   }
   {
     const bool p2 = s->inv2[0] != 0.0 && s->inv2[1] != 0.0 && s->inv2[2] != 0.0;
@@ -1001,7 +1030,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
-    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, s->hist_tiles));
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, wave_words(s)));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     (x ? s->grid_blocks_x : s->grid_blocks) = cus * per_cu;
   }
@@ -1088,39 +1117,59 @@ static hipError_t drain_folds(smcrt_scene* s) {
 }
 
 // Records the record pool must hold for one launch of n photons.
+// Pool records that a launch's records do not fill: per wave, the last chunk (sorted path),
+// or the open bucket of every tile plus the unused ids of its batch (bucketed path).
+static double pool_slack_records(const smcrt_scene* s) {
+  const double waves = (double)std::max(s->grid_blocks, s->grid_blocks_x) * 4.0;
+  return s->bucketed ? waves * (double)(s->n_tiles + BUCKET_BATCH) * BUCKET_RECORDS : waves * CHUNK_RECORDS;
+}
 static uint64_t pool_records_for(const smcrt_scene* s, uint64_t n) {
-  const double want = (double)n * s->rpp_est * POOL_SLACK + (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
+  const double want = (double)n * s->rpp_est * POOL_SLACK + pool_slack_records(s);
   return (uint64_t)std::min(want, (double)MAX_POOL_RECORDS);
 }
 
 // Make sure the record pool holds `records` (grow only). Returns false if it cannot.
 static bool ensure_pool(smcrt_scene* s, uint64_t records) {
+  // (the pool is counted in CHUNK_RECORDS units on both paths: a chunk is 64 buckets)
   uint64_t chunks = (records + CHUNK_RECORDS - 1) / CHUNK_RECORDS;
+  if (s->pool_cap_chunks) chunks = std::min(chunks, s->pool_cap_chunks);
   if (chunks <= s->pool_chunks) return true;
   // grow with 25% headroom so launch-to-launch jitter of the estimate never reallocates
   // (a reallocation synchronises the device)
   chunks = std::min<uint64_t>(chunks + chunks / 4, MAX_POOL_RECORDS / CHUNK_RECORDS);
+  if (s->pool_cap_chunks) chunks = std::min(chunks, s->pool_cap_chunks);
   // the launches and folds in flight (on any stream) use these buffers
   (void)hipDeviceSynchronize();
   (void)drain_folds(s);
   auto release = [&]() {
-    void* old[] = {s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1], s->d_pieces};
+    void* old[] = {s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1], s->d_pieces,
+                   s->d_bucket_tile[0], s->d_bucket_tile[1], s->d_order};
     for (void* p : old)
       if (p) (void)hipFree(p);
     s->d_pool[0] = s->d_pool[1] = s->d_sorted = nullptr;
     s->d_chunk_fill[0] = s->d_chunk_fill[1] = nullptr;
+    s->d_bucket_tile[0] = s->d_bucket_tile[1] = s->d_order = nullptr;
     s->d_pieces = nullptr;
     s->pool_chunks = 0;
   };
   release();
   const uint64_t cap = chunks * CHUNK_RECORDS;
-  // pieces <= records / piece size + one partial piece per tile (deposit.h bin_scan)
+  // pieces <= records / piece size + one partial piece per tile (deposit.h bin_scan, bk_scan)
   const uint64_t pieces = std::min<uint64_t>(cap / MIN_PIECE_RECORDS, REDUCE_PIECES + 1) + s->n_tiles + 1;
-  if (hipMalloc((void**)&s->d_pool[0], cap * 8) != hipSuccess || hipMalloc((void**)&s->d_pool[1], cap * 8) != hipSuccess ||
-      hipMalloc((void**)&s->d_sorted, cap * 8) != hipSuccess ||
-      hipMalloc((void**)&s->d_chunk_fill[0], chunks * 4) != hipSuccess ||
-      hipMalloc((void**)&s->d_chunk_fill[1], chunks * 4) != hipSuccess ||
-      hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) != hipSuccess) {
+  const uint64_t buckets = cap / BUCKET_RECORDS;
+  bool ok = hipMalloc((void**)&s->d_pool[0], cap * 8) == hipSuccess && hipMalloc((void**)&s->d_pool[1], cap * 8) == hipSuccess &&
+            hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) == hipSuccess;
+  if (ok && s->bucketed)  // bucket fills, bucket tiles (per slot) and the tile-ordered id list
+    ok = hipMalloc((void**)&s->d_chunk_fill[0], buckets * 4) == hipSuccess &&
+         hipMalloc((void**)&s->d_chunk_fill[1], buckets * 4) == hipSuccess &&
+         hipMalloc((void**)&s->d_bucket_tile[0], buckets * 4) == hipSuccess &&
+         hipMalloc((void**)&s->d_bucket_tile[1], buckets * 4) == hipSuccess &&
+         hipMalloc((void**)&s->d_order, buckets * 4) == hipSuccess;
+  else if (ok)  // chunk fills (per slot) and the tile-sorted copy of the records
+    ok = hipMalloc((void**)&s->d_sorted, cap * 8) == hipSuccess &&
+         hipMalloc((void**)&s->d_chunk_fill[0], chunks * 4) == hipSuccess &&
+         hipMalloc((void**)&s->d_chunk_fill[1], chunks * 4) == hipSuccess;
+  if (!ok) {
     (void)hipGetLastError();
     release();
     return false;
@@ -1143,7 +1192,9 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
   HIPCHK(hipMemcpyAsync(C, &Ch, sizeof(KCold), hipMemcpyHostToDevice, stream));
   if (binned) {
     HIPCHK(hipMemsetAsync(s->d_dep_ctl[sl], 0, 4 * sizeof(uint32_t), stream));
-    if (K.hist_tiles)
+    if (K.bucket_tiles)  // per-tile bucket counts
+      HIPCHK(hipMemsetAsync(s->d_bin_counts[sl], 0, (size_t)s->n_tiles * sizeof(uint32_t), stream));
+    else if (K.hist_tiles)
       HIPCHK(hipMemsetAsync(s->d_bin_counts[sl], 0, (size_t)s->n_tiles * BIN_BLOCKS * sizeof(uint32_t), stream));
   }
   hipEvent_t* ev = nullptr;
@@ -1169,7 +1220,7 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
     const smcrt_detector* a_dets = K.dets;
     const int64_t* a_off = K.det_off;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&a_dets, (void*)&a_off, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, K.hist_tiles), stream));
+    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, wave_words(s)), stream));
   }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
@@ -1180,6 +1231,14 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
     if (ev) HIPCHK(hipEventRecord(ev[2], fs));
     const uint32_t nch = (uint32_t)s->pool_chunks;
     const uint64_t nv = (uint64_t)s->grid.nx * s->grid.ny * s->grid.nz;
+    if (K.bucket_tiles) {  // bucketed: list each tile's buckets, then sum them
+      hipLaunchKernelGGL(bk_scan, dim3(1), dim3(1024), 0, fs, s->d_bin_counts[sl], s->n_tiles, s->d_tile_start,
+                         s->d_tile_count, s->d_pieces, s->d_dep_ctl[sl]);
+      hipLaunchKernelGGL(bk_place, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_bucket_tile[sl], s->d_dep_ctl[sl],
+                         K.n_buckets, s->n_tiles, s->d_tile_count, s->d_order);
+      hipLaunchKernelGGL(bk_reduce, dim3(1024), dim3(1024), 0, fs, s->d_pool[sl], s->d_order, s->d_chunk_fill[sl],
+                         s->d_pieces, s->d_dep_ctl[sl], nv, Ch.jmean);
+    } else {
     if (!K.hist_tiles)  // else the transport kernel built the counts
       hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_pool[sl], s->d_chunk_fill[sl],
                          s->d_dep_ctl[sl], nch, s->n_tiles, s->d_bin_counts[sl]);
@@ -1192,6 +1251,7 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
                        s->d_sorted, (uint64_t)s->pool_chunks * CHUNK_RECORDS);
     hipLaunchKernelGGL(bin_reduce, dim3(1024), dim3(1024), 0, fs, s->d_sorted, s->d_pieces, s->d_dep_ctl[sl], nv,
                        Ch.jmean);
+    }
     HIPCHK(hipGetLastError());
     // remember how many records this launch produced (read back lazily, never waited for)
     HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl, s->d_dep_ctl[sl], 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
@@ -1311,10 +1371,11 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.key1 = (uint32_t)(cfg->seed >> 32);
   Ch.jmean = dt.jmean; Ch.absorb = dt.absorb; Ch.emission = dt.emission;
   Ch.chunk_fill = nullptr; Ch.dep_ctl = nullptr; Ch.bin_counts = nullptr;  // (per slot, below)
+  Ch.bucket_tile = nullptr; Ch.bucket_fill = nullptr; Ch.tile_nb = nullptr;
   Ch.det_bins = dt.det_bins; Ch.nscatt = dt.nscatt; Ch.moments = dt.moments;
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = s->d_queue;
-  K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0;
+  K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
@@ -1323,7 +1384,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   for (uint64_t done = 0; done < cfg->n_photons;) {
     refine_rpp(s);
     uint64_t n = cfg->n_photons - done;
-    K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0;
+    K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
     bool calibrate = false;
     if (binned) {
       // records per photon are scene-dependent: the scene's first large launch starts with a
@@ -1332,7 +1393,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
       const uint64_t want = pool_records_for(s, n);
       if (!ensure_pool(s, want)) (void)ensure_pool(s, want / 4);  // smaller pool, more batches
       if (s->pool_chunks) {
-        const double usable = (double)(s->pool_chunks * CHUNK_RECORDS) - (double)s->grid_blocks * 4.0 * CHUNK_RECORDS;
+        const double usable = (double)(s->pool_chunks * CHUNK_RECORDS) - pool_slack_records(s);
         n = std::min<uint64_t>(n, (uint64_t)std::max(65536.0, usable / (s->rpp_est * POOL_SLACK)));
         // (taken after ensure_pool: it may have reallocated the pool)
         K.rec_pool = s->d_pool[s->slot];
@@ -1341,6 +1402,13 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
         Ch.bin_counts = s->d_bin_counts[s->slot];
         K.n_chunks = (uint32_t)s->pool_chunks;
         K.hist_tiles = s->hist_tiles;
+        if (s->bucketed) {
+          Ch.bucket_fill = s->d_chunk_fill[s->slot];
+          Ch.bucket_tile = s->d_bucket_tile[s->slot];
+          Ch.tile_nb = s->d_bin_counts[s->slot];
+          K.bucket_tiles = s->n_tiles;
+          K.n_buckets = (uint32_t)(s->pool_chunks * (CHUNK_RECORDS / BUCKET_RECORDS));
+        }
       }
     }
     Ch.n_photons = n;

@@ -72,6 +72,9 @@ struct KCold {
   uint32_t* chunk_fill;       // records in each used chunk (deposit.h)
   uint32_t* dep_ctl;          // [0] next chunk, [1] overflowed deposits
   uint32_t* bin_counts;       // fused tile histogram, counts[tile][chunk % BIN_BLOCKS]
+  uint32_t* bucket_tile;      // bucketed path: tile of each bucket id (TILE_INVALID: unused)
+  uint32_t* bucket_fill;      // bucketed path: records in each bucket
+  uint32_t* tile_nb;          // bucketed path: buckets claimed per tile
   SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
 
@@ -99,6 +102,9 @@ struct KParams {
   // fused tile histogram (deposit.h): counts[tile][chunk % BIN_BLOCKS] built by the
   // transport kernel from a per-wave LDS histogram; hist_tiles == 0 -> bin_hist does it
   uint32_t hist_tiles;
+  // bucketed deposition (deposit.h): records go straight into per-tile buckets of the pool;
+  // bucket_tiles != 0 selects it (and is the tile count), n_buckets is the pool's size
+  uint32_t bucket_tiles, n_buckets;
 };
 
 // ------------------------------------------------------------------ voxels -------

@@ -173,18 +173,34 @@ def test_point_source_symmetry():
     assert abs(j.sum() / n - 6.0) < 0.1  # ~6 cm path per photon (Survey §6 probe: 6.01-6.05)
 
 
-@pytest.mark.parametrize("env", [{}, {"SMCRT_FUSED_HIST": "0"}, {"SMCRT_DEPOSIT": "atomic"}],
-                         ids=["fused-hist", "hist-kernel", "atomics"])
+@pytest.mark.parametrize("env", [{}, {"SMCRT_DEPOSIT": "sorted"}, {"SMCRT_FUSED_HIST": "0"},
+                                 {"SMCRT_DEPOSIT": "atomic"}],
+                         ids=["buckets", "sorted-fused-hist", "sorted-hist-kernel", "atomics"])
 def test_deposit_paths(monkeypatch, env):
-    """Every jmean deposition path (binned with the tile histogram fused into the transport
-    kernel, binned with the separate bin_hist kernel, fp64 atomics) gives the oracle's
-    result. The paths are chosen when the scene is created."""
+    """Every jmean deposition path (records filed into per-tile buckets by the transport
+    kernel; records sorted by tile with the histogram fused into the transport kernel or
+    built by the separate bin_hist kernel; fp64 atomics) gives the oracle's result. The paths
+    are chosen when the scene is created."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
     gpu, cpu = both(sc, scene.grid(96, 96, 96, 1, 1, 1), scene.point_source(), 20000)
     compare(gpu, cpu)
     assert cpu.counter("deposits") > 1_000_000
+
+
+@pytest.mark.parametrize("mode", ["buckets", "sorted"])
+def test_pool_exhaustion_spills_to_atomics(monkeypatch, mode):
+    """A record pool far too small for the launch (SMCRT_POOL_CAP) runs out mid-kernel: the
+    deposits that no longer fit are added with fp64 atomics, and the tallies still equal
+    the oracle's."""
+    monkeypatch.setenv("SMCRT_POOL_CAP", str(3 * 16384))
+    if mode == "sorted":
+        monkeypatch.setenv("SMCRT_DEPOSIT", "sorted")
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    gpu, cpu = both(sc, scene.grid(64, 64, 64, 1, 1, 1), scene.point_source(), 20000)
+    compare(gpu, cpu)
+    assert cpu.counter("deposits") > 20 * 3 * 16384
 
 
 def test_multi_launch_pool_reuse():
