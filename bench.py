@@ -65,7 +65,7 @@ def workload(name, grid_n):
         return (builders.synthetic_vessels(512), scene.grid(n, n, n, 0.16, 0.09, 0.13),
                 scene.uniform_source((-0.16, -0.09, 0.1299), (0.32, 0.0, 0.0), (0.0, 0.18, 0.0), (0.0, 0.0, -1.0)),
                 [], f"M4 (build-defined) synthetic vessel net: 512 capsules + dermis box, uniform source, {n}^3 grid",
-                1_000_000)
+                4_000_000)
     if name == "m5":
         n = grid_n or 128
         dets = [scene.circle_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.05, 50),
@@ -356,6 +356,9 @@ def main():
     ap.add_argument("--no-ref", action="store_true", help="skip the reference-pinned spatial checks")
     ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
     ap.add_argument("--sync-fold", action="store_true", help="diagnostic: each step waits for its own fold")
+    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1),
+                    help="1: steps run on the scene's two internal streams (SMCRT_FLAG_OVERLAP), so a "
+                         "step's slowest photons finish beside the next step")
     ap.add_argument("--source", default="default", choices=["default", "uniform"],
                     help="diagnostic: uniform = parallelogram source over the z=0.99 plane")
     ap.add_argument("--no-dets", action="store_true", help="diagnostic: the workload's scene without its detectors")
@@ -395,6 +398,8 @@ def main():
         # the deposit fold of step k runs beside step k+1's transport kernel; the fence
         # before the reduce makes jmean complete inside the timed region
         run_flags |= abi.FLAG_ASYNC_FOLD
+    if args.overlap:
+        run_flags |= abi.FLAG_OVERLAP
     eng = Engine(sc, g, dets, device=torch.cuda.current_device())
     comm = None
     if world > 1:

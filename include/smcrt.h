@@ -200,8 +200,13 @@ enum {
                                          initial layer mask ds<=0, scatter-order moments */
   SMCRT_FLAG_END_EARLY = 1u << 4,     /* test_kernel end_early: stop after the 4th scatter */
   SMCRT_FLAG_RECORD_PHOTONS = 1u << 5, /* fill smcrt_tallies.records (debug/parity) */
-  SMCRT_FLAG_ASYNC_FOLD = 1u << 6      /* smcrt_run_device: the jmean fold may finish after later work
+  SMCRT_FLAG_ASYNC_FOLD = 1u << 6,     /* smcrt_run_device: the jmean fold may finish after later work
                                           on the stream; jmean is complete after smcrt_scene_fence */
+  SMCRT_FLAG_OVERLAP = 1u << 7         /* smcrt_run_device: launches run on the scene's two internal
+                                          streams, each after the caller's earlier work, so launch k+1
+                                          fills the GPU while launch k's slowest photons finish; every
+                                          tally is complete in `stream` order only after
+                                          smcrt_scene_fence (implies SMCRT_FLAG_ASYNC_FOLD) */
 };
 
 typedef struct smcrt_run_config {
@@ -336,9 +341,10 @@ int smcrt_run_origins(smcrt_scene* scene, const smcrt_source* src, const double*
  * escape function (kernelsMod.f90:589-603). `kappa` may be NULL. */
 int smcrt_scene_classify(smcrt_scene* scene, const double* points, int64_t n, int32_t* layer, double* kappa);
 
-/* Make `stream` wait for every deposit fold in flight (SMCRT_FLAG_ASYNC_FOLD launches): jmean
- * is complete in `stream` order after this call. The fold of one launch then runs beside
- * the next launch's transport kernel (two record-log slots). */
+/* Make `stream` wait for every deposit fold in flight (SMCRT_FLAG_ASYNC_FOLD launches) and
+ * every launch in flight on the internal streams (SMCRT_FLAG_OVERLAP): all tallies are
+ * complete in `stream` order after this call. The fold of one launch then runs beside the
+ * next launch's transport kernel (two record-log slots). */
 int smcrt_scene_fence(smcrt_scene* scene, void* stream);
 
 /* Per-kernel device time (ms) of the launches made since the previous query, from HIP

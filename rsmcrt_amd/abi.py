@@ -56,6 +56,7 @@ FLAG_TEST_KERNEL = 1 << 3
 FLAG_END_EARLY = 1 << 4
 FLAG_RECORD_PHOTONS = 1 << 5
 FLAG_ASYNC_FOLD = 1 << 6
+FLAG_OVERLAP = 1 << 7
 
 # counters
 COUNTER_NAMES = [

@@ -13,26 +13,26 @@ namespace smcrt {
 struct V3 {
   double x, y, z;
 };
-__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
-__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ V3 mul(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }   // vec*scal
-__device__ __forceinline__ V3 smul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }  // scal*vec
-__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ double len(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
-__device__ __forceinline__ V3 vabs(V3 a) { return v3(fabs(a.x), fabs(a.y), fabs(a.z)); }
-__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
-__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
-__device__ __forceinline__ double clampd(double v, double lo, double hi) { return dmin(dmax(v, lo), hi); }
+__host__ __device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__host__ __device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__host__ __device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__host__ __device__ __forceinline__ V3 mul(V3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }   // vec*scal
+__host__ __device__ __forceinline__ V3 smul(double s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }  // scal*vec
+__host__ __device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ double len(V3 a) { return sqrt(a.x * a.x + a.y * a.y + a.z * a.z); }
+__host__ __device__ __forceinline__ V3 vabs(V3 a) { return v3(fabs(a.x), fabs(a.y), fabs(a.z)); }
+__host__ __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : b; }
+__host__ __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : b; }
+__host__ __device__ __forceinline__ double clampd(double v, double lo, double hi) { return dmin(dmax(v, lo), hi); }
 
 // vec_dot_mat, vector_class.f90:292-304 (transform column-major)
-__device__ __forceinline__ V3 dotmat(V3 a, const double* t) {
+__host__ __device__ __forceinline__ V3 dotmat(V3 a, const double* t) {
   return v3(t[0] * a.x + t[1] * a.y + t[2] * a.z + t[3], t[4] * a.x + t[5] * a.y + t[6] * a.z + t[7],
             t[8] * a.x + t[9] * a.y + t[10] * a.z + t[11]);
 }
 
 // CSG operators, sdfModifiers.f90:428-491
-__device__ __forceinline__ double csg(int32_t op, double d1, double d2, double k) {
+__host__ __device__ __forceinline__ double csg(int32_t op, double d1, double d2, double k) {
   switch (op) {
     case SMCRT_OP_UNION: return dmin(d1, d2);
     case SMCRT_OP_SMOOTH_UNION: {
@@ -51,7 +51,7 @@ __device__ __forceinline__ double csg(int32_t op, double d1, double d2, double k
 // invert(translate(c)), setupGeometry.f90:64,289), so ((x*1 + y*0) + z*0) + t = x + t.
 // This is exact for every finite input; at most the sign of a zero result differs, which
 // no SDF below can observe (they use squares, abs, min/max and comparisons with 0).
-__device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos, bool translate_only) {
+__host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos, bool translate_only) {
   const double* P = nd->param;
   const double* t = nd->transform;
   const V3 p = translate_only ? v3(pos.x + t[3], pos.y + t[7], pos.z + t[11]) : dotmat(pos, t);

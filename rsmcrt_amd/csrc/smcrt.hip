@@ -228,6 +228,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
                                            __shfl(capi, l, 64), __shfl(capj, l, 64));
           if (lane_id == l) R = o;
         }
+      } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)
+        R = eval_culled(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj);
       } else {
         R = eval_sdfs(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }
@@ -690,6 +692,10 @@ struct smcrt_scene {
   ProgOp* d_prog = nullptr;
   int n_prog = 0;
   int coop_lanes = 0;
+  // exact SDF culling (cull.h): grid + lists + the always-evaluated program, one allocation
+  CullGrid* d_cull = nullptr;
+  void* d_cull_data = nullptr;
+  double cull_mean_list = 0.0;
   double inv2[3] = {0.0, 0.0, 0.0};
   int grid_mode = 0;  // transport_kernel<*, GM>: 1 = every 2*max a power of two, 2 = and every n too
   int32_t fe[3] = {0, 0, 0};
@@ -697,7 +703,14 @@ struct smcrt_scene {
   double* d_faces = nullptr;
   smcrt_detector* d_dets = nullptr;
   int64_t* d_det_off = nullptr;
-  unsigned long long* d_queue = nullptr;
+  unsigned long long* d_queue = nullptr;  // work-queue heads: [0], [1] internal streams, [2] caller stream
+  // SMCRT_FLAG_OVERLAP: launches alternate between two internal streams (lstream), so the next
+  // launch's blocks fill the CUs its predecessor's tail leaves idle
+  hipStream_t lstream[2] = {nullptr, nullptr};
+  hipEvent_t lev[2] = {nullptr, nullptr};  // the last launch on lstream[i] is done
+  hipEvent_t ev_in = nullptr;              // the caller's work before an overlapped call
+  bool lpending[2] = {false, false};
+  int lturn = 0;
   KCold* d_cold = nullptr;  // COLD_SLOTS launch slots (ring, stream-ordered writes)
   uint64_t cold_seq = 0;
   // tallies owned by the scene for the synchronous smcrt_run
@@ -839,12 +852,19 @@ void smcrt_scene_destroy(smcrt_scene* s) {
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1],
                   s->d_dep_ctl[0], s->d_dep_ctl[1], s->d_tile_count, s->d_tile_start, s->d_bin_counts[0],
-                  s->d_bin_counts[1], s->d_pieces, s->d_bucket_tile[0], s->d_bucket_tile[1], s->d_order};
+                  s->d_bin_counts[1], s->d_pieces, s->d_bucket_tile[0], s->d_bucket_tile[1], s->d_order,
+                  s->d_cull, s->d_cull_data};
   for (int i = 0; i < 2; ++i) {
     if (s->ctl_ev[i]) (void)hipEventDestroy(s->ctl_ev[i]);
     if (s->ev_f[i]) (void)hipEventDestroy(s->ev_f[i]);
   }
   if (s->ev_t) (void)hipEventDestroy(s->ev_t);
+  for (int i = 0; i < 2; ++i) {
+    if (s->lstream[i]) (void)hipStreamSynchronize(s->lstream[i]);
+    if (s->lev[i]) (void)hipEventDestroy(s->lev[i]);
+    if (s->lstream[i]) (void)hipStreamDestroy(s->lstream[i]);
+  }
+  if (s->ev_in) (void)hipEventDestroy(s->ev_in);
   if (s->fstream) (void)hipStreamDestroy(s->fstream);
   for (hipEvent_t e : s->tev) (void)hipEventDestroy(e);
   if (s->h_ctl) (void)hipHostFree(s->h_ctl);
@@ -948,6 +968,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   // A sparse wave evaluates its lanes' SDF arrays one lane at a time across the wave when
   // that is cheaper than the serial per-lane chain over all n_top tops (transport.h).
   s->coop_lanes = n_top >= 8 ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
+  // exact culling of the SDF array for many-top scenes (cull.h); SMCRT_CULL=0 turns it off
+  CullHost cull;
+  {
+    const char* ce = std::getenv("SMCRT_CULL");
+    const double gh[3] = {grid->xmax, grid->ymax, grid->zmax};
+    if (s->coop_lanes > 0 && !(ce && std::string(ce) == "0")) cull = build_cull(nodes, n_nodes, top, n_top, gh);
+  }
   // n*p/(2*max) may be computed as n*p*inv exactly when 2*max is a power of two
   const double maxes[3] = {grid->xmax, grid->ymax, grid->zmax};
   for (int a = 0; a < 3; ++a) {
@@ -957,7 +984,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
-      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, 1)) ||
+      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, 3)) ||
       (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
@@ -972,7 +999,44 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (e == hipSuccess)
     e = hipMemcpy(s->d_det_off, s->h_det_off.data(), sizeof(int64_t) * (n_dets + 1), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+    e = hipStreamCreateWithFlags(&s->lstream[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&s->lev[i], hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
+  if (cull.enabled) {  // [ProgOp always | u32 off | u32 list | double lb], each 16-B aligned
+    std::vector<ProgOp> pa;
+    for (int32_t t : cull.always)
+      for (int32_t ip = top_first[t]; ip < top_first[t + 1]; ++ip) pa.push_back(prog[ip]);
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const size_t b_pa = al(pa.size() * sizeof(ProgOp)), b_off = al(cull.off.size() * 4),
+                 b_list = al(std::max<size_t>(1, cull.list.size()) * 4), b_lb = al(cull.lb.size() * 8);
+    std::vector<unsigned char> blob(b_pa + b_off + b_list + b_lb, 0);
+    std::memcpy(blob.data(), pa.data(), pa.size() * sizeof(ProgOp));
+    std::memcpy(blob.data() + b_pa, cull.off.data(), cull.off.size() * 4);
+    std::memcpy(blob.data() + b_pa + b_off, cull.list.data(), cull.list.size() * 4);
+    std::memcpy(blob.data() + b_pa + b_off + b_list, cull.lb.data(), cull.lb.size() * 8);
+    if ((st = dalloc((unsigned char**)&s->d_cull_data, blob.size())) || (st = dalloc(&s->d_cull, 1)))
+      return cleanup_fail(st);
+    unsigned char* base = (unsigned char*)s->d_cull_data;
+    CullGrid G;
+    for (int a = 0; a < 3; ++a) { G.lo[a] = cull.lo[a]; G.n[a] = cull.n[a]; }
+    G.cell = cull.cell;
+    G.inv_cell = 1.0 / cull.cell;
+    G.n_prog_always = (int32_t)pa.size();
+    G.prog_always = base;
+    G.off = (const uint32_t*)(base + b_pa);
+    G.list = (const uint32_t*)(base + b_pa + b_off);
+    G.lb = (const double*)(base + b_pa + b_off + b_list);
+    e = hipMemcpy(s->d_cull_data, blob.data(), blob.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(s->d_cull, &G, sizeof G, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("cull upload: ") + hipGetErrorString(e)));
+    s->cull_mean_list = cull.mean_list;
+    if (std::getenv("SMCRT_CULL_LOG"))  // diagnostics
+      std::fprintf(stderr, "[cull] %d tops, %zu always, %d x %d x %d cells of %.4g, %.1f tops per cell\n", n_top,
+                   cull.always.size(), cull.n[0], cull.n[1], cull.n[2], cull.cell, cull.mean_list);
+  }
   {  // binned deposition state (deposit.h)
     const uint64_t nv = (uint64_t)grid->nx * grid->ny * grid->nz;
     const uint64_t tiles = (nv + TILE_VOXELS - 1) / TILE_VOXELS;
@@ -1183,11 +1247,14 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
 // s->fstream, ordered after the launch by an event. The fold of the previous launch may still
 // run while this transport kernel does: they touch different slots (and jmean is only
 // written by folds, which are serial on fstream).
-static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hipStream_t stream, int sl) {
+static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_t stream, int sl, int qi) {
   const bool binned = K.rec_pool != nullptr;
   if (binned && s->f_pending[sl]) HIPCHK(hipStreamWaitEvent(stream, s->ev_f[sl], 0));  // slot free
-  HIPCHK(hipMemsetAsync(s->d_queue, 0, sizeof(unsigned long long), stream));
-  // this launch's cold parameters: a ring slot, written in stream order before the kernel
+  Ch.queue = s->d_queue + qi;  // (a queue head per stream: overlapped launches run concurrently)
+  HIPCHK(hipMemsetAsync(Ch.queue, 0, sizeof(unsigned long long), stream));
+  // this launch's cold parameters: a ring slot, written in stream order before the kernel.
+  // (Overlapped launches alternate streams and COLD_SLOTS is even, so a slot is always
+  // rewritten on the stream that last read it.)
   KCold* C = s->d_cold + (s->cold_seq++ % COLD_SLOTS);
   HIPCHK(hipMemcpyAsync(C, &Ch, sizeof(KCold), hipMemcpyHostToDevice, stream));
   if (binned) {
@@ -1290,6 +1357,15 @@ static int launch_one(smcrt_scene* s, KParams K, const KCold& Ch, bool xsrc, hip
     std::fprintf(stderr, "\n");
     std::memset(ht, 0, sizeof(ht));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_t), ht, sizeof(ht)));
+    unsigned long long hc[6];
+    HIPCHK(hipMemcpyFromSymbol(hc, HIP_SYMBOL(g_cull_diag), sizeof(hc)));
+    if (hc[0] + hc[2])
+      std::fprintf(stderr, "[diag-cull] culled lane-EVALs %llu, bound fallbacks %llu (%.4f), capture/outside %llu, "
+                   "mean list %.1f, wave-EVALs %llu with a full fallback %.3f\n", hc[0], hc[1],
+                   (double)hc[1] / (double)std::max(1ull, hc[0]), hc[2], (double)hc[3] / (double)std::max(1ull, hc[0]),
+                   hc[4], (double)hc[5] / (double)std::max(1ull, hc[4]));
+    std::memset(hc, 0, sizeof(hc));
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_cull_diag), hc, sizeof(hc)));
   }
 #endif
   return SMCRT_OK;
@@ -1351,6 +1427,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.prog = s->d_prog;
   K.n_prog = s->n_prog;
   K.coop_lanes = s->coop_lanes;
+  K.cull = s->d_cull;
   K.inv2x = s->inv2[0]; K.inv2y = s->inv2[1]; K.inv2z = s->inv2[2];
   K.fex = s->fe[0]; K.fey = s->fe[1]; K.fez = s->fe[2];
   K.props = s->d_props;
@@ -1374,13 +1451,21 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.bucket_tile = nullptr; Ch.bucket_fill = nullptr; Ch.tile_nb = nullptr;
   Ch.det_bins = dt.det_bins; Ch.nscatt = dt.nscatt; Ch.moments = dt.moments;
   Ch.counters = (unsigned long long*)dt.counters;
-  Ch.queue = s->d_queue;
+  Ch.queue = nullptr;  // (set per launch: launch_one)
   K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
   const bool binned = dt.jmean && (cfg->flags & SMCRT_FLAG_PATHLENGTH) && !(cfg->flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
                       s->n_tiles > 0 && !s->force_atomic;
+  const bool overlap = (cfg->flags & SMCRT_FLAG_OVERLAP) != 0;
+  if (overlap) {  // the internal streams start after the caller's earlier work
+    HIPCHK(hipEventRecord(s->ev_in, stream));
+    for (int i = 0; i < 2; ++i) HIPCHK(hipStreamWaitEvent(s->lstream[i], s->ev_in, 0));
+  } else {  // a plain launch runs after every overlapped one (same tallies, same buffers)
+    for (int i = 0; i < 2; ++i)
+      if (s->lpending[i]) HIPCHK(hipStreamWaitEvent(stream, s->lev[i], 0));
+  }
   for (uint64_t done = 0; done < cfg->n_photons;) {
     refine_rpp(s);
     uint64_t n = cfg->n_photons - done;
@@ -1420,7 +1505,16 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
       if (s->ctl_pending[sl]) { HIPCHK(hipEventSynchronize(s->ctl_ev[sl])); refine_rpp(s); }
       s->h_ctl[8 * sl + 4] = (uint32_t)std::min<uint64_t>(n, 0xFFFFFFFFull);
     }
-    int st = launch_one(s, K, Ch, xsrc, stream, sl);
+    int st;
+    if (overlap) {
+      const int q = s->lturn;
+      s->lturn ^= 1;
+      st = launch_one(s, K, Ch, xsrc, s->lstream[q], sl, q);
+      if (!st && hipEventRecord(s->lev[q], s->lstream[q]) != hipSuccess) st = fail(SMCRT_ERR_HIP, "event record failed");
+      s->lpending[q] = true;
+    } else {
+      st = launch_one(s, K, Ch, xsrc, stream, sl, 2);
+    }
     if (st) return st;
     if (K.rec_pool) s->slot ^= 1;
     if (calibrate && K.rec_pool) {
@@ -1430,7 +1524,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
     done += n;
   }
   // the tallies are complete in `stream` order at return, unless the caller defers the folds
-  if (!(cfg->flags & SMCRT_FLAG_ASYNC_FOLD) && s->last_slot >= 0 && s->f_pending[s->last_slot])
+  if (!(cfg->flags & (SMCRT_FLAG_ASYNC_FOLD | SMCRT_FLAG_OVERLAP)) && s->last_slot >= 0 && s->f_pending[s->last_slot])
     HIPCHK(hipStreamWaitEvent(stream, s->ev_f[s->last_slot], 0));
   return SMCRT_OK;
 }
@@ -1452,7 +1546,7 @@ static int run_sync(smcrt_scene* s, const smcrt_source* src, const smcrt_run_con
   // A synchronous run returns complete tallies: its folds always join s->stream before the
   // copies, whatever the caller's flags say (SMCRT_FLAG_ASYNC_FOLD is for smcrt_run_device).
   smcrt_run_config cfg_local = *cfg_in;
-  cfg_local.flags &= ~(uint32_t)SMCRT_FLAG_ASYNC_FOLD;
+  cfg_local.flags &= ~(uint32_t)(SMCRT_FLAG_ASYNC_FOLD | SMCRT_FLAG_OVERLAP);
   const smcrt_run_config* cfg = &cfg_local;
   const int64_t nv = (int64_t)s->grid.nx * s->grid.ny * s->grid.nz;
   const bool want[3] = {io->jmean || io->jmean_f64, io->absorb || io->absorb_f64, io->emission || io->emission_f64};
@@ -1623,6 +1717,8 @@ int smcrt_scene_fence(smcrt_scene* s, void* stream) {
   if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
   std::lock_guard<std::mutex> g(s->mu);
   HIPCHK(hipSetDevice(s->device));
+  for (int i = 0; i < 2; ++i)  // overlapped launches (their folds are ordered after them)
+    if (s->lpending[i]) HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->lev[i], 0));
   if (s->last_slot >= 0 && s->f_pending[s->last_slot])  // folds are serial: the last covers all
     HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->ev_f[s->last_slot], 0));
   return SMCRT_OK;

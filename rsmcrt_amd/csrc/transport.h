@@ -24,6 +24,7 @@
 #include "detmath.h"
 #include "geometry.h"
 #include "srcplan.h"
+#include "cull.h"
 
 namespace smcrt {
 
@@ -105,6 +106,8 @@ struct KParams {
   // bucketed deposition (deposit.h): records go straight into per-tile buckets of the pool;
   // bucket_tiles != 0 selects it (and is the tile count), n_buckets is the pool's size
   uint32_t bucket_tiles, n_buckets;
+  // exact SDF culling (cull.h), many-top scenes in the COOP instantiation; NULL = off
+  const CullGrid* __restrict__ cull;
 };
 
 // ------------------------------------------------------------------ voxels -------
@@ -925,6 +928,110 @@ __device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restri
   r.maxloc = loc;
   r.va = capi > 0 ? __shfl(va, (capi - 1) & 63, 64) : 0.0;
   r.vb = capj > 0 ? __shfl(vb, (capj - 1) & 63, 64) : 0.0;
+  return r;
+}
+
+// Culled EVAL (cull.h): the always-evaluated tops wave-uniformly, then each lane walks its
+// cell's list of tops with per-lane loads; a lane whose bound test fails (or that needs the
+// Fresnel/normal captures, or lies outside the culling grid) takes part in one wave-uniform
+// full EVAL instead. The merge keeps eval_sdfs' results exactly: min and abs-min are order
+// free, and maxloc ties go to the lowest top index as eval_sdfs' index-order strict compare.
+// Call in wave-uniform control flow.
+#ifdef SMCRT_DIAG
+// diagnostic builds: [0] culled lane-EVALs [1] bound-test fallbacks [2] capture/outside
+// fallbacks [3] list entries walked [4] wave-EVALs [5] wave-EVALs with a full fallback
+__device__ unsigned long long g_cull_diag[6];
+#endif
+__device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict__ nodes,
+                                               const ProgOp* __restrict__ prog, int32_t n_prog,
+                                               const CullGrid* __restrict__ G, V3 q, bool have, bool mask_le,
+                                               int32_t capi, int32_t capj) {
+  EvalOut r;
+  r.minabs = __builtin_inf();
+  r.minv = __builtin_inf();
+  r.va = 0.0; r.vb = 0.0;
+  r.maxloc = 0;
+  double best = -__builtin_inf();
+  {  // the unboundable tops, wave-uniform (scalar-loaded program)
+    const ProgOp* __restrict__ pa = (const ProgOp*)G->prog_always;
+    const int32_t na = G->n_prog_always;
+    double acc = 0.0;
+    for (int32_t ip = 0; ip < na; ++ip) {
+      const ProgOp op = pa[ip];
+      const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
+      const double v = sdf_prim(nodes + node, q, op.translate_only != 0);
+      if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
+      else acc = csg(op.op, acc, v, op.k);
+      if (op.top > 0) {
+        const double d = acc;
+        const double a = fabs(d);
+        if (a < r.minabs) r.minabs = a;
+        if (d < r.minv) r.minv = d;
+        const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+        if (neg && (r.maxloc == 0 || d > best)) { best = d; r.maxloc = op.top; }
+      }
+    }
+  }
+  bool full = !have || capi != 0 || capj != 0;
+  const double fx = (q.x - G->lo[0]) * G->inv_cell, fy = (q.y - G->lo[1]) * G->inv_cell,
+               fz = (q.z - G->lo[2]) * G->inv_cell;
+  if (!(fx >= 0.0 && fx < (double)G->n[0] && fy >= 0.0 && fy < (double)G->n[1] && fz >= 0.0 &&
+        fz < (double)G->n[2]))
+    full = true;
+  if (!full) {
+    const int32_t ix = (int32_t)fx, iy = (int32_t)fy, iz = (int32_t)fz;
+    const uint32_t c = (uint32_t)ix + (uint32_t)G->n[0] * ((uint32_t)iy + (uint32_t)G->n[1] * (uint32_t)iz);
+    const uint32_t b = G->off[c], e = G->off[c + 1];
+    const uint2* __restrict__ ent = (const uint2*)G->list;
+    for (uint32_t k = b; k < e; ++k) {  // per lane: its cell's tops, ascending
+      const uint2 en = ent[k];
+      const int32_t i = (int32_t)(en.x & CULL_TOP_MASK);
+      double d;
+      if (en.x & CULL_MODEL) {  // a model: its ops in the flattened program
+        const int32_t o0 = prog[n_prog + i].node, o1 = prog[n_prog + i + 1].node;
+        double acc = 0.0;
+        for (int32_t ip = o0; ip < o1; ++ip) {
+          const ProgOp op = prog[ip];
+          const double v = sdf_prim(nodes + op.node, q, op.translate_only != 0);
+          if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
+          else acc = csg(op.op, acc, v, op.k);
+        }
+        d = acc;
+      } else {
+        d = sdf_prim(nodes + en.y, q, (en.x & CULL_TRANSLATE) != 0);
+      }
+      const int32_t t = i + 1;
+      const double a = fabs(d);
+      if (a < r.minabs) r.minabs = a;
+      if (d < r.minv) r.minv = d;
+      const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+      if (neg && (r.maxloc == 0 || d > best || (d == best && t < r.maxloc))) { best = d; r.maxloc = t; }
+    }
+    // every unlisted top has ds >= max(distance to the cell's boundary, lb[c])
+    const double cx = G->lo[0] + (double)ix * G->cell, cy = G->lo[1] + (double)iy * G->cell,
+                 cz = G->lo[2] + (double)iz * G->cell;
+    double h = dmin(dmin(dmin(q.x - cx, cx + G->cell - q.x), dmin(q.y - cy, cy + G->cell - q.y)),
+                    dmin(q.z - cz, cz + G->cell - q.z));
+    h = dmax(h, 0.0);
+    const double T = dmax(h, G->lb[c]) * (1.0 - 1e-12);
+    if (!(r.minabs < T)) full = true;
+#ifdef SMCRT_DIAG
+    atomicAdd(&g_cull_diag[0], 1ull);
+    atomicAdd(&g_cull_diag[3], (unsigned long long)(e - b));
+    if (full) atomicAdd(&g_cull_diag[1], 1ull);
+#endif
+  }
+#ifdef SMCRT_DIAG
+  else if (have) atomicAdd(&g_cull_diag[2], 1ull);
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&g_cull_diag[4], 1ull);
+  }
+  if ((threadIdx.x & 63) == 0 && __ballot(have && full)) atomicAdd(&g_cull_diag[5], 1ull);
+#endif
+  if (__ballot(have && full)) {
+    const EvalOut f = eval_sdfs(nodes, prog, n_prog, q, mask_le, capi, capj);
+    if (full) r = f;
+  }
   return r;
 }
 

@@ -439,10 +439,14 @@ def test_general_emitter_with_detectors():
     assert cpu.counter("detector_hits") > 0
 
 
-def test_async_fold_pipeline():
+@pytest.mark.parametrize("overlap", [False, True], ids=["async-fold", "overlap"])
+def test_async_fold_pipeline(overlap):
     """FLAG_ASYNC_FOLD launches on a caller stream (the bench's mode: the fold of launch k runs
     beside launch k+1's transport kernel in the other record slot) + a fence give the same
-    tallies as one synchronous run of the same photons."""
+    tallies as one synchronous run of the same photons. With FLAG_OVERLAP the launches also
+    alternate between the scene's two internal streams (launch k+1 starts while launch k's
+    slowest photons finish), a plain run afterwards is ordered behind them, and the tallies
+    are the same."""
     import torch
     sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
     g = scene.grid(64, 64, 64, 1, 1, 1)
@@ -456,10 +460,14 @@ def test_async_fold_pipeline():
     dt.jmean, dt.absorb, dt.counters = jm.data_ptr(), ab.data_ptr(), ctr.data_ptr()
     stream = torch.cuda.current_stream()
     n, k = 300_000, 5
+    fl = abi.FLAG_PATHLENGTH | abi.FLAG_ASYNC_FOLD | (abi.FLAG_OVERLAP if overlap else 0)
     with Engine(sc, g) as eng:
         for i in range(k):
-            eng.run_device(src, Engine.config(n, seed=SEED, flags=abi.FLAG_PATHLENGTH | abi.FLAG_ASYNC_FOLD,
-                                              first_photon=i * n), dt, stream.cuda_stream)
+            eng.run_device(src, Engine.config(n, seed=SEED, flags=fl, first_photon=i * n), dt, stream.cuda_stream)
+        if overlap:  # a plain launch on the caller's stream waits for the overlapped ones
+            eng.run_device(src, Engine.config(n, seed=SEED, flags=abi.FLAG_PATHLENGTH, first_photon=k * n), dt,
+                           stream.cuda_stream)
+            k += 1
         eng.fence(stream.cuda_stream)
         torch.cuda.synchronize()
         ref = eng.run(src, n * k, seed=SEED)
@@ -494,6 +502,61 @@ def test_coop_eval_models_and_many_tops():
     gpu, cpu = both(sc, scene.grid(40, 40, 40, 1, 1, 1), src, 1500)
     compare(gpu, cpu)
     assert cpu.counter("fresnel") > 0
+
+
+def _culling_scene(seed=7):
+    """~60 tops for the culled EVAL (cull.h): random capsules, rotated and translated
+    spheres, tori and capped cylinders, smooth-union / intersection / subtraction models, a
+    cone and a scaled sphere (never culled), inside a medium box (always evaluated)."""
+    from rsmcrt_amd.scene import (Scene, box, capsule, cone, cylinder, invert, model, mono, rotate_x, rotate_z,
+                                  sphere, torus, translate)
+    rng = np.random.default_rng(seed)
+    mm = lambda a, b: (np.array(a) @ np.array(b)).tolist()  # noqa: E731
+    sdfs = []
+    lay = lambda: len(sdfs) + 1  # noqa: E731
+    for i in range(30):
+        a = rng.uniform(-0.6, 0.6, 3)
+        b = a + rng.normal(0, 0.08, 3)
+        sdfs.append(capsule(tuple(a), tuple(b), float(rng.uniform(0.01, 0.04)),
+                            mono(20.0, 0.5, 0.8, 1.3 + 0.01 * (i % 5)), lay()))
+    for i in range(8):
+        c = rng.uniform(-0.6, 0.6, 3)
+        t = invert(mm(mm(rotate_z(17.0 * i), rotate_x(9.0 * i)), translate(tuple(c))))
+        sdfs.append(sphere(float(rng.uniform(0.02, 0.06)), mono(8.0, 0.2, 0.7, 1.4), lay(), transform=t))
+    for i in range(4):
+        c = rng.uniform(-0.5, 0.5, 3)
+        t = invert(mm(rotate_x(30.0 * i), translate(tuple(c))))
+        sdfs.append(torus(0.06, 0.015, mono(8.0, 0.2, 0.7, 1.35), lay(), transform=t))
+        a = rng.uniform(-0.6, 0.6, 3)
+        sdfs.append(cylinder(tuple(a), tuple(a + rng.normal(0, 0.1, 3)), 0.02, mono(8.0, 0.2, 0.7, 1.33), lay()))
+    opt_m = mono(5.0, 0.2, 0.5, 1.45)
+    sdfs.append(model([sphere(0.07, opt_m, lay(), transform=invert(translate((0.3, 0.3, 0.3)))),
+                       capsule((0.3, 0.2, 0.3), (0.3, 0.45, 0.3), 0.03, opt_m, lay())], abi.OP_SMOOTH_UNION, 0.04))
+    sdfs.append(model([sphere(0.09, opt_m, lay(), transform=invert(translate((-0.3, 0.3, -0.3)))),
+                       box((0.12, 0.12, 0.12), opt_m, lay(), transform=invert(translate((-0.27, 0.3, -0.3))))],
+                      abi.OP_INTERSECTION, 0.0))
+    sdfs.append(model([sphere(0.05, opt_m, lay(), transform=invert(translate((0.3, -0.3, 0.0)))),
+                       sphere(0.08, opt_m, lay(), transform=invert(translate((0.32, -0.3, 0.0))))],
+                      abi.OP_SUBTRACTION, 0.0))
+    sdfs.append(cone((0.0, -0.5, -0.5), (0.0, -0.4, -0.5), 0.05, 0.02, mono(8.0, 0.2, 0.7, 1.38), lay()))
+    sdfs.append(sphere(0.03, mono(8.0, 0.2, 0.7, 1.39), lay(),
+                       transform=[[2.0, 0, 0, 0], [0, 2.0, 0, 0], [0, 0, 2.0, 0], [-0.8, 0.8, 0.4, 1.0]]))
+    sdfs.append(box((2.0, 2.0, 2.0), mono(3.0, 0.05, 0.8, 1.0), lay()))
+    return Scene(sdfs)
+
+
+@pytest.mark.parametrize("src_kind", ["point", "uniform"])
+def test_culled_eval_mixed_scene(src_kind):
+    """Exact SDF culling (cull.h, used for scenes with >= 16 tops): a mixed ~60-top scene with
+    rigidly transformed primitives, CSG models of every op, and unboundable tops, Fresnel at
+    every crossing. Every record, counter and tally equals the oracle's full evaluation."""
+    sc = _culling_scene()
+    assert sc.n_top >= 50
+    src = (scene.point_source() if src_kind == "point" else
+           scene.uniform_source((-1.0, -1.0, 0.999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0)))
+    gpu, cpu = both(sc, scene.grid(48, 48, 48, 1, 1, 1), src, 6000)
+    compare(gpu, cpu)
+    assert cpu.counter("fresnel") > 1000
 
 
 def test_sync_run_ignores_async_fold_flag():

@@ -4,7 +4,7 @@
 # usage (on the GPU box): TAG=r02_v1 bash tools/profile_round.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r02}
-PASSES="trace sq fetch write valu" PROF_ARGS="${PROF_ARGS:---no-cpu --steps 3 --warmup 2}" bash tools/profile.sh || exit $?
+PASSES="trace sq fetch write valu" PROF_ARGS="${PROF_ARGS:---no-cpu --no-ref --steps 3 --warmup 2}" bash tools/profile.sh || exit $?
 mkdir -p gpurun_out/$TAG
 python3 tools/prof_summary.py gpurun_out/prof --last 3 --batch ${BATCH:-16000000} --grid ${GRID:-128} \
   --workload ${WORKLOAD:-m1} --json gpurun_out/$TAG/summary.json --traffic gpurun_out/$TAG/transport_traffic.json \
