@@ -45,7 +45,9 @@ def main():
     ap.add_argument("--workload", default="m1")
     a = ap.parse_args()
     out = {}
-    tr = find(a.dir, "trace", "kernel_trace") or os.path.join(a.dir, "kernel_trace.csv")
+    tr = os.path.join(a.dir, "kernel_trace.csv")  # (a copied summary directory)
+    if not os.path.exists(tr):
+        tr = find(a.dir, "trace", "kernel_trace")
     disp = defaultdict(list)
     for r in read(tr):
         k = short(r["Kernel_Name"])
@@ -89,7 +91,7 @@ def main():
             # the whole step: the transport kernel plus the deposit-fold kernels that follow each
             # of its launches (same dispatch count), per launch
             step = {kk: out[kk]["hbm_bytes_per_dispatch"] for kk in out
-                    if (kk == k or kk.startswith("bin_") or kk.startswith("dda_") or kk.startswith("fold_"))
+                    if (kk == k or kk.startswith(("bin_", "bk_", "dda_", "fold_")))
                     and "hbm_bytes_per_dispatch" in out[kk]}
             classes = {c: out[k][c] for c in out[k] if c.startswith("SQ_INSTS_VALU_")}
             with open(a.traffic, "w") as f:
