@@ -373,20 +373,22 @@ struct BucketLog {
   uint32_t next, end;
 };
 
-// Per-wave LDS state: bf[t] = records in tile t's open bucket (BUCKET_RECORDS: none open),
-// bi[t] = its id. Call in wave-uniform control flow.
-__device__ __forceinline__ void init_buckets(uint32_t* bf, uint32_t* bi, uint32_t n_tiles) {
+// Per-wave LDS state, one 64-bit word per tile: (id << 32) | fill, where fill = records in
+// the tile's open bucket (BUCKET_RECORDS: none open) and id = that bucket. One LDS
+// add-and-return of 1 hands a deposit both its slot and its bucket. Call in wave-uniform
+// control flow.
+__device__ __forceinline__ unsigned long long bucket_word(uint32_t id, uint32_t fill) {
+  return ((unsigned long long)id << 32) | fill;
+}
+__device__ __forceinline__ void init_buckets(unsigned long long* bs, uint32_t n_tiles) {
   const int lane = threadIdx.x & 63;
-  for (uint32_t t = lane; t < n_tiles; t += 64) {
-    bf[t] = BUCKET_RECORDS;
-    bi[t] = BUCKET_NONE;
-  }
+  for (uint32_t t = lane; t < n_tiles; t += 64) bs[t] = bucket_word(BUCKET_NONE, BUCKET_RECORDS);
 }
 
 __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __restrict__ C, BucketLog& W,
-                                                      bool over, uint32_t pos, uint32_t t, unsigned long long rec,
-                                                      uint32_t vox, double val, uint32_t& overflow, uint32_t* bf,
-                                                      uint32_t* bi) {
+                                                      bool over, uint32_t pos, uint32_t oldid, uint32_t t,
+                                                      unsigned long long rec, uint32_t vox, double val,
+                                                      uint32_t& overflow, unsigned long long* bs) {
   const int lane = threadIdx.x & 63;
   // The deposit that found its tile's fill at exactly BUCKET_RECORDS claims the next bucket;
   // the others of this instruction that overflowed the same tile follow it into the new one.
@@ -406,16 +408,17 @@ __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __res
   if (claim) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
     const uint32_t nb = next + rank;
-    const uint32_t old = __hip_atomic_load(bi + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if (old < K.n_buckets) C->bucket_fill[old] = BUCKET_RECORDS;  // the full bucket
+    if (oldid < K.n_buckets) C->bucket_fill[oldid] = BUCKET_RECORDS;  // the full bucket
     if (nb < K.n_buckets) {
       C->bucket_tile[nb] = t;
       atomicAdd(C->tile_nb + t, 1u);
-      __hip_atomic_store(bi + t, nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      atomicSub(bf + t, BUCKET_RECORDS);  // -> the number that overflowed into it
+      // id: oldid -> nb, fill: -BUCKET_RECORDS (-> the number that overflowed into it); the
+      // fill is >= BUCKET_RECORDS here, so the low word never borrows from the id
+      const unsigned long long delta = ((unsigned long long)(nb - oldid) << 32) - BUCKET_RECORDS;
+      __hip_atomic_fetch_add(bs + t, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     } else {
-      __hip_atomic_store(bi + t, BUCKET_EXHAUSTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-      __hip_atomic_store(bf + t, FILL_EXHAUSTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      __hip_atomic_store(bs + t, bucket_word(BUCKET_EXHAUSTED, FILL_EXHAUSTED), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
   }
   W.next = next + nc;
@@ -423,7 +426,7 @@ __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __res
   __builtin_amdgcn_wave_barrier();
   bool spill = false;
   if (over) {
-    const uint32_t b = __hip_atomic_load(bi + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const uint32_t b = (uint32_t)(__hip_atomic_load(bs + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> 32);
     if (b < K.n_buckets && pos - BUCKET_RECORDS < BUCKET_RECORDS) {
       K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos - BUCKET_RECORDS)] = rec;
     } else {  // pool exhausted: stay correct with fp64 atomics
@@ -435,30 +438,28 @@ __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __res
 }
 
 __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __restrict__ C, BucketLog& W, bool dep,
-                                              uint32_t vox, double val, uint32_t& overflow, uint32_t* bf,
-                                              uint32_t* bi) {
+                                              uint32_t vox, double val, uint32_t& overflow,
+                                              unsigned long long* bs) {
   if (!__ballot(dep)) return;
   const uint32_t t = vox >> TILE_SHIFT;
   const unsigned long long rec = pack_record(vox, val);
-  uint32_t pos = 0;
-  if (dep) pos = atomicAdd(bf + t, 1u);
+  unsigned long long w = 0;
+  if (dep) w = __hip_atomic_fetch_add(bs + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  const uint32_t pos = (uint32_t)w, b = (uint32_t)(w >> 32);
   const bool over = dep && pos >= BUCKET_RECORDS;
-  if (dep && !over) {
-    const uint32_t b = __hip_atomic_load(bi + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + pos] = rec;
-  }
-  if (__ballot(over)) bucket_slow(K, C, W, over, pos, t, rec, vox, val, overflow, bf, bi);
+  if (dep && !over) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + pos] = rec;
+  if (__ballot(over)) bucket_slow(K, C, W, over, pos, b, t, rec, vox, val, overflow, bs);
 }
 
 // End of the kernel for one wave: record the fill of every open bucket and retire the unused
 // ids of the batch; add the wave's record and overflow counts.
 __device__ __forceinline__ void close_buckets(const KParams& K, const KCold* __restrict__ C, const BucketLog& W,
-                                              uint32_t records, uint32_t overflow, const uint32_t* bf,
-                                              const uint32_t* bi) {
+                                              uint32_t records, uint32_t overflow, const unsigned long long* bs) {
   const int lane = threadIdx.x & 63;
   for (uint32_t t = lane; t < K.bucket_tiles; t += 64) {
-    const uint32_t b = bi[t];
-    if (b < K.n_buckets) C->bucket_fill[b] = bf[t] < BUCKET_RECORDS ? bf[t] : BUCKET_RECORDS;
+    const unsigned long long w = bs[t];
+    const uint32_t b = (uint32_t)(w >> 32), f = (uint32_t)w;
+    if (b < K.n_buckets) C->bucket_fill[b] = f < BUCKET_RECORDS ? f : BUCKET_RECORDS;
   }
   const uint32_t id = W.next + lane;
   if (id < W.end && id < K.n_buckets) C->bucket_tile[id] = TILE_INVALID;

@@ -51,26 +51,35 @@ __host__ __device__ __forceinline__ double csg(int32_t op, double d1, double d2,
 // invert(translate(c)), setupGeometry.f90:64,289), so ((x*1 + y*0) + z*0) + t = x + t.
 // This is exact for every finite input; at most the sign of a zero result differs, which
 // no SDF below can observe (they use squares, abs, min/max and comparisons with 0).
-__host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos, bool translate_only) {
-  const double* P = nd->param;
-  const double* t = nd->transform;
-  const V3 p = translate_only ? v3(pos.x + t[3], pos.y + t[7], pos.z + t[11]) : dotmat(pos, t);
-  switch (nd->kind) {
+//
+// sdf_prim_s reads the primitive's kind, transform t[0..11] and parameters P[0..7] with a
+// stride of S doubles (S = 1: a node; S = 64: the cooperative EVAL's LDS table, one column
+// per lane, transport.h); sdf_prim is it applied to a node.
+template <int S>
+__host__ __device__ __forceinline__ double sdf_prim_s(int32_t kind, const double* __restrict__ t,
+                                                      const double* __restrict__ P_, V3 pos, bool translate_only) {
+#define P(i) P_[(i) * S]
+#define T(i) t[(i) * S]
+  const V3 p = translate_only ? v3(pos.x + T(3), pos.y + T(7), pos.z + T(11))
+                              : v3(T(0) * pos.x + T(1) * pos.y + T(2) * pos.z + T(3),
+                                   T(4) * pos.x + T(5) * pos.y + T(6) * pos.z + T(7),
+                                   T(8) * pos.x + T(9) * pos.y + T(10) * pos.z + T(11));  // dotmat
+  switch (kind) {
     case SMCRT_SDF_SPHERE:  // :494-508
-      return sqrt(p.x * p.x + p.y * p.y + p.z * p.z) - P[0];
+      return sqrt(p.x * p.x + p.y * p.y + p.z * p.z) - P(0);
     case SMCRT_SDF_BOX: {  // :510-525
-      const V3 q = vabs(p) - v3(P[0], P[1], P[2]);
+      const V3 q = vabs(p) - v3(P(0), P(1), P(2));
       return len(v3(dmax(q.x, 0.0), dmax(q.y, 0.0), dmax(q.z, 0.0))) + dmin(dmax(q.x, dmax(q.y, q.z)), 0.0);
     }
     case SMCRT_SDF_TORUS: {  // :527-542
-      const V3 q = v3(len(v3(p.x, 0.0, p.z)) - P[0], p.y, 0.0);
-      return len(q) - P[1];
+      const V3 q = v3(len(v3(p.x, 0.0, p.z)) - P(0), p.y, 0.0);
+      return len(q) - P(1);
     }
     case SMCRT_SDF_CYLINDER: {  // :544-581
-      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const V3 a = v3(P(0), P(1), P(2)), b = v3(P(3), P(4), P(5));
       const V3 ba = b - a, pa = p - a;
       const double baba = dot(ba, ba), paba = dot(pa, ba);
-      const double x = len(mul(pa, baba) - mul(ba, paba)) - P[6] * baba;
+      const double x = len(mul(pa, baba) - mul(ba, paba)) - P(6) * baba;
       const double y = fabs(paba - baba * 0.5) - baba * 0.5;
       const double x2 = x * x, y2 = (y * y) * baba;
       double d;
@@ -83,23 +92,23 @@ __host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __rest
     }
     case SMCRT_SDF_TRIPRISM: {  // :583-597
       const V3 q = vabs(p);
-      return dmax(q.z - P[1], dmax(q.x * 0.866025 + p.y * 0.5, -p.y) - P[0] * 0.5);
+      return dmax(q.z - P(1), dmax(q.x * 0.866025 + p.y * 0.5, -p.y) - P(0) * 0.5);
     }
     case SMCRT_SDF_SEGMENT: {  // :599-626
-      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const V3 a = v3(P(0), P(1), P(2)), b = v3(P(3), P(4), P(5));
       const V3 pa = p - a, ba = b - a;
       const double h = clampd(dot(pa, ba) / dot(ba, ba), 0.0, 1.0);
       return len(pa - mul(ba, h)) - 0.1;
     }
     case SMCRT_SDF_CAPSULE: {  // :628-648
-      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
+      const V3 a = v3(P(0), P(1), P(2)), b = v3(P(3), P(4), P(5));
       const V3 pa = p - a, ba = b - a;
       const double h = clampd(dot(pa, ba) / dot(ba, ba), 0.0, 1.0);
-      return len(pa - mul(ba, h)) - P[6];
+      return len(pa - mul(ba, h)) - P(6);
     }
     case SMCRT_SDF_CONE: {  // :650-686
-      const V3 a = v3(P[0], P[1], P[2]), b = v3(P[3], P[4], P[5]);
-      const double ra = P[6], rb = P[7];
+      const V3 a = v3(P(0), P(1), P(2)), b = v3(P(3), P(4), P(5));
+      const double ra = P(6), rb = P(7);
       const double rba = rb - ra;
       const double baba = dot(b - a, b - a);
       const double papa = dot(p - a, p - a);
@@ -115,7 +124,7 @@ __host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __rest
       return s * sqrt(dmin(cax * cax + baba * (cay * cay), cbx * cbx + baba * (cby * cby)));
     }
     case SMCRT_SDF_EGG: {  // :688-718
-      const double r1 = P[0], r2 = P[1], hh = P[2];
+      const double r1 = P(0), r2 = P(1), hh = P(2);
       const V3 pin = v3(fabs(p.x), p.y, p.z);
       const double r = r1 - r2;
       const double h_in = hh + r;
@@ -125,11 +134,18 @@ __host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __rest
       return len(pin + v3(l, 0.0, 0.0)) - (r1 + l);
     }
     case SMCRT_SDF_PLANE:  // :720-735
-      return dot(p, v3(P[0], P[1], P[2]));
+      return dot(p, v3(P(0), P(1), P(2)));
     default:
       return __builtin_nan("");
   }
+#undef P
+#undef T
 }
+
+__host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos, bool translate_only) {
+  return sdf_prim_s<1>(nd->kind, nd->transform, nd->param, pos, translate_only);
+}
+
 
 // The SDF array flattened into one instruction stream, so the kernel evaluates every
 // top-level SDF (and every CSG child, folded left to right as eval_model does,

@@ -102,11 +102,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   // bucketed path's open bucket per tile (fill | id: 2 * bucket_tiles words)
   const uint32_t wave_words = K.bucket_tiles ? 2 * K.bucket_tiles : K.hist_tiles;
   uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * wave_words;
-  uint32_t* const bfill = whist;
-  uint32_t* const bid = whist + K.bucket_tiles;
-  if (K.bucket_tiles) init_buckets(bfill, bid, K.bucket_tiles);
+  // (wave_words is even and sh_dyn 8-byte aligned: the bucket words are 8-byte aligned)
+  unsigned long long* const bstate = (unsigned long long*)whist;
+  if (K.bucket_tiles) init_buckets(bstate, K.bucket_tiles);
   else
     for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
+  // the cooperative EVAL's primitive table (COOP instantiations), after the wave words
+  double* const ctab = sh_dyn + hist_off + 2 * wave_words;
+  if constexpr (COOP) {
+    if (K.ctab)
+      for (int i = threadIdx.x; i < CTAB_DOUBLES; i += blockDim.x) ctab[i] = K.ctab[i];
+  }
 #pragma unroll
   for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
 #pragma unroll
@@ -217,7 +223,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       const int32_t capj = fres ? L.old_layer : 0;
       const bool mask_le = test_kernel && L.st == ST_LAYER;
       const uint64_t evm = __ballot(have);
-      if (COOP && (uint32_t)__popcll(evm) <= (uint32_t)K.coop_lanes) {  // a sparse wave: one lane at a time
+      if (COOP && K.ctab && (uint32_t)__popcll(evm) <= (uint32_t)K.coop_lanes) {  // sparse wave, LDS table
+        const V3 q = eval_query(L);
+        uint64_t m = evm;
+        while (m) {  // (m and l are scalars: the lane's query reaches the wave by readlane)
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          const V3 ql = v3(readlane_f64(q.x, l), readlane_f64(q.y, l), readlane_f64(q.z, l));
+          const EvalOut o = eval_coop_tab(ctab, K.n_top, ql, __builtin_amdgcn_readlane((int)mask_le, l) != 0,
+                                          __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l));
+          if (lane_id == l) R = o;
+        }
+      } else if (COOP && (uint32_t)__popcll(evm) <= (uint32_t)K.coop_lanes) {  // a sparse wave: one lane at a time
         const V3 q = eval_query(L);
         uint64_t m = evm;
         while (m) {
@@ -408,7 +425,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
         if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, C, W, dep, vox, val, overflow, whist); }
 #else
         if (binned) {
-          if (K.bucket_tiles) emit_bucketed(K, C, WB, dep, vox, val, overflow, bfill, bid);
+          if (K.bucket_tiles) emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
           else emit_deposits(K, C, W, dep, vox, val, overflow, whist);
         }
 #endif
@@ -591,7 +608,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   }
 
   if (binned) {
-    if (K.bucket_tiles) close_buckets(K, C, WB, w_dep - overflow, overflow, bfill, bid);
+    if (K.bucket_tiles) close_buckets(K, C, WB, w_dep - overflow, overflow, bstate);
     else close_log(K, C, W, overflow, whist);
   }
 
@@ -692,6 +709,7 @@ struct smcrt_scene {
   ProgOp* d_prog = nullptr;
   int n_prog = 0;
   int coop_lanes = 0;
+  double* d_ctab = nullptr;  // the cooperative EVAL's primitive table (transport.h), or NULL
   // exact SDF culling (cull.h): grid + lists + the always-evaluated program, one allocation
   CullGrid* d_cull = nullptr;
   void* d_cull_data = nullptr;
@@ -811,9 +829,10 @@ static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
 }
 
 // Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
-static size_t transport_lds(const smcrt_scene* s, uint32_t wave_words) {
+static size_t transport_lds(const smcrt_scene* s, uint32_t wave_words, bool xsrc) {
+  const bool ctab = s->d_ctab && !xsrc && s->coop_lanes > 0;  // the COOP instantiation stages it
   return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
-         (size_t)4 * wave_words * sizeof(uint32_t);
+         (size_t)4 * wave_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0);
 }
 // LDS words per wave of the deposit state (deposit.h): open buckets or the tile histogram.
 static uint32_t wave_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_tiles : s->hist_tiles; }
@@ -848,7 +867,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->fstream) (void)hipStreamSynchronize(s->fstream);
-  void* ptrs[] = {s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
+  void* ptrs[] = {s->d_ctab, s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1],
                   s->d_dep_ctl[0], s->d_dep_ctl[1], s->d_tile_count, s->d_tile_start, s->d_bin_counts[0],
@@ -968,6 +987,23 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   // A sparse wave evaluates its lanes' SDF arrays one lane at a time across the wave when
   // that is cheaper than the serial per-lane chain over all n_top tops (transport.h).
   s->coop_lanes = n_top >= 8 ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
+  // The cooperative EVAL's LDS table: at most 64 tops, none of them a model (transport.h).
+  // SMCRT_COOP_TAB=0 keeps the global-memory cooperative EVAL.
+  std::vector<double> ctab;
+  {
+    const char* ct = std::getenv("SMCRT_COOP_TAB");
+    bool ok = s->coop_lanes > 0 && n_top <= 64 && !(ct && std::string(ct) == "0");
+    for (int32_t i = 0; ok && i < n_top; ++i) ok = nodes[top[i]].kind != SMCRT_SDF_MODEL;
+    if (ok) {
+      ctab.assign(CTAB_DOUBLES, 0.0);
+      for (int32_t i = 0; i < n_top; ++i) {
+        const smcrt_sdf_node& nd = nodes[top[i]];
+        for (int r = 0; r < 12; ++r) ctab[r * 64 + i] = nd.transform[r];
+        for (int r = 0; r < 8; ++r) ctab[(12 + r) * 64 + i] = nd.param[r];
+        ctab[20 * 64 + i] = (double)nd.kind + (translate_only(top[i]) ? 16.0 : 0.0);
+      }
+    }
+  }
   // exact culling of the SDF array for many-top scenes (cull.h); SMCRT_CULL=0 turns it off
   CullHost cull;
   {
@@ -992,6 +1028,10 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   hipError_t e = hipSuccess;
   if (e == hipSuccess) e = hipMemcpy(s->d_nodes, nodes, sizeof(smcrt_sdf_node) * n_nodes, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_prog, prog.data(), sizeof(ProgOp) * prog.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess && !ctab.empty()) {
+    if ((st = dalloc(&s->d_ctab, ctab.size()))) return cleanup_fail(st);
+    e = hipMemcpy(s->d_ctab, ctab.data(), sizeof(double) * ctab.size(), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMemcpy(s->d_props, s->h_props.data(), sizeof(TopProps) * n_top, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_faces, faces.data(), sizeof(double) * faces.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && n_dets)
@@ -1094,7 +1134,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
-    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, wave_words(s)));
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, wave_words(s), x == 1));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     (x ? s->grid_blocks_x : s->grid_blocks) = cus * per_cu;
   }
@@ -1287,7 +1327,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     const smcrt_detector* a_dets = K.dets;
     const int64_t* a_off = K.det_off;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&a_dets, (void*)&a_off, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, wave_words(s)), stream));
+    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, wave_words(s), xsrc), stream));
   }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
@@ -1428,6 +1468,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.n_prog = s->n_prog;
   K.coop_lanes = s->coop_lanes;
   K.cull = s->d_cull;
+  K.ctab = s->d_ctab;
   K.inv2x = s->inv2[0]; K.inv2y = s->inv2[1]; K.inv2z = s->inv2[2];
   K.fex = s->fe[0]; K.fey = s->fe[1]; K.fez = s->fe[2];
   K.props = s->d_props;

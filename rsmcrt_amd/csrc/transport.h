@@ -108,6 +108,9 @@ struct KParams {
   uint32_t bucket_tiles, n_buckets;
   // exact SDF culling (cull.h), many-top scenes in the COOP instantiation; NULL = off
   const CullGrid* __restrict__ cull;
+  // the cooperative EVAL's table of primitives (CTAB_ROWS x 64 doubles, column = top - 1),
+  // staged in LDS by the COOP instantiation; NULL when the scene does not qualify
+  const double* __restrict__ ctab;
 };
 
 // ------------------------------------------------------------------ voxels -------
@@ -928,6 +931,88 @@ __device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restri
   r.maxloc = loc;
   r.va = capi > 0 ? __shfl(va, (capi - 1) & 63, 64) : 0.0;
   r.vb = capj > 0 ? __shfl(vb, (capj - 1) & 63, 64) : 0.0;
+  return r;
+}
+
+// ---- cooperative EVAL from an LDS table (COOP instantiation, at most 64 single-primitive
+// tops). Lane j keeps top j+1 in column j of a [CTAB_ROWS][64] fp64 table: transform rows
+// 0-11, parameters 12-19, kind + 16 * translate_only in row 20. A sparse wave evaluates one
+// lane's query point with every lane computing its own top from LDS (no vector memory on the
+// path, so nothing waits for the wave's outstanding record stores) and reduces with DPP.
+constexpr int CTAB_ROWS = 21;
+constexpr int CTAB_DOUBLES = CTAB_ROWS * 64;
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// v of the DPP source lane, or `old` where the control selects none (bound_ctrl off)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double old, double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v), o = (uint64_t)__double_as_longlong(old);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)o, (int)(uint32_t)b, CTRL, ROWS, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(o >> 32), (int)(uint32_t)(b >> 32), CTRL, ROWS, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int32_t dpp_i32(int32_t old, int32_t v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xf, false);
+}
+struct CoopAcc {
+  double minabs, minv, best;
+  int32_t loc;
+};
+// Fold b into a: the serial scan's strict compares, maxloc ties to the lowest top index.
+__device__ __forceinline__ void coop_fold(CoopAcc& a, const CoopAcc& b) {
+  if (b.minabs < a.minabs) a.minabs = b.minabs;
+  if (b.minv < a.minv) a.minv = b.minv;
+  if (b.loc != 0 && (a.loc == 0 || b.best > a.best || (b.best == a.best && b.loc < a.loc))) {
+    a.best = b.best;
+    a.loc = b.loc;
+  }
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void coop_step(CoopAcc& a) {
+  CoopAcc b;
+  b.minabs = dpp_f64<CTRL, ROWS>(__builtin_inf(), a.minabs);
+  b.minv = dpp_f64<CTRL, ROWS>(__builtin_inf(), a.minv);
+  b.best = dpp_f64<CTRL, ROWS>(-__builtin_inf(), a.best);
+  b.loc = dpp_i32<CTRL, ROWS>(0, a.loc);
+  coop_fold(a, b);
+}
+// The whole wave evaluates the SDF array at the wave-uniform point q (all lanes active).
+__device__ __forceinline__ EvalOut eval_coop_tab(const double* ct, int32_t n_top, V3 q, bool mask_le, int32_t capi,
+                                                 int32_t capj) {
+  const int lane = (int)(threadIdx.x & 63);
+  CoopAcc a;
+  a.minabs = __builtin_inf(); a.minv = __builtin_inf(); a.best = -__builtin_inf(); a.loc = 0;
+  double d = 0.0;
+  if (lane < n_top) {
+    const double kc = ct[20 * 64 + lane];
+    const int32_t kind = (int32_t)kc & 15;
+    d = sdf_prim_s<64>(kind, ct + lane, ct + 12 * 64 + lane, q, kc >= 16.0);
+    a.minabs = fabs(d);
+    a.minv = d;
+    const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+    if (neg) { a.best = d; a.loc = lane + 1; }
+  }
+  // inclusive row scans (row_shr 1, 2, 4, 8), then row 0 -> 1 and 2 -> 3 (row_bcast:15),
+  // then rows 0-1 -> 2-3 (row_bcast:31): lane 63 holds the wave's fold
+  coop_step<0x111, 0xf>(a);
+  coop_step<0x112, 0xf>(a);
+  coop_step<0x114, 0xf>(a);
+  coop_step<0x118, 0xf>(a);
+  coop_step<0x142, 0xa>(a);
+  coop_step<0x143, 0xc>(a);
+  EvalOut r;
+  r.minabs = readlane_f64(a.minabs, 63);
+  r.minv = readlane_f64(a.minv, 63);
+  r.maxloc = __builtin_amdgcn_readlane(a.loc, 63);
+  r.va = capi > 0 ? readlane_f64(d, capi - 1) : 0.0;
+  r.vb = capj > 0 ? readlane_f64(d, capj - 1) : 0.0;
   return r;
 }
 

@@ -72,3 +72,72 @@ def test_example_reproduces_scat_test_kat(lib_path, tmp_path, kats):
     k = kats["scat_test_nscatt"]
     assert abs(v - k["value"]) <= k["thr"], out
     assert re.search(r"photons = 100000\b", out), out
+
+
+# ---- the conversion glue (bindings/fortran/smcrt_glue.f90) ----------
+GLUE_SCENES = ("scat_test", "aptran", "validation1", "omg", "test_dects")
+SRC_FIELDS = ("pos", "dir", "p1", "p2", "p3", "radius", "beam_size", "focal_length", "rlo", "rhi", "sigma", "rotation")
+
+
+def _read_glue(path):
+    """One glue_scenes.f90 output: counts, node table, top, detectors, source fields."""
+    import numpy as np
+    raw = open(path, "rb").read()
+    n_nodes, n_top, n_dets = np.frombuffer(raw[:12], dtype=np.int32)
+    off = 12
+    nodes = (abi.SdfNode * int(n_nodes)).from_buffer_copy(raw[off:off + n_nodes * C.sizeof(abi.SdfNode)])
+    off += n_nodes * C.sizeof(abi.SdfNode)
+    top = np.frombuffer(raw[off:off + 4 * n_top], dtype=np.int32)
+    off += 4 * n_top
+    dets = (abi.Detector * max(1, int(n_dets))).from_buffer_copy(
+        raw[off:off + n_dets * C.sizeof(abi.Detector)] + b"\0" * (0 if n_dets else C.sizeof(abi.Detector)))
+    off += n_dets * C.sizeof(abi.Detector)
+    kind, beam = np.frombuffer(raw[off:off + 8], dtype=np.int32)
+    vals = np.frombuffer(raw[off + 8:], dtype=np.float64)
+    sizes = (3, 3, 3, 3, 3, 1, 1, 1, 1, 1, 1, 3)
+    src, k = {"kind": int(kind), "beam": int(beam)}, 0
+    for name, n in zip(SRC_FIELDS, sizes):
+        src[name] = list(vals[k:k + n])
+        k += n
+    assert k == len(vals)
+    return int(n_nodes), list(top), nodes, [dets[i] for i in range(n_dets)], src
+
+
+def _fields(struct):
+    out = {}
+    for name, _ in struct._fields_:
+        if name.startswith("reserved"):
+            continue
+        v = getattr(struct, name)
+        out[name] = list(v) if hasattr(v, "__len__") else v
+    return out
+
+
+def test_glue_tables_match_the_toml_front_end(lib_path, tmp_path):
+    """smcrt_glue's constructors, flattening, detector and source conversion (driven by
+    glue_scenes.f90 as setupGeometry.f90 / parse_detectors.f90 / parse_source.f90 would) give
+    the same node, top, detector and source tables, field for field and bit for bit, as the
+    C++ front end's smcrt_job_scene on the same res/*.toml files."""
+    from rsmcrt_amd.job import Job
+    libdir = os.path.dirname(lib_path)
+    for f in ("smcrt_mod.f90", "smcrt_glue.f90", "glue_scenes.f90"):
+        shutil.copy(os.path.join(FDIR, f), tmp_path)
+    subprocess.run([FC, "-O2", "-c", "smcrt_mod.f90"], cwd=tmp_path, check=True)
+    subprocess.run([FC, "-O2", "-c", "smcrt_glue.f90"], cwd=tmp_path, check=True)
+    subprocess.run([FC, "-O2", "-o", "glue_scenes", "glue_scenes.f90", "smcrt_glue.o", "smcrt_mod.o",
+                    f"-L{libdir}", "-lsmcrt", f"-Wl,-rpath,{libdir}"], cwd=tmp_path, check=True)
+    subprocess.run([str(tmp_path / "glue_scenes"), str(tmp_path)], check=True)
+    for name in GLUE_SCENES:
+        n_nodes, top, nodes, dets, src = _read_glue(tmp_path / f"{name}.bin")
+        j = Job(os.path.join(ROOT, "tests", "golden", "res", f"{name}.toml"))
+        d = j.desc
+        assert n_nodes == d.n_nodes and len(top) == d.n_top and len(dets) == d.n_dets, name
+        assert top == list(j.top[:d.n_top]), name
+        for i in range(n_nodes):
+            assert _fields(nodes[i]) == _fields(j.nodes[i]), (name, "node", i)
+        for i, det in enumerate(dets):
+            assert _fields(det) == _fields(j.dets[i]), (name, "detector", i)
+        assert src["kind"] == d.source.kind and src["beam"] == d.source.beam, name
+        for k in SRC_FIELDS:
+            want = getattr(d.source, k)
+            assert src[k] == (list(want) if hasattr(want, "__len__") else [want]), (name, "source", k)
