@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <limits>
 #include <thread>
 
@@ -150,9 +151,12 @@ double box_dist(const double* clo, const double* chi, const Bound& b) {
 CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t* top, int32_t n_top,
                     const double grid_half[3]) {
   CullHost H;
-  constexpr int32_t MIN_TOPS = 16, K_NEAREST = 8, N_PROBE = 16, MAX_LIST = 64;
-  constexpr double CELLS_PER_TOP = 64.0, ALWAYS_FRACTION = 0.25;
-  constexpr double MAX_CELLS = 1 << 18;
+  constexpr int32_t MIN_TOPS = 16, N_PROBE = 16;
+  constexpr double ALWAYS_FRACTION = 0.25;
+  // grid resolution and list cap (SMCRT_CULL_CPT / _MAX_CELLS / _MAX_LIST override, experiments)
+  auto env = [](const char* k, double d) { const char* v = std::getenv(k); return v ? std::atof(v) : d; };
+  const double CELLS_PER_TOP = env("SMCRT_CULL_CPT", 64.0), MAX_CELLS = env("SMCRT_CULL_MAX_CELLS", 1 << 18);
+  const int32_t MAX_LIST = (int32_t)env("SMCRT_CULL_MAX_LIST", 64), K_NEAREST = (int32_t)env("SMCRT_CULL_K", 8);
   if (n_top < MIN_TOPS) return H;
   std::vector<Bound> bd((size_t)n_top);
   Bound dom;

@@ -59,6 +59,13 @@ __device__ unsigned long long g_diag[72];
 __device__ unsigned long long g_diag_t[9];
 #endif
 
+// a sparse wave of a culled scene evaluates its lanes' query points one at a time with the
+// whole wave (eval_culled_coop) when at most this many lanes need an EVAL
+#ifndef SMCRT_COOP_CULL_LANES
+#define SMCRT_COOP_CULL_LANES 8
+#endif
+constexpr uint32_t COOP_CULL_LANES = SMCRT_COOP_CULL_LANES;
+
 template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
 #ifndef SMCRT_WAVES_PER_EU
 #define SMCRT_WAVES_PER_EU 3
@@ -234,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
                                           __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l));
           if (lane_id == l) R = o;
         }
-      } else if (COOP && (uint32_t)__popcll(evm) <= (uint32_t)K.coop_lanes) {  // a sparse wave: one lane at a time
+      } else if (COOP && !K.cull && (uint32_t)__popcll(evm) <= (uint32_t)K.coop_lanes) {  // sparse, one lane at a time
         const V3 q = eval_query(L);
         uint64_t m = evm;
         while (m) {
@@ -243,6 +250,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           const V3 ql = v3(__shfl(q.x, l, 64), __shfl(q.y, l, 64), __shfl(q.z, l, 64));
           const EvalOut o = eval_sdfs_coop(nodes, prog, K.n_prog, K.n_top, ql, __shfl((int)mask_le, l, 64) != 0,
                                            __shfl(capi, l, 64), __shfl(capj, l, 64));
+          if (lane_id == l) R = o;
+        }
+      } else if (COOP && K.cull && (uint32_t)__popcll(evm) <= COOP_CULL_LANES) {  // sparse wave, culled
+        const V3 q = eval_query(L);
+        uint64_t m = evm;
+        while (m) {
+          const int l = __builtin_ctzll(m);
+          m &= m - 1;
+          const V3 ql = v3(readlane_f64(q.x, l), readlane_f64(q.y, l), readlane_f64(q.z, l));
+          const EvalOut o = eval_culled_coop(nodes, prog, K.n_prog, K.cull, ql,
+                                             __builtin_amdgcn_readlane((int)mask_le, l) != 0,
+                                             __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l));
           if (lane_id == l) R = o;
         }
       } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)

@@ -1120,4 +1120,104 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
   return r;
 }
 
+// Culled EVAL for ONE wave-uniform query point q with the whole wave cooperating: the
+// always-evaluated tops wave-uniformly, then lane j takes entry b + j (+64, ...) of q's cell
+// list and the wave reduces with DPP (eval_coop_tab's fold), so a sparse wave pays one or two
+// memory latencies per list instead of one per entry and lane. Results equal eval_culled's
+// (and so eval_sdfs'): min and abs-min are order free, maxloc ties go to the lowest index.
+// Call with all lanes active; q, mask_le, capi and capj must be wave-uniform.
+__device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __restrict__ nodes,
+                                                    const ProgOp* __restrict__ prog, int32_t n_prog,
+                                                    const CullGrid* __restrict__ G, V3 q, bool mask_le,
+                                                    int32_t capi, int32_t capj) {
+  const int lane = (int)(threadIdx.x & 63);
+  EvalOut r;
+  r.minabs = __builtin_inf();
+  r.minv = __builtin_inf();
+  r.va = 0.0; r.vb = 0.0;
+  r.maxloc = 0;
+  double best = -__builtin_inf();
+  {  // the unboundable tops, wave-uniform (as eval_culled)
+    const ProgOp* __restrict__ pa = (const ProgOp*)G->prog_always;
+    const int32_t na = G->n_prog_always;
+    double acc = 0.0;
+    for (int32_t ip = 0; ip < na; ++ip) {
+      const ProgOp op = pa[ip];
+      const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
+      const double v = sdf_prim(nodes + node, q, op.translate_only != 0);
+      if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
+      else acc = csg(op.op, acc, v, op.k);
+      if (op.top > 0) {
+        const double d = acc;
+        const double a = fabs(d);
+        if (a < r.minabs) r.minabs = a;
+        if (d < r.minv) r.minv = d;
+        const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+        if (neg && (r.maxloc == 0 || d > best)) { best = d; r.maxloc = op.top; }
+      }
+    }
+  }
+  bool full = capi != 0 || capj != 0;
+  const double fx = (q.x - G->lo[0]) * G->inv_cell, fy = (q.y - G->lo[1]) * G->inv_cell,
+               fz = (q.z - G->lo[2]) * G->inv_cell;
+  if (!(fx >= 0.0 && fx < (double)G->n[0] && fy >= 0.0 && fy < (double)G->n[1] && fz >= 0.0 &&
+        fz < (double)G->n[2]))
+    full = true;
+  if (!full) {
+    const int32_t ix = (int32_t)fx, iy = (int32_t)fy, iz = (int32_t)fz;
+    const uint32_t c = (uint32_t)ix + (uint32_t)G->n[0] * ((uint32_t)iy + (uint32_t)G->n[1] * (uint32_t)iz);
+    const uint32_t b = G->off[c], e = G->off[c + 1];
+    const uint2* __restrict__ ent = (const uint2*)G->list;
+    CoopAcc a;
+    a.minabs = r.minabs; a.minv = r.minv; a.best = best; a.loc = r.maxloc;  // (every lane: the uniform part)
+    for (uint32_t k0 = b; k0 < e; k0 += 64) {
+      const uint32_t k = k0 + (uint32_t)lane;
+      if (k < e) {
+        const uint2 en = ent[k];
+        const int32_t i = (int32_t)(en.x & CULL_TOP_MASK);
+        double d;
+        if (en.x & CULL_MODEL) {
+          const int32_t o0 = prog[n_prog + i].node, o1 = prog[n_prog + i + 1].node;
+          double acc = 0.0;
+          for (int32_t ip = o0; ip < o1; ++ip) {
+            const ProgOp op = prog[ip];
+            const double v = sdf_prim(nodes + op.node, q, op.translate_only != 0);
+            if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
+            else acc = csg(op.op, acc, v, op.k);
+          }
+          d = acc;
+        } else {
+          d = sdf_prim(nodes + en.y, q, (en.x & CULL_TRANSLATE) != 0);
+        }
+        CoopAcc o;
+        o.minabs = fabs(d);
+        o.minv = d;
+        const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+        o.best = neg ? d : -__builtin_inf();
+        o.loc = neg ? i + 1 : 0;
+        coop_fold(a, o);
+      }
+    }
+    coop_step<0x111, 0xf>(a);
+    coop_step<0x112, 0xf>(a);
+    coop_step<0x114, 0xf>(a);
+    coop_step<0x118, 0xf>(a);
+    coop_step<0x142, 0xa>(a);
+    coop_step<0x143, 0xc>(a);
+    r.minabs = readlane_f64(a.minabs, 63);
+    r.minv = readlane_f64(a.minv, 63);
+    r.maxloc = __builtin_amdgcn_readlane(a.loc, 63);
+    // every unlisted top has ds >= max(distance to the cell's boundary, lb[c])
+    const double cx = G->lo[0] + (double)ix * G->cell, cy = G->lo[1] + (double)iy * G->cell,
+                 cz = G->lo[2] + (double)iz * G->cell;
+    double h = dmin(dmin(dmin(q.x - cx, cx + G->cell - q.x), dmin(q.y - cy, cy + G->cell - q.y)),
+                    dmin(q.z - cz, cz + G->cell - q.z));
+    h = dmax(h, 0.0);
+    const double T = dmax(h, G->lb[c]) * (1.0 - 1e-12);
+    if (!(r.minabs < T)) full = true;
+  }
+  if (full) r = eval_sdfs(nodes, prog, n_prog, q, mask_le, capi, capj);
+  return r;
+}
+
 }  // namespace smcrt
