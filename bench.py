@@ -53,7 +53,7 @@ def workload(name, grid_n):
         return (builders.setup_sphere_scene(builders.random_sphere_list(40)), scene.grid(n, n, n, 1.0, 1.0, 1.0),
                 scene.uniform_source((-1.0, -1.0, 0.9999999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0)),
                 [], f"M2 sphere_scene (res/sphere.toml): 40 random spheres n=1.37, uniform source z=0.9999999, "
-                f"{n}^3 grid (setupGeometry.f90:250-294)", 400_000)
+                f"{n}^3 grid (setupGeometry.f90:250-294)", 800_000)
     if name == "m3":
         n = grid_n or 128
         return (builders.setup_tran_and_jacques(), scene.grid(n, n, n, 1.0, 1.0, 1.0),
@@ -73,7 +73,7 @@ def workload(name, grid_n):
         return (builders.skin_layers(), scene.grid(n, n, n, 0.05, 0.05, 0.05),
                 scene.pencil_source((0.0, 0.0, 0.0499), (0.0, 0.0, -1.0)), dets,
                 f"M5 (build-defined) skin: layered boxes with Fresnel at every interface, pencil beam, circle + "
-                f"annulus reflectance detectors, {n}^3 grid", 8_000_000)
+                f"annulus reflectance detectors, {n}^3 grid", 6_000_000)
     raise ValueError(name)
 
 

@@ -714,6 +714,11 @@ int dalloc(T** p, size_t n) {
 
 }  // namespace
 
+// Record-log slots (and internal launch streams) per scene: launches whose pools are small
+// enough run up to MAX_SLOTS deep, so long-tailed launches overlap more than pairwise.
+constexpr int MAX_SLOTS = 4;
+constexpr uint64_t DEEP_SLOT_BYTES = 24ull << 30;  // a slot pool at most this large: MAX_SLOTS slots
+
 struct smcrt_scene {
   int device = 0;
   int n_nodes = 0, n_top = 0, n_dets = 0;
@@ -740,16 +745,16 @@ struct smcrt_scene {
   double* d_faces = nullptr;
   smcrt_detector* d_dets = nullptr;
   int64_t* d_det_off = nullptr;
-  unsigned long long* d_queue = nullptr;  // work-queue heads: [0], [1] internal streams, [2] caller stream
-  // SMCRT_FLAG_OVERLAP: launches alternate between two internal streams (lstream), so the next
-  // launch's blocks fill the CUs its predecessor's tail leaves idle
-  hipStream_t lstream[2] = {nullptr, nullptr};
-  hipEvent_t lev[2] = {nullptr, nullptr};  // the last launch on lstream[i] is done
+  unsigned long long* d_queue = nullptr;  // work-queue heads: [i] internal stream i, [MAX_SLOTS] caller stream
+  // SMCRT_FLAG_OVERLAP: launches rotate over n_slots internal streams (lstream), so the next
+  // launches' blocks fill the CUs their predecessors' tails leave idle
+  hipStream_t lstream[MAX_SLOTS] = {};
+  hipEvent_t lev[MAX_SLOTS] = {};  // the last launch on lstream[i] is done
   hipEvent_t ev_in = nullptr;              // the caller's work before an overlapped call
-  bool lpending[2] = {false, false};
+  bool lpending[MAX_SLOTS] = {};
   int lturn = 0;
-  KCold* d_cold = nullptr;  // COLD_SLOTS launch slots (ring, stream-ordered writes)
-  uint64_t cold_seq = 0;
+  KCold* d_cold = nullptr;  // launch parameters: COLD_PER_STREAM ring slots per launch stream
+  uint64_t cold_seq[MAX_SLOTS + 1] = {};
   // tallies owned by the scene for the synchronous smcrt_run
   double* d_grids = nullptr;  // jmean | absorb | emission
   double* d_small = nullptr;  // det bins | nscatt | moments(24)
@@ -771,21 +776,24 @@ struct smcrt_scene {
   uint32_t n_tiles = 0;
   // Two record-log slots, used by alternate launches: the fold of launch k (on fstream)
   // reads its slot while launch k+1's transport kernel fills the other.
-  unsigned long long* d_pool[2] = {nullptr, nullptr};  // record log, cap records
+  // record-log slots in use (2, or MAX_SLOTS when a slot's pool is small: ensure_pool), and as
+  // many internal launch streams; a launch's fold frees its slot
+  int n_slots = 2;
+  unsigned long long* d_pool[MAX_SLOTS] = {};  // record log, cap records
   unsigned long long* d_sorted = nullptr;  // tile-sorted records (folds are serial on fstream)
   // bucketed path: per slot the tile of each bucket id (bucket fills use d_chunk_fill, the
   // per-tile bucket counts d_bin_counts); shared by the serial folds: ids in tile order
-  uint32_t* d_bucket_tile[2] = {nullptr, nullptr};
+  uint32_t* d_bucket_tile[MAX_SLOTS] = {};
   uint32_t* d_order = nullptr;
-  uint32_t* d_chunk_fill[2] = {nullptr, nullptr};
-  uint32_t* d_dep_ctl[2] = {nullptr, nullptr};  // [0] chunks taken [1] overflow [2] pieces [3] records
+  uint32_t* d_chunk_fill[MAX_SLOTS] = {};
+  uint32_t* d_dep_ctl[MAX_SLOTS] = {};  // [0] chunks taken [1] overflow [2] pieces [3] records
   uint32_t* d_tile_count = nullptr;  // n_tiles
   uint32_t* d_tile_start = nullptr;  // n_tiles
-  uint32_t* d_bin_counts[2] = {nullptr, nullptr};  // [n_tiles][BIN_BLOCKS]
+  uint32_t* d_bin_counts[MAX_SLOTS] = {};  // [n_tiles][BIN_BLOCKS]
   hipStream_t fstream = nullptr;  // the deposit folds
   hipEvent_t ev_t = nullptr;      // a transport launch finished (fstream waits on it)
-  hipEvent_t ev_f[2] = {nullptr, nullptr};  // the fold of slot i finished
-  bool f_pending[2] = {false, false};
+  hipEvent_t ev_f[MAX_SLOTS] = {};  // the fold of slot i finished
+  bool f_pending[MAX_SLOTS] = {};
   int slot = 0, last_slot = -1;
   size_t scatter_lds = 0;
   Piece* d_pieces = nullptr;
@@ -793,8 +801,8 @@ struct smcrt_scene {
   double rpp_est = 1024.0;           // deposit records per photon, refined from past launches
   bool rpp_measured = false;
   uint32_t* h_ctl = nullptr;         // pinned copies of dep_ctl, 8 words per slot ([4] = photons)
-  hipEvent_t ctl_ev[2] = {nullptr, nullptr};
-  bool ctl_pending[2] = {false, false};
+  hipEvent_t ctl_ev[MAX_SLOTS] = {};
+  bool ctl_pending[MAX_SLOTS] = {};
   bool force_atomic = false;  // SMCRT_DEPOSIT=atomic
   uint64_t pool_cap_chunks = 0;  // SMCRT_POOL_CAP (records; tests of pool exhaustion): 0 = none
   // smcrt_scene_kernel_times: event quads (before / after transport on the launch stream,
@@ -808,7 +816,8 @@ struct smcrt_scene {
 };
 
 constexpr size_t MAX_TIMED = 256;
-constexpr uint64_t COLD_SLOTS = 64;
+constexpr uint64_t COLD_PER_STREAM = 16;
+constexpr uint64_t COLD_SLOTS = COLD_PER_STREAM * (MAX_SLOTS + 1);  // a ring per launch stream
 constexpr uint32_t MAX_FUSED_HIST_TILES = 512;  // 8 KiB of LDS per block for the wave histograms
 // Record pool: record indices in the bin kernels are 32-bit, so at most 2^32 - 2^28 records
 // (30 GiB, plus the same again for the sorted copy) per launch; a launch that would need more
@@ -888,16 +897,16 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   if (s->fstream) (void)hipStreamSynchronize(s->fstream);
   void* ptrs[] = {s->d_ctab, s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
-                  s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1],
-                  s->d_dep_ctl[0], s->d_dep_ctl[1], s->d_tile_count, s->d_tile_start, s->d_bin_counts[0],
-                  s->d_bin_counts[1], s->d_pieces, s->d_bucket_tile[0], s->d_bucket_tile[1], s->d_order,
-                  s->d_cull, s->d_cull_data};
-  for (int i = 0; i < 2; ++i) {
+                  s->d_sorted, s->d_tile_count, s->d_tile_start, s->d_pieces, s->d_order, s->d_cull, s->d_cull_data};
+  for (int i = 0; i < MAX_SLOTS; ++i) {
+    void* per[] = {s->d_pool[i], s->d_chunk_fill[i], s->d_dep_ctl[i], s->d_bin_counts[i], s->d_bucket_tile[i]};
+    for (void* p : per)
+      if (p) (void)hipFree(p);
     if (s->ctl_ev[i]) (void)hipEventDestroy(s->ctl_ev[i]);
     if (s->ev_f[i]) (void)hipEventDestroy(s->ev_f[i]);
   }
   if (s->ev_t) (void)hipEventDestroy(s->ev_t);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < MAX_SLOTS; ++i) {
     if (s->lstream[i]) (void)hipStreamSynchronize(s->lstream[i]);
     if (s->lev[i]) (void)hipEventDestroy(s->lev[i]);
     if (s->lstream[i]) (void)hipStreamDestroy(s->lstream[i]);
@@ -1039,7 +1048,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
-      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, 3)) ||
+      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 1)) ||
       (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
@@ -1058,7 +1067,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (e == hipSuccess)
     e = hipMemcpy(s->d_det_off, s->h_det_off.data(), sizeof(int64_t) * (n_dets + 1), hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
-  for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+  for (int i = 0; i < MAX_SLOTS && e == hipSuccess; ++i) {
     e = hipStreamCreateWithFlags(&s->lstream[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&s->lev[i], hipEventDisableTiming);
   }
@@ -1105,24 +1114,23 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (const char* pc = std::getenv("SMCRT_POOL_CAP"))
       s->pool_cap_chunks = std::max<uint64_t>(1, std::strtoull(pc, nullptr, 10) / CHUNK_RECORDS);
     if (s->n_tiles) {
-      if ((st = dalloc(&s->d_dep_ctl[0], 4)) || (st = dalloc(&s->d_dep_ctl[1], 4)) ||
-          (st = dalloc(&s->d_tile_count, s->n_tiles)) || (st = dalloc(&s->d_tile_start, s->n_tiles)) ||
-          (st = dalloc(&s->d_bin_counts[0], (size_t)s->n_tiles * BIN_BLOCKS)) ||
-          (st = dalloc(&s->d_bin_counts[1], (size_t)s->n_tiles * BIN_BLOCKS)))
+      if ((st = dalloc(&s->d_tile_count, s->n_tiles)) || (st = dalloc(&s->d_tile_start, s->n_tiles)))
         return cleanup_fail(st);
+      for (int i = 0; i < MAX_SLOTS; ++i)
+        if ((st = dalloc(&s->d_dep_ctl[i], 4)) || (st = dalloc(&s->d_bin_counts[i], (size_t)s->n_tiles * BIN_BLOCKS)))
+          return cleanup_fail(st);
       s->scatter_lds = scatter_lds_bytes(s->n_tiles);
       if (hipFuncSetAttribute((const void*)bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)s->scatter_lds) != hipSuccess)
         return cleanup_fail(fail(SMCRT_ERR_HIP, "bin_scatter LDS attribute"));
-      if (hipHostMalloc((void**)&s->h_ctl, 16 * sizeof(uint32_t)) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ctl_ev[0], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ctl_ev[1], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ev_f[0], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ev_f[1], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&s->ev_t, hipEventDisableTiming) != hipSuccess ||
-          hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking) != hipSuccess)
-        return cleanup_fail(fail(SMCRT_ERR_HIP, "pinned/event/stream allocation failed"));
-      std::memset(s->h_ctl, 0, 16 * sizeof(uint32_t));
+      bool ok = hipHostMalloc((void**)&s->h_ctl, 8 * MAX_SLOTS * sizeof(uint32_t)) == hipSuccess &&
+                hipEventCreateWithFlags(&s->ev_t, hipEventDisableTiming) == hipSuccess &&
+                hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking) == hipSuccess;
+      for (int i = 0; ok && i < MAX_SLOTS; ++i)
+        ok = hipEventCreateWithFlags(&s->ctl_ev[i], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&s->ev_f[i], hipEventDisableTiming) == hipSuccess;
+      if (!ok) return cleanup_fail(fail(SMCRT_ERR_HIP, "pinned/event/stream allocation failed"));
+      std::memset(s->h_ctl, 0, 8 * MAX_SLOTS * sizeof(uint32_t));
     }
   }
   int per_cu = 0, cus = 0;
@@ -1213,8 +1221,8 @@ extern "C" {
 
 // Refine the records-per-photon estimate from the last binned launch, if it has landed.
 static void refine_rpp(smcrt_scene* s) {
-  for (int i = 0; i < 2; ++i) {
-    const int sl = s->last_slot < 0 ? i : (s->last_slot + 1 + i) & 1;  // the older slot first
+  for (int i = 0; i < s->n_slots; ++i) {
+    const int sl = s->last_slot < 0 ? i : (s->last_slot + 1 + i) % s->n_slots;  // the oldest slot first
     if (s->ctl_pending[sl] && hipEventQuery(s->ctl_ev[sl]) == hipSuccess) {
       s->ctl_pending[sl] = false;
       const uint32_t* h = s->h_ctl + 8 * sl;
@@ -1235,7 +1243,7 @@ static void refine_rpp(smcrt_scene* s) {
 static hipError_t drain_folds(smcrt_scene* s) {
   if (!s->fstream) return hipSuccess;
   const hipError_t e = hipStreamSynchronize(s->fstream);
-  s->f_pending[0] = s->f_pending[1] = false;
+  for (bool& f : s->f_pending) f = false;
   return e;
 }
 
@@ -1265,33 +1273,48 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   (void)hipDeviceSynchronize();
   (void)drain_folds(s);
   auto release = [&]() {
-    void* old[] = {s->d_pool[0], s->d_pool[1], s->d_sorted, s->d_chunk_fill[0], s->d_chunk_fill[1], s->d_pieces,
-                   s->d_bucket_tile[0], s->d_bucket_tile[1], s->d_order};
+    void* old[] = {s->d_sorted, s->d_pieces, s->d_order};
     for (void* p : old)
       if (p) (void)hipFree(p);
-    s->d_pool[0] = s->d_pool[1] = s->d_sorted = nullptr;
-    s->d_chunk_fill[0] = s->d_chunk_fill[1] = nullptr;
-    s->d_bucket_tile[0] = s->d_bucket_tile[1] = s->d_order = nullptr;
+    for (int i = 0; i < MAX_SLOTS; ++i) {
+      void* per[] = {s->d_pool[i], s->d_chunk_fill[i], s->d_bucket_tile[i]};
+      for (void* p : per)
+        if (p) (void)hipFree(p);
+      s->d_pool[i] = nullptr;
+      s->d_chunk_fill[i] = s->d_bucket_tile[i] = nullptr;
+    }
+    s->d_sorted = nullptr;
+    s->d_order = nullptr;
     s->d_pieces = nullptr;
     s->pool_chunks = 0;
   };
   release();
   const uint64_t cap = chunks * CHUNK_RECORDS;
+  // small pools run MAX_SLOTS deep (SMCRT_SLOTS=2 keeps two), large ones two
+  {
+    const char* ns = std::getenv("SMCRT_SLOTS");
+    const int want = ns && std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS;
+    s->n_slots = cap * 8 <= DEEP_SLOT_BYTES ? want : 2;
+    s->slot = 0;    // (the device is idle here: every slot and stream is free)
+    s->lturn = 0;
+    s->last_slot = -1;
+  }
   // pieces <= records / piece size + one partial piece per tile (deposit.h bin_scan, bk_scan)
   const uint64_t pieces = std::min<uint64_t>(cap / MIN_PIECE_RECORDS, REDUCE_PIECES + 1) + s->n_tiles + 1;
   const uint64_t buckets = cap / BUCKET_RECORDS;
-  bool ok = hipMalloc((void**)&s->d_pool[0], cap * 8) == hipSuccess && hipMalloc((void**)&s->d_pool[1], cap * 8) == hipSuccess &&
-            hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) == hipSuccess;
-  if (ok && s->bucketed)  // bucket fills, bucket tiles (per slot) and the tile-ordered id list
-    ok = hipMalloc((void**)&s->d_chunk_fill[0], buckets * 4) == hipSuccess &&
-         hipMalloc((void**)&s->d_chunk_fill[1], buckets * 4) == hipSuccess &&
-         hipMalloc((void**)&s->d_bucket_tile[0], buckets * 4) == hipSuccess &&
-         hipMalloc((void**)&s->d_bucket_tile[1], buckets * 4) == hipSuccess &&
-         hipMalloc((void**)&s->d_order, buckets * 4) == hipSuccess;
-  else if (ok)  // chunk fills (per slot) and the tile-sorted copy of the records
-    ok = hipMalloc((void**)&s->d_sorted, cap * 8) == hipSuccess &&
-         hipMalloc((void**)&s->d_chunk_fill[0], chunks * 4) == hipSuccess &&
-         hipMalloc((void**)&s->d_chunk_fill[1], chunks * 4) == hipSuccess;
+  bool ok = hipMalloc((void**)&s->d_pieces, pieces * sizeof(Piece)) == hipSuccess;
+  for (int i = 0; ok && i < s->n_slots; ++i) {
+    ok = hipMalloc((void**)&s->d_pool[i], cap * 8) == hipSuccess;
+    if (ok && s->bucketed)  // bucket fills and bucket tiles, per slot
+      ok = hipMalloc((void**)&s->d_chunk_fill[i], buckets * 4) == hipSuccess &&
+           hipMalloc((void**)&s->d_bucket_tile[i], buckets * 4) == hipSuccess;
+    else if (ok)  // chunk fills, per slot
+      ok = hipMalloc((void**)&s->d_chunk_fill[i], chunks * 4) == hipSuccess;
+  }
+  if (ok && s->bucketed)  // the tile-ordered bucket id list (folds are serial)
+    ok = hipMalloc((void**)&s->d_order, buckets * 4) == hipSuccess;
+  else if (ok)  // the tile-sorted copy of the records
+    ok = hipMalloc((void**)&s->d_sorted, cap * 8) == hipSuccess;
   if (!ok) {
     (void)hipGetLastError();
     release();
@@ -1312,9 +1335,9 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   Ch.queue = s->d_queue + qi;  // (a queue head per stream: overlapped launches run concurrently)
   HIPCHK(hipMemsetAsync(Ch.queue, 0, sizeof(unsigned long long), stream));
   // this launch's cold parameters: a ring slot, written in stream order before the kernel.
-  // (Overlapped launches alternate streams and COLD_SLOTS is even, so a slot is always
-  // rewritten on the stream that last read it.)
-  KCold* C = s->d_cold + (s->cold_seq++ % COLD_SLOTS);
+  // (Each stream has its own ring of slots, so a slot is only ever rewritten in stream order
+  // after the launch that read it.)
+  KCold* C = s->d_cold + (size_t)qi * COLD_PER_STREAM + (s->cold_seq[qi]++ % COLD_PER_STREAM);
   HIPCHK(hipMemcpyAsync(C, &Ch, sizeof(KCold), hipMemcpyHostToDevice, stream));
   if (binned) {
     HIPCHK(hipMemsetAsync(s->d_dep_ctl[sl], 0, 4 * sizeof(uint32_t), stream));
@@ -1521,9 +1544,9 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   const bool overlap = (cfg->flags & SMCRT_FLAG_OVERLAP) != 0;
   if (overlap) {  // the internal streams start after the caller's earlier work
     HIPCHK(hipEventRecord(s->ev_in, stream));
-    for (int i = 0; i < 2; ++i) HIPCHK(hipStreamWaitEvent(s->lstream[i], s->ev_in, 0));
+    for (int i = 0; i < MAX_SLOTS; ++i) HIPCHK(hipStreamWaitEvent(s->lstream[i], s->ev_in, 0));
   } else {  // a plain launch runs after every overlapped one (same tallies, same buffers)
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MAX_SLOTS; ++i)
       if (s->lpending[i]) HIPCHK(hipStreamWaitEvent(stream, s->lev[i], 0));
   }
   for (uint64_t done = 0; done < cfg->n_photons;) {
@@ -1568,15 +1591,15 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
     int st;
     if (overlap) {
       const int q = s->lturn;
-      s->lturn ^= 1;
+      s->lturn = (s->lturn + 1) % s->n_slots;
       st = launch_one(s, K, Ch, xsrc, s->lstream[q], sl, q);
       if (!st && hipEventRecord(s->lev[q], s->lstream[q]) != hipSuccess) st = fail(SMCRT_ERR_HIP, "event record failed");
       s->lpending[q] = true;
     } else {
-      st = launch_one(s, K, Ch, xsrc, stream, sl, 2);
+      st = launch_one(s, K, Ch, xsrc, stream, sl, MAX_SLOTS);
     }
     if (st) return st;
-    if (K.rec_pool) s->slot ^= 1;
+    if (K.rec_pool) s->slot = (s->slot + 1) % s->n_slots;
     if (calibrate && K.rec_pool) {
       HIPCHK(hipEventSynchronize(s->ctl_ev[sl]));
       refine_rpp(s);
@@ -1777,7 +1800,7 @@ int smcrt_scene_fence(smcrt_scene* s, void* stream) {
   if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
   std::lock_guard<std::mutex> g(s->mu);
   HIPCHK(hipSetDevice(s->device));
-  for (int i = 0; i < 2; ++i)  // overlapped launches (their folds are ordered after them)
+  for (int i = 0; i < MAX_SLOTS; ++i)  // overlapped launches (their folds are ordered after them)
     if (s->lpending[i]) HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->lev[i], 0));
   if (s->last_slot >= 0 && s->f_pending[s->last_slot])  // folds are serial: the last covers all
     HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->ev_f[s->last_slot], 0));
