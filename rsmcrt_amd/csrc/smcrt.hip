@@ -65,6 +65,10 @@ __device__ unsigned long long g_diag_t[9];
 #define SMCRT_COOP_CULL_LANES 8
 #endif
 constexpr uint32_t COOP_CULL_LANES = SMCRT_COOP_CULL_LANES;
+// the solo march of a wave's last photon (COOP instantiations; -DSMCRT_SOLO=0 turns it off)
+#ifndef SMCRT_SOLO
+#define SMCRT_SOLO 1
+#endif
 
 template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
 #ifndef SMCRT_WAVES_PER_EU
@@ -219,6 +223,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     }
 #endif
     DIAG_T(1);
+#if SMCRT_SOLO
+    // ---- solo march: a wave left with ONE photon that is not waiting for an event -------
+    // In a launch's tail a lone photon pays the whole trip (every phase's checks, one EVAL
+    // and at most SMCRT_DDA_PER_ITER crossings) per march step. When that photon stands at
+    // the march loop's EVAL (ST_M1, inttau2.f90:177-191), the wave instead runs the march
+    // cycle M1 -> M0 -> segment for it in a tight loop: the cooperative EVAL with every lane,
+    // the program points of P3 (ST_M1) and P4 (ST_M0) in the owner lane, and the whole
+    // segment's crossings at once. The photon's own sequence of operations is exactly the
+    // main loop's, so its trajectory, counters and records are unchanged. The loop ends as
+    // soon as the photon leaves the cycle (boundary probe ST_B0, a fault, a new event).
+    if constexpr (COOP) {
+      const bool ev_wait = (L.st == ST_INTERACT || L.st == ST_T2 || L.st == ST_EMIT || L.st == ST_DONE);
+      const uint64_t act = __ballot(L.st != ST_IDLE && !ev_wait);
+      if (__popcll(act) == 1) {
+        const int ow = __builtin_ctzll(act);
+        bool run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
+        while (run) {
+          const V3 q = v3(readlane_f64(L.pos.x, ow), readlane_f64(L.pos.y, ow), readlane_f64(L.pos.z, ow));
+          EvalOut S;
+          if (K.ctab) S = eval_coop_tab(ctab, K.n_top, q, false, 0, 0);
+          else if (K.cull) S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0);
+          else S = eval_sdfs(nodes, prog, K.n_prog, q, false, 0, 0);
+          w_sdf += (uint32_t)K.n_top;  // ST_M1's ds array is counted (packet%cnts)
+          if (lane_id == ow) {
+            L.pend = false;  // P3, ST_M1: :177-191
+            L.minabs = S.minabs;
+            L.d = S.minabs;
+            if (S.minv > 0.0) { L.tflag = true; L.st = ST_B0; }
+            else L.st = ST_M0;
+            if (L.st == ST_M0) {  // P4, ST_M0: :155-176
+              if (!(L.d >= eps)) {
+                L.st = ST_B0;
+              } else if (++L.loopc > (uint32_t)MAX_MARCH_ITERS) {
+                L.fault = true; L.tflag = true; L.st = ST_B0;
+              } else {
+                const double kap = props[L.layer - 1].kappa;
+                const double t = L.d * kap;
+                const V3 oldpos = L.pos;
+                if (L.taurun + t < L.tau) {
+                  L.taurun = L.taurun + t;
+                  L.pos = L.pos + smul(L.d, L.dir);
+                  L.st = ST_M1; L.pend = true;
+                } else {
+                  L.d = (L.tau - L.taurun) / kap;
+                  L.taurun = L.tau;
+                  L.pos = L.pos + smul(L.d, L.dir);
+                  L.st = ST_B0;
+                }
+                start_segment<GM>(K, L, sh, oldpos, L.d);
+              }
+            }
+          }
+          // the segment's crossings (the owner's; wave-uniform so records stay wave-compacted)
+          while (__builtin_amdgcn_readlane((int)L.seg, ow)) {
+            bool dep = false;
+            uint32_t vox = 0;
+            double val = 0.0;
+            if (lane_id == ow) dda_step<GM>(K, L, xf, yf, zf, dep, vox, val);
+            w_dep += __popcll(__ballot(dep));
+            if (binned) {
+              if (K.bucket_tiles) emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+              else emit_deposits(K, C, W, dep, vox, val, overflow, whist);
+            } else if (dep) {
+              double* const jm = C->jmean;
+              if (jm) atomic_add_nr(jm + vox, val);
+            }
+          }
+          run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
+        }
+      }
+    }
+#endif
     // ---- EVAL phase: the SDF array at the lane's query point ----------------------------
     const bool have = !L.seg && L.pend;
     EvalOut R;
