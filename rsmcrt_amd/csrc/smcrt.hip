@@ -69,6 +69,10 @@ constexpr uint32_t COOP_CULL_LANES = SMCRT_COOP_CULL_LANES;
 #ifndef SMCRT_SOLO
 #define SMCRT_SOLO 1
 #endif
+#ifndef SMCRT_SOLO_LANES
+#define SMCRT_SOLO_LANES 4
+#endif
+constexpr int SOLO_LANES = SMCRT_SOLO_LANES;
 
 template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
 #ifndef SMCRT_WAVES_PER_EU
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 #endif
     DIAG_T(1);
 #if SMCRT_SOLO
-    // ---- solo march: a wave left with ONE photon that is not waiting for an event -------
+    // ---- solo march: a wave left with at most SOLO_LANES photons not waiting for an event -
     // In a launch's tail a lone photon pays the whole trip (every phase's checks, one EVAL
     // and at most SMCRT_DDA_PER_ITER crossings) per march step. When that photon stands at
     // the march loop's EVAL (ST_M1, inttau2.f90:177-191), the wave instead runs the march
@@ -236,9 +240,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     if constexpr (COOP) {
       const bool ev_wait = (L.st == ST_INTERACT || L.st == ST_T2 || L.st == ST_EMIT || L.st == ST_DONE);
       const uint64_t act = __ballot(L.st != ST_IDLE && !ev_wait);
-      if (__popcll(act) == 1) {
-        const int ow = __builtin_ctzll(act);
-        bool run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
+      const uint64_t cand = __ballot(L.st == ST_M1 && L.pend && !L.seg);
+      if (cand && __popcll(act) <= SOLO_LANES) {  // (a few photons: one after the other)
+        const int ow = __builtin_ctzll(cand);
+        bool run = true;
         while (run) {
           const V3 q = v3(readlane_f64(L.pos.x, ow), readlane_f64(L.pos.y, ow), readlane_f64(L.pos.z, ow));
           EvalOut S;
