@@ -36,6 +36,7 @@ def find(d, stem, kind):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--source", default="", help="the committed profiles/ directory these numbers are copied to")
     ap.add_argument("dir")
     ap.add_argument("--last", type=int, default=3)
     ap.add_argument("--json")
@@ -102,7 +103,7 @@ def main():
                            "valu_insts_per_launch": out[k].get("SQ_INSTS_VALU"),
                            "salu_insts_per_launch": out[k].get("SQ_INSTS_SALU"),
                            "valu_classes": classes,
-                           "avg_ms": out[k]["avg_ms_last"], "source": os.path.relpath(a.dir)}, f, indent=1)
+                           "avg_ms": out[k]["avg_ms_last"], "source": a.source or os.path.relpath(a.dir)}, f, indent=1)
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1, sort_keys=True)

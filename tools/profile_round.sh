@@ -7,7 +7,7 @@ TAG=${TAG:-r02}
 PASSES="trace sq fetch write valu" PROF_ARGS="${PROF_ARGS:---no-cpu --no-ref --steps 3 --warmup 2}" bash tools/profile.sh || exit $?
 mkdir -p gpurun_out/$TAG
 python3 tools/prof_summary.py gpurun_out/prof --last 3 --batch ${BATCH:-16000000} --grid ${GRID:-128} \
-  --workload ${WORKLOAD:-m1} --json gpurun_out/$TAG/summary.json --traffic gpurun_out/$TAG/transport_traffic.json \
+  --workload ${WORKLOAD:-m1} --source profiles/$TAG --json gpurun_out/$TAG/summary.json --traffic gpurun_out/$TAG/transport_traffic.json \
   > gpurun_out/$TAG/summary.txt
 cat gpurun_out/$TAG/summary.txt
 for p in trace pmc_sq pmc_fetch pmc_write pmc_valu; do
