@@ -53,7 +53,7 @@ def workload(name, grid_n):
         return (builders.setup_sphere_scene(builders.random_sphere_list(40)), scene.grid(n, n, n, 1.0, 1.0, 1.0),
                 scene.uniform_source((-1.0, -1.0, 0.9999999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0)),
                 [], f"M2 sphere_scene (res/sphere.toml): 40 random spheres n=1.37, uniform source z=0.9999999, "
-                f"{n}^3 grid (setupGeometry.f90:250-294)", 800_000)
+                f"{n}^3 grid (setupGeometry.f90:250-294)", 12_800_000)
     if name == "m3":
         n = grid_n or 128
         return (builders.setup_tran_and_jacques(), scene.grid(n, n, n, 1.0, 1.0, 1.0),
@@ -65,7 +65,7 @@ def workload(name, grid_n):
         return (builders.synthetic_vessels(512), scene.grid(n, n, n, 0.16, 0.09, 0.13),
                 scene.uniform_source((-0.16, -0.09, 0.1299), (0.32, 0.0, 0.0), (0.0, 0.18, 0.0), (0.0, 0.0, -1.0)),
                 [], f"M4 (build-defined) synthetic vessel net: 512 capsules + dermis box, uniform source, {n}^3 grid",
-                4_000_000)
+                8_000_000)
     if name == "m5":
         n = grid_n or 128
         dets = [scene.circle_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.05, 50),
