@@ -81,6 +81,24 @@ def test_sphere_scene():
     compare(gpu, cpu)
 
 
+@pytest.mark.parametrize("variant", ["table", "culled", "global"])
+def test_tail_machinery_wall_photons(variant, monkeypatch):
+    """Photons launched next to a wall of the bounding box and moving parallel to it march in
+    thousands of tiny steps (M2's tail), so most of their steps run in sparse
+    waves: the solo march and the cooperative EVAL from the LDS table ("table"), the
+    cooperative culled EVAL ("culled": SMCRT_COOP_TAB=0) or the global cooperative EVAL
+    ("global": table and culling off). Every variant must equal the oracle bit for bit."""
+    if variant != "table":
+        monkeypatch.setenv("SMCRT_COOP_TAB", "0")
+    if variant == "global":
+        monkeypatch.setenv("SMCRT_CULL", "0")
+    sc = builders.setup_sphere_scene(builders.random_sphere_list(40))
+    src = scene.uniform_source((-1.0, -1.0, 0.9999999), (1e-3, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, scene.grid(32, 32, 32, 1, 1, 1), src, 300)
+    compare(gpu, cpu)
+    assert cpu.counter("sdf_evals") > 300 * 41 * 500  # (long marches: the tail machinery ran)
+
+
 def test_detectors_validation1():
     sc = builders.setup_box(90.0, 10.0, 0.75, 1.0, (100.0, 100.0, 0.02), (100.0, 100.0, 0.03))
     g = scene.grid(50, 50, 50, 50.0, 50.0, 0.015)
@@ -439,15 +457,17 @@ def test_general_emitter_with_detectors():
     assert cpu.counter("detector_hits") > 0
 
 
-@pytest.mark.parametrize("overlap", [False, True], ids=["async-fold", "overlap"])
-def test_async_fold_pipeline(overlap):
+@pytest.mark.parametrize("overlap,slots", [(False, 4), (True, 4), (True, 2)], ids=["async-fold", "overlap", "overlap-2"])
+def test_async_fold_pipeline(overlap, slots, monkeypatch):
     """FLAG_ASYNC_FOLD launches on a caller stream (the bench's mode: the fold of launch k runs
-    beside launch k+1's transport kernel in the other record slot) + a fence give the same
+    beside later launches' transport kernels in other record slots) + a fence give the same
     tallies as one synchronous run of the same photons. With FLAG_OVERLAP the launches also
-    alternate between the scene's two internal streams (launch k+1 starts while launch k's
-    slowest photons finish), a plain run afterwards is ordered behind them, and the tallies
-    are the same."""
+    rotate over the scene's internal streams (four here: small record slots; two with
+    SMCRT_SLOTS=2), so launch k+1.. start while launch k's slowest photons finish; a plain run
+    afterwards is ordered behind them, and the tallies are the same."""
     import torch
+    if slots == 2:
+        monkeypatch.setenv("SMCRT_SLOTS", "2")
     sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
     g = scene.grid(64, 64, 64, 1, 1, 1)
     src = scene.point_source()
