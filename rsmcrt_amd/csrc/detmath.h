@@ -72,6 +72,26 @@ struct Rng {
 __device__ __forceinline__ uint64_t d2u(double x) { return (uint64_t)__double_as_longlong(x); }
 __device__ __forceinline__ double u2d(uint64_t u) { return __longlong_as_double((long long)u); }
 
+// IEEE fp64 division split in two. For `n / d` the compiler emits (gfx950):
+//   D = v_div_scale(d); r = v_rcp(D); twice { e = fma(-D, r, 1); r = fma(r, e, r) };
+//   q = N*r; res = fma(-D, q, N); v_div_fmas(res, r, q); v_div_fixup(.., d, n)
+// with N = v_div_scale(n). While 2^-500 <= |n|, |d| <= 4 neither operand is scaled, vcc
+// stays 0 (v_div_fmas is a plain fma) and v_div_fixup passes the quotient through, so the
+// two halves below give the correctly rounded n / d bit for bit. The first half depends
+// on d only and can be shared by every division by the same d.
+__device__ __forceinline__ double ieee_rcp_f64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double ieee_div_tail_f64(double n, double d, double r) {
+  const double q = n * r;
+  const double res = __builtin_fma(-d, q, n);
+  return __builtin_fma(res, r, q);
+}
+
 // natural log: fdlibm e_log.c algorithm (identical operation sequence to the oracle)
 #ifdef SMCRT_ABL_FAST_MATH  // timing ablation only: fp32 hardware log/sin/cos, not bit-exact
 __device__ __forceinline__ double det_log(double x) { return (double)__logf((float)x); }

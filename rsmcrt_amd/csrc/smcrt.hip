@@ -516,6 +516,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     if (__ballot(L.seg)) {  // wave-uniform, so deposit records can be wave-compacted
 #pragma unroll
       for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {
+#if SMCRT_DDA_MIN_ITERS < SMCRT_DDA_PER_ITER
+        // past the first crossings, walk on only while enough lanes still have a segment
+        if (k >= SMCRT_DDA_MIN_ITERS && __popcll(__ballot(L.seg)) < SMCRT_DDA_MIN_LANES) break;
+#endif
         bool dep = false;
         uint32_t vox = 0;
         double val = 0.0;

@@ -40,6 +40,14 @@ constexpr int64_t MAX_INTERACTIONS = 100000000;
 #ifndef SMCRT_DDA_PER_ITER
 #define SMCRT_DDA_PER_ITER 3
 #endif
+// Crossings past the first SMCRT_DDA_MIN_ITERS of a trip run only while at least
+// SMCRT_DDA_MIN_LANES lanes of the wave still have a segment.
+#ifndef SMCRT_DDA_MIN_ITERS
+#define SMCRT_DDA_MIN_ITERS SMCRT_DDA_PER_ITER
+#endif
+#ifndef SMCRT_DDA_MIN_LANES
+#define SMCRT_DDA_MIN_LANES 1
+#endif
 // A wave runs the photon-event phase once this many lanes wait for it (or no lane has
 // anything else to do).
 #ifndef SMCRT_FETCH_CHUNK
@@ -745,9 +753,9 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   const V3 dir = L.dir;
   const bool capped = ++L.dda_it > (uint32_t)MAX_DDA_ITERS;  // runaway guard: fault
   // wall_dist, :467-521: d_a = (face_a - old_a)/dir_a, dcell = min, ldir_a = (dcell == d_a).
-  // Only the smallest quotient is needed exactly: the three are ranked with hardware
-  // reciprocals (relative error far below the 2^-16 margin required), and the one winner
-  // is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
+  // Only the smallest quotient is needed exactly: the three are ranked by products with
+  // the refined reciprocals (relative error far below the 2^-16 margin required), and the
+  // one winner is divided exactly. If the ranking is not clear-cut by that margin (near-ties, zero
   // or negative distances, a zero direction component, NaN), all three are divided exactly
   // as the reference does. Both paths give the reference's dcell and ldir bit for bit.
   // the wall each axis moves towards: xface(ci+1) going +, xface(ci) going - (0-based here)
@@ -757,22 +765,30 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   const double nx = fx - L.old.x;
   const double ny = fy - L.old.y;
   const double nz = fz - L.old.z;
-  const double ax = nx * __builtin_amdgcn_rcp(dir.x);
-  const double ay = ny * __builtin_amdgcn_rcp(dir.y);
-  const double az = nz * __builtin_amdgcn_rcp(dir.z);
+  // The reciprocal half of the IEEE fp64 division sequence (v_rcp_f64 + two Newton steps, as
+  // the compiler expands `n / d`) depends on the direction only, so it is computed once per
+  // trip (the compiler hoists it out of the unrolled crossings); per crossing only the
+  // numerator half (mul, residual fma, correction fma) remains.
+  const double rx = ieee_rcp_f64(dir.x), ry = ieee_rcp_f64(dir.y), rz = ieee_rcp_f64(dir.z);
+  const double ax = nx * rx;
+  const double ay = ny * ry;
+  const double az = nz * rz;
   // Clear-cut: exactly two estimates lie above the margin over the smallest. (A NaN is
   // above nothing, so it can never leave two above: such lanes take the exact path.)
   const double amin = fmin(fmin(ax, ay), az);
   const double thr = amin * (1.0 + 0x1.0p-16);
   const bool ux = ax > thr, uy = ay > thr, uz = az > thr;
   const bool two = ((ux ^ uy) ^ uz) == false && (ux || uy || uz);
-  const bool fast = two && amin > 0.0 && dir.x != 0.0 && dir.y != 0.0 && dir.z != 0.0;
+  // (the magnitude bounds keep the operands where the division sequence does no scaling)
+  const bool fast0 = two && amin > 0.0 && fabs(dir.x) >= 0x1.0p-500 && fabs(dir.y) >= 0x1.0p-500 &&
+                     fabs(dir.z) >= 0x1.0p-500;
+  bool lx = !ux, ly = !uy, lz = !uz;
+  const double num = lx ? nx : (ly ? ny : nz), den = lx ? dir.x : (ly ? dir.y : dir.z);
+  const double rcp = lx ? rx : (ly ? ry : rz);
+  const bool fast = fast0 && fabs(num) >= 0x1.0p-500;
   double dcell;
-  bool lx, ly, lz;
   if (fast) {
-    lx = !ux; ly = !uy; lz = !uz;
-    const double num = lx ? nx : (ly ? ny : nz), den = lx ? dir.x : (ly ? dir.y : dir.z);
-    dcell = num / den;
+    dcell = ieee_div_tail_f64(num, den, rcp);  // == num / den bit for bit
   } else {
     double dx = -999.0, dy = -999.0, dz = -999.0;
     if (dir.x > 0.0 || dir.x < 0.0) dx = nx / dir.x;
