@@ -544,7 +544,14 @@ __global__ __launch_bounds__(BIN_THREADS) void bk_place(const uint32_t* __restri
 
 // ---- bk_reduce: one piece (buckets of one tile) per block, fp64 LDS sums into jmean --------
 // (blockDim.x must be 1024)
-constexpr uint32_t REDUCE_STAGE_BUCKETS = 256;
+#ifndef SMCRT_RED_STAGE
+#define SMCRT_RED_STAGE 512
+#endif
+#ifndef SMCRT_RED_UNROLL
+#define SMCRT_RED_UNROLL 16
+#endif
+constexpr uint32_t REDUCE_STAGE_BUCKETS = SMCRT_RED_STAGE;  // <= 1024 (one id per thread)
+constexpr int RED_UNROLL = SMCRT_RED_UNROLL;                // record loads in flight per thread
 __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __restrict__ pool,
                                                   const uint32_t* __restrict__ order,
                                                   const uint32_t* __restrict__ bucket_fill,
@@ -552,39 +559,46 @@ __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __re
                                                   const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
                                                   double* __restrict__ jmean) {
   __shared__ double acc[TILE_VOXELS];
-  __shared__ uint32_t ids[REDUCE_STAGE_BUCKETS], fills[REDUCE_STAGE_BUCKETS];
+  // bucket ids and fills of a stage, double-buffered: the next stage's ids are loaded while
+  // this stage's records are summed, and one barrier per stage suffices
+  __shared__ uint32_t ids[2][REDUCE_STAGE_BUCKETS], fills[2][REDUCE_STAGE_BUCKETS];
   const uint32_t n_pieces = dep_ctl[2];
   for (uint32_t pi = blockIdx.x; pi < n_pieces; pi += gridDim.x) {
     const Piece p = pieces[pi];
     for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) acc[i] = 0.0;
-    for (uint32_t k0 = 0; k0 < p.count; k0 += REDUCE_STAGE_BUCKETS) {
+    uint32_t nid = 0;
+    if (threadIdx.x < REDUCE_STAGE_BUCKETS && threadIdx.x < p.count) nid = order[p.start + threadIdx.x];
+    uint32_t buf = 0;
+    for (uint32_t k0 = 0; k0 < p.count; k0 += REDUCE_STAGE_BUCKETS, buf ^= 1u) {
       const uint32_t kn = p.count - k0 < REDUCE_STAGE_BUCKETS ? p.count - k0 : REDUCE_STAGE_BUCKETS;
-      __syncthreads();
       if (threadIdx.x < kn) {
-        const uint32_t b = order[p.start + k0 + threadIdx.x];
-        ids[threadIdx.x] = b;
-        fills[threadIdx.x] = bucket_fill[b];
+        ids[buf][threadIdx.x] = nid;
+        fills[buf][threadIdx.x] = bucket_fill[nid];
       }
-      __syncthreads();
+      __syncthreads();  // (also orders the previous use of this buffer, two stages ago)
+      const uint32_t k1 = k0 + REDUCE_STAGE_BUCKETS;
+      if (threadIdx.x < REDUCE_STAGE_BUCKETS && k1 + threadIdx.x < p.count) nid = order[p.start + k1 + threadIdx.x];
+      const uint32_t* const sid = ids[buf];
+      const uint32_t* const sfill = fills[buf];
       const uint32_t slots = kn << BUCKET_SHIFT;
       uint32_t s = threadIdx.x;
-      for (; s + 7 * 1024 < slots; s += 8 * 1024) {  // 8 loads in flight per thread
-        unsigned long long x[8];
-        bool v[8];
+      for (; s + (RED_UNROLL - 1) * 1024 < slots; s += RED_UNROLL * 1024) {
+        unsigned long long x[RED_UNROLL];
+        bool v[RED_UNROLL];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < RED_UNROLL; ++k) {
           const uint32_t j = s + k * 1024, kb = j >> BUCKET_SHIFT, r = j & (BUCKET_RECORDS - 1);
-          v[k] = r < fills[kb];
-          x[k] = v[k] ? pool[((uint64_t)ids[kb] << BUCKET_SHIFT) + r] : 0ull;
+          v[k] = r < sfill[kb];
+          x[k] = v[k] ? pool[((uint64_t)sid[kb] << BUCKET_SHIFT) + r] : 0ull;
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
+        for (int k = 0; k < RED_UNROLL; ++k)
           if (v[k]) atomicAdd(&acc[(uint32_t)(x[k] >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x[k]));
       }
       for (; s < slots; s += 1024) {
         const uint32_t kb = s >> BUCKET_SHIFT, r = s & (BUCKET_RECORDS - 1);
-        if (r < fills[kb]) {
-          const unsigned long long x = pool[((uint64_t)ids[kb] << BUCKET_SHIFT) + r];
+        if (r < sfill[kb]) {
+          const unsigned long long x = pool[((uint64_t)sid[kb] << BUCKET_SHIFT) + r];
           atomicAdd(&acc[(uint32_t)(x >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x));
         }
       }
