@@ -353,46 +353,61 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 // deposit: the record's write and its read; the sorted path above moves 40 B).
 //
 // A bucket is BUCKET_RECORDS consecutive pool slots that hold records of one tile only.
-// Every wave keeps, in LDS, one open bucket per tile (id + fill) and takes bucket ids from a
-// wave-private batch of BUCKET_BATCH ids (one returning atomic per batch). A deposit is an
-// LDS add-and-return on its tile's fill plus one 8-B store; only the deposit that fills a
-// bucket takes the rare slow path (claim the next id, record the full bucket).
+// The four waves of a block share, in LDS, one 64-bit word per tile:
+//   cur (24 bits) | next (24 bits) | fill (16 bits)
+// `cur` is the tile's open bucket, `next` the bucket that follows it (taken in advance), and
+// fill the records claimed in `cur`. A deposit is one LDS add-and-return of 1 on that word,
+// which hands it its slot: fill < BUCKET_RECORDS -> cur[fill]; fill in [BUCKET_RECORDS,
+// 2*BUCKET_RECORDS) -> next[fill - BUCKET_RECORDS], so no deposit ever waits for another;
+// beyond that (a claim still pending) -> an exact fp64 atomic. The deposit that found fill at
+// exactly BUCKET_RECORDS takes the slow path: it makes `next` the open bucket, takes a fresh
+// `next` from its wave's batch of ids (BUCKET_BATCH per returning atomic) and rebases fill
+// with one compare-and-swap. Sharing the words per block (round 2: per wave before) keeps 4x
+// fewer buckets open, so their partly written cache lines fit in L2 and leave it whole.
 // The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
 constexpr uint32_t BUCKET_BATCH = 64;                    // ids a wave takes at a time
-constexpr uint32_t BUCKET_NONE = 0xFFFFFFFFu;            // no bucket open for the tile yet
-constexpr uint32_t BUCKET_EXHAUSTED = 0xFFFFFFFEu;       // pool full: the tile's deposits use atomics
+constexpr uint32_t BUCKET_ID_NONE = 0xFFFFFFu;           // no bucket (24-bit id field)
+constexpr uint32_t BUCKET_ID_EXHAUSTED = 0xFFFFFEu;      // pool full: the tile's deposits use atomics
 constexpr uint32_t TILE_INVALID = 0xFFFFFFFFu;           // bucket_tile of an id never used
-constexpr uint32_t FILL_EXHAUSTED = 0x40000000u;         // fill of an exhausted tile: always "over"
-constexpr uint32_t MAX_DIRECT_TILES = 512;               // 8 B of LDS per tile per wave
+constexpr uint32_t MAX_DIRECT_TILES = 512;               // 8 B of LDS per tile per block
 constexpr uint32_t MIN_PIECE_BUCKETS = MIN_PIECE_RECORDS / BUCKET_RECORDS;
+// (pool ids stay below 2^24 - 2^20: MAX_POOL_RECORDS <= 2^32 - 2^28 records)
 
 // Wave-uniform batch of bucket ids [next, end) (scalar registers).
 struct BucketLog {
   uint32_t next, end;
 };
 
-// Per-wave LDS state, one 64-bit word per tile: (id << 32) | fill, where fill = records in
-// the tile's open bucket (BUCKET_RECORDS: none open) and id = that bucket. One LDS
-// add-and-return of 1 hands a deposit both its slot and its bucket. Call in wave-uniform
-// control flow.
-__device__ __forceinline__ unsigned long long bucket_word(uint32_t id, uint32_t fill) {
-  return ((unsigned long long)id << 32) | fill;
+__device__ __forceinline__ unsigned long long bucket_word(uint32_t cur, uint32_t next, uint32_t fill) {
+  return ((unsigned long long)cur << 40) | ((unsigned long long)next << 16) | fill;
 }
-__device__ __forceinline__ void init_buckets(unsigned long long* bs, uint32_t n_tiles) {
-  const int lane = threadIdx.x & 63;
-  for (uint32_t t = lane; t < n_tiles; t += 64) bs[t] = bucket_word(BUCKET_NONE, BUCKET_RECORDS);
+__device__ __forceinline__ uint32_t bw_cur(unsigned long long w) { return (uint32_t)(w >> 40); }
+__device__ __forceinline__ uint32_t bw_next(unsigned long long w) { return (uint32_t)(w >> 16) & 0xFFFFFFu; }
+__device__ __forceinline__ uint32_t bw_fill(unsigned long long w) { return (uint32_t)w & 0xFFFFu; }
+
+// Block start (every thread calls it; the caller's barrier publishes the words): one id per
+// tile taken as the tiles' first `next`; fill = BUCKET_RECORDS makes the first deposit of a
+// tile open it.
+__device__ __forceinline__ void init_buckets(const KParams& K, const KCold* __restrict__ C, unsigned long long* bs) {
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(C->dep_ctl, K.bucket_tiles);
+  base = uniform(__shfl(base, 0, 64));
+  for (uint32_t t = lane; t < K.bucket_tiles; t += 64) {
+    const uint32_t id = base + t;
+    bs[t] = bucket_word(BUCKET_ID_NONE, id < K.n_buckets ? id : BUCKET_ID_EXHAUSTED, BUCKET_RECORDS);
+  }
 }
 
+// The rare part of a deposit instruction (wave-uniform call): the claims of the lanes that
+// found fill == BUCKET_RECORDS, and the exact atomic for lanes that found no slot.
 __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __restrict__ C, BucketLog& W,
-                                                      bool over, uint32_t pos, uint32_t oldid, uint32_t t,
-                                                      unsigned long long rec, uint32_t vox, double val,
-                                                      uint32_t& overflow, unsigned long long* bs) {
+                                            bool claim, bool spill, unsigned long long w, uint32_t t,
+                                            uint32_t vox, double val, uint32_t& overflow, unsigned long long* bs) {
   const int lane = threadIdx.x & 63;
-  // The deposit that found its tile's fill at exactly BUCKET_RECORDS claims the next bucket;
-  // the others of this instruction that overflowed the same tile follow it into the new one.
-  const bool claim = over && pos == BUCKET_RECORDS;
   const uint64_t cm = __ballot(claim);
   const uint32_t nc = (uint32_t)__popcll(cm);
   uint32_t next = uniform(W.next), end = uniform(W.end);
@@ -407,33 +422,30 @@ __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __res
   }
   if (claim) {
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-    const uint32_t nb = next + rank;
-    if (oldid < K.n_buckets) C->bucket_fill[oldid] = BUCKET_RECORDS;  // the full bucket
-    if (nb < K.n_buckets) {
-      C->bucket_tile[nb] = t;
+    const uint32_t fresh = next + rank < K.n_buckets ? next + rank : BUCKET_ID_EXHAUSTED;
+    const uint32_t cur = bw_cur(w), nx = bw_next(w);
+    if (cur < K.n_buckets) C->bucket_fill[cur] = BUCKET_RECORDS;  // the full bucket
+    if (nx < K.n_buckets) {  // `next` becomes the tile's open bucket
+      C->bucket_tile[nx] = t;
       atomicAdd(C->tile_nb + t, 1u);
-      // id: oldid -> nb, fill: -BUCKET_RECORDS (-> the number that overflowed into it); the
-      // fill is >= BUCKET_RECORDS here, so the low word never borrows from the id
-      const unsigned long long delta = ((unsigned long long)(nb - oldid) << 32) - BUCKET_RECORDS;
-      __hip_atomic_fetch_add(bs + t, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    } else {
-      __hip_atomic_store(bs + t, bucket_word(BUCKET_EXHAUSTED, FILL_EXHAUSTED), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    // cur <- next, next <- fresh, fill -= BUCKET_RECORDS; deposits that came after the next
+    // bucket filled up (fill >= 2*BUCKET_RECORDS) took the atomic path, so fill is capped
+    // first and the deposit that finds BUCKET_RECORDS again opens `fresh`. Only this lane
+    // changes cur/next while its claim is pending, so they are still (cur, nx) here.
+    unsigned long long old = __hip_atomic_load(bs + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+      const uint32_t f = bw_fill(old);
+      const uint32_t f2 = (f < 2 * BUCKET_RECORDS ? f : 2 * BUCKET_RECORDS) - BUCKET_RECORDS;
+      const unsigned long long nw = bucket_word(nx, fresh, f2);
+      if (__hip_atomic_compare_exchange_strong(bs + t, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP))
+        break;
     }
   }
   W.next = next + nc;
   W.end = end;
-  __builtin_amdgcn_wave_barrier();
-  bool spill = false;
-  if (over) {
-    const uint32_t b = (uint32_t)(__hip_atomic_load(bs + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> 32);
-    if (b < K.n_buckets && pos - BUCKET_RECORDS < BUCKET_RECORDS) {
-      K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos - BUCKET_RECORDS)] = rec;
-    } else {  // pool exhausted: stay correct with fp64 atomics
-      atomic_add_nr(C->jmean + vox, val);
-      spill = true;
-    }
-  }
+  if (spill) atomic_add_nr(C->jmean + vox, val);  // exact fp64 fallback
   overflow += (uint32_t)__popcll(__ballot(spill));
 }
 
@@ -442,30 +454,39 @@ __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __r
                                               unsigned long long* bs) {
   if (!__ballot(dep)) return;
   const uint32_t t = vox >> TILE_SHIFT;
-  const unsigned long long rec = pack_record(vox, val);
   unsigned long long w = 0;
-  if (dep) w = __hip_atomic_fetch_add(bs + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-  const uint32_t pos = (uint32_t)w, b = (uint32_t)(w >> 32);
-  const bool over = dep && pos >= BUCKET_RECORDS;
-  if (dep && !over) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + pos] = rec;
-  if (__ballot(over)) bucket_slow(K, C, W, over, pos, b, t, rec, vox, val, overflow, bs);
+  if (dep) w = __hip_atomic_fetch_add(bs + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const uint32_t pos = bw_fill(w);
+  const uint32_t b = pos < BUCKET_RECORDS ? bw_cur(w) : bw_next(w);
+  const bool ok = dep && pos < 2 * BUCKET_RECORDS && b < K.n_buckets;
+  if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
+  const bool claim = dep && pos == BUCKET_RECORDS;
+  const bool spill = dep && !ok;
+  if (__ballot(claim || spill)) bucket_slow(K, C, W, claim, spill, w, t, vox, val, overflow, bs);
 }
 
-// End of the kernel for one wave: record the fill of every open bucket and retire the unused
-// ids of the batch; add the wave's record and overflow counts.
+// End of the kernel for one wave: retire the unused ids of its batch and add its record and
+// overflow counts. (close_block_buckets then closes the block's words.)
 __device__ __forceinline__ void close_buckets(const KParams& K, const KCold* __restrict__ C, const BucketLog& W,
-                                              uint32_t records, uint32_t overflow, const unsigned long long* bs) {
+                                              uint32_t records, uint32_t overflow) {
   const int lane = threadIdx.x & 63;
-  for (uint32_t t = lane; t < K.bucket_tiles; t += 64) {
-    const unsigned long long w = bs[t];
-    const uint32_t b = (uint32_t)(w >> 32), f = (uint32_t)w;
-    if (b < K.n_buckets) C->bucket_fill[b] = f < BUCKET_RECORDS ? f : BUCKET_RECORDS;
-  }
   const uint32_t id = W.next + lane;
   if (id < W.end && id < K.n_buckets) C->bucket_tile[id] = TILE_INVALID;
   if (lane == 0) {
     if (records) atomicAdd(C->dep_ctl + 3, records);
     if (overflow) atomicAdd(C->dep_ctl + 1, overflow);
+  }
+}
+// After the block's last deposit (behind a block barrier; every thread calls it): the fill of
+// each open bucket, and the unused `next` ids retired. No claim is pending here, so fill is
+// at most BUCKET_RECORDS and nothing was written into `next`.
+__device__ __forceinline__ void close_block_buckets(const KParams& K, const KCold* __restrict__ C,
+                                                    const unsigned long long* bs) {
+  for (uint32_t t = threadIdx.x; t < K.bucket_tiles; t += blockDim.x) {
+    const unsigned long long w = bs[t];
+    const uint32_t cur = bw_cur(w), nx = bw_next(w), f = bw_fill(w);
+    if (cur < K.n_buckets) C->bucket_fill[cur] = f < BUCKET_RECORDS ? f : BUCKET_RECORDS;
+    if (nx < K.n_buckets) C->bucket_tile[nx] = TILE_INVALID;
   }
 }
 

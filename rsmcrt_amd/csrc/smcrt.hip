@@ -117,9 +117,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   // bucketed path's open bucket per tile (fill | id: 2 * bucket_tiles words)
   const uint32_t wave_words = K.bucket_tiles ? 2 * K.bucket_tiles : K.hist_tiles;
   uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * wave_words;
-  // (wave_words is even and sh_dyn 8-byte aligned: the bucket words are 8-byte aligned)
-  unsigned long long* const bstate = (unsigned long long*)whist;
-  if (K.bucket_tiles) init_buckets(bstate, K.bucket_tiles);
+  // the bucketed path's words are shared by the block's waves (deposit.h); sh_dyn is 8-byte
+  // aligned, so they are too
+  unsigned long long* const bstate = (unsigned long long*)(sh_dyn + hist_off);
+  if (K.bucket_tiles) init_buckets(K, C, bstate);
   else
     for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
   // the cooperative EVAL's primitive table (COOP instantiations), after the wave words
@@ -712,8 +713,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   }
 
   if (binned) {
-    if (K.bucket_tiles) close_buckets(K, C, WB, w_dep - overflow, overflow, bstate);
-    else close_log(K, C, W, overflow, whist);
+    if (K.bucket_tiles) {
+      close_buckets(K, C, WB, w_dep - overflow, overflow);
+      __syncthreads();  // every wave of the block is done depositing
+      close_block_buckets(K, C, bstate);
+    } else {
+      close_log(K, C, W, overflow, whist);
+    }
   }
 
 #ifdef SMCRT_DIAG
