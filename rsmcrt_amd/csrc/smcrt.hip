@@ -113,8 +113,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   }
   double* const startp = sh_dyn + hist_off + threadIdx.x;  // [3][256] when n_dets > 0
   if (K.n_dets) hist_off += 3 * 256;
-  // per-wave deposit state: the sorted path's tile histogram (hist_tiles words) or the
-  // bucketed path's open bucket per tile (fill | id: 2 * bucket_tiles words)
+  // deposit state: the sorted path's per-wave tile histogram (hist_tiles words) or the
+  // bucketed path's per-block word per tile (cur | next | fill: 2 * bucket_tiles words)
   const uint32_t wave_words = K.bucket_tiles ? 2 * K.bucket_tiles : K.hist_tiles;
   uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * wave_words;
   // the bucketed path's words are shared by the block's waves (deposit.h); sh_dyn is 8-byte
@@ -953,7 +953,8 @@ static size_t transport_lds(const smcrt_scene* s, uint32_t wave_words, bool xsrc
   return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
          (size_t)4 * wave_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0);
 }
-// LDS words per wave of the deposit state (deposit.h): open buckets or the tile histogram.
+// LDS words per wave of the deposit state (deposit.h): the tile histogram, or open buckets
+// (the bucketed path's words are shared by the block and use the first wave's share).
 static uint32_t wave_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_tiles : s->hist_tiles; }
 
 static TopProps make_props(const smcrt_sdf_node& nd) {
