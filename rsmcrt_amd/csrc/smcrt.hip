@@ -808,7 +808,10 @@ int dalloc(T** p, size_t n) {
 // Record-log slots (and internal launch streams) per scene: launches whose pools are small
 // enough run up to MAX_SLOTS deep, so long-tailed launches overlap more than pairwise.
 constexpr int MAX_SLOTS = 4;
-constexpr uint64_t DEEP_SLOT_BYTES = 24ull << 30;  // a slot pool at most this large: MAX_SLOTS slots
+#ifndef SMCRT_DEEP_SLOT_GIB
+#define SMCRT_DEEP_SLOT_GIB 24
+#endif
+constexpr uint64_t DEEP_SLOT_BYTES = (uint64_t)SMCRT_DEEP_SLOT_GIB << 30;  // a slot pool at most this large: MAX_SLOTS slots
 
 struct smcrt_scene {
   int device = 0;

@@ -221,6 +221,22 @@ def test_pool_exhaustion_spills_to_atomics(monkeypatch, mode):
     assert cpu.counter("deposits") > 20 * 3 * 16384
 
 
+@pytest.mark.parametrize("cap", [0, 4 * 16384], ids=["pool", "small-pool"])
+def test_bucket_contention_pencil_beam(monkeypatch, cap):
+    """Block-shared buckets under the worst contention: a pencil beam along +z through a
+    weakly scattering sphere, so every lane of every wave of a block crosses the same voxels
+    at the same time and files into the same tile word. Claims of the next bucket race with
+    deposits of the other waves (deposits past the next bucket take the exact atomic path),
+    optionally with a pool that runs out; the tallies still equal the oracle's."""
+    if cap:
+        monkeypatch.setenv("SMCRT_POOL_CAP", str(cap))
+    sc = builders.setup_sphere(0.5, 0.01, 0.9, 1.0, 1.0)
+    src = scene.pencil_source((0.0, 0.0, -0.99), (0.0, 0.0, 1.0))
+    gpu, cpu = both(sc, scene.grid(64, 64, 64, 1, 1, 1), src, 60000)
+    compare(gpu, cpu)
+    assert cpu.counter("deposits") > 60000 * 40
+
+
 def test_multi_launch_pool_reuse():
     """A scene reused for batches of very different size (calibration launch, pool growth,
     sub-batching) accumulates exactly the single-run result."""
