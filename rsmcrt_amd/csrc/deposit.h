@@ -371,7 +371,7 @@ constexpr uint32_t BUCKET_BATCH = 64;                    // ids a wave takes at 
 constexpr uint32_t BUCKET_ID_NONE = 0xFFFFFFu;           // no bucket (24-bit id field)
 constexpr uint32_t BUCKET_ID_EXHAUSTED = 0xFFFFFEu;      // pool full: the tile's deposits use atomics
 constexpr uint32_t TILE_INVALID = 0xFFFFFFFFu;           // bucket_tile of an id never used
-constexpr uint32_t MAX_DIRECT_TILES = 512;               // 8 B of LDS per tile per block
+constexpr uint32_t MAX_DIRECT_TILES = 1024;              // 8 B of LDS per tile per block
 constexpr uint32_t MIN_PIECE_BUCKETS = MIN_PIECE_RECORDS / BUCKET_RECORDS;
 // (pool ids stay below 2^24 - 2^20: MAX_POOL_RECORDS <= 2^32 - 2^28 records)
 

@@ -115,7 +115,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   if (K.n_dets) hist_off += 3 * 256;
   // deposit state: the sorted path's per-wave tile histogram (hist_tiles words) or the
   // bucketed path's per-block word per tile (cur | next | fill: 2 * bucket_tiles words)
-  const uint32_t wave_words = K.bucket_tiles ? 2 * K.bucket_tiles : K.hist_tiles;
+  const uint32_t wave_words = K.bucket_tiles ? 0u : K.hist_tiles;
+  const uint32_t dep_words = K.bucket_tiles ? 2 * K.bucket_tiles : 4 * K.hist_tiles;  // the block's
   uint32_t* const whist = (uint32_t*)(sh_dyn + hist_off) + (threadIdx.x >> 6) * wave_words;
   // the bucketed path's words are shared by the block's waves (deposit.h); sh_dyn is 8-byte
   // aligned, so they are too
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   else
     for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
   // the cooperative EVAL's primitive table (COOP instantiations), after the wave words
-  double* const ctab = sh_dyn + hist_off + 2 * wave_words;
+  double* const ctab = sh_dyn + hist_off + dep_words / 2;
   if constexpr (COOP) {
     if (K.ctab)
       for (int i = threadIdx.x; i < CTAB_DOUBLES; i += blockDim.x) ctab[i] = K.ctab[i];
@@ -950,15 +951,16 @@ static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
   return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : (s->coop_lanes > 0 ? 2 : 0)];
 }
 
-// Dynamic LDS of the transport kernel: staged props + faces, then 4 wave tile histograms.
-static size_t transport_lds(const smcrt_scene* s, uint32_t wave_words, bool xsrc) {
+// Dynamic LDS of the transport kernel: staged props + faces, detector start points, then the
+// deposit words (4 wave tile histograms, or the block's bucket words), then the coop table.
+static size_t transport_lds(const smcrt_scene* s, uint32_t dep_words, bool xsrc) {
   const bool ctab = s->d_ctab && !xsrc && s->coop_lanes > 0;  // the COOP instantiation stages it
   return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
-         (size_t)4 * wave_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0);
+         (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0);
 }
-// LDS words per wave of the deposit state (deposit.h): the tile histogram, or open buckets
-// (the bucketed path's words are shared by the block and use the first wave's share).
-static uint32_t wave_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_tiles : s->hist_tiles; }
+// 32-bit LDS words of a block's deposit state (deposit.h): a tile histogram per wave, or one
+// 64-bit bucket word per tile shared by the block.
+static uint32_t dep_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_tiles : 4 * s->hist_tiles; }
 
 static TopProps make_props(const smcrt_sdf_node& nd) {
   TopProps p;  // init_mono, opticalProperties.f90:107-125
@@ -1256,7 +1258,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
-    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, wave_words(s), x == 1));
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, dep_words(s), x == 1));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     (x ? s->grid_blocks_x : s->grid_blocks) = cus * per_cu;
   }
@@ -1347,7 +1349,9 @@ static hipError_t drain_folds(smcrt_scene* s) {
 // or the open bucket of every tile plus the unused ids of its batch (bucketed path).
 static double pool_slack_records(const smcrt_scene* s) {
   const double waves = (double)std::max(s->grid_blocks, s->grid_blocks_x) * 4.0;
-  return s->bucketed ? waves * (double)(s->n_tiles + BUCKET_BATCH) * BUCKET_RECORDS : waves * CHUNK_RECORDS;
+  // bucketed: per block and tile an open bucket and its pre-taken successor, per wave a batch
+  return s->bucketed ? (waves / 4.0 * 2.0 * s->n_tiles + waves * BUCKET_BATCH) * BUCKET_RECORDS
+                     : waves * CHUNK_RECORDS;
 }
 static uint64_t pool_records_for(const smcrt_scene* s, uint64_t n) {
   const double want = (double)n * s->rpp_est * POOL_SLACK + pool_slack_records(s);
@@ -1464,7 +1468,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     const smcrt_detector* a_dets = K.dets;
     const int64_t* a_off = K.det_off;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&a_dets, (void*)&a_off, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, wave_words(s), xsrc), stream));
+    HIPCHK(hipLaunchKernel(transport_fn(s, xsrc), dim3(blocks), dim3(256), args, transport_lds(s, dep_words(s), xsrc), stream));
   }
   HIPCHK(hipGetLastError());
   if (ev) HIPCHK(hipEventRecord(ev[1], stream));
