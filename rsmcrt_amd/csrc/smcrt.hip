@@ -74,11 +74,17 @@ constexpr uint32_t COOP_CULL_LANES = SMCRT_COOP_CULL_LANES;
 #endif
 constexpr int SOLO_LANES = SMCRT_SOLO_LANES;
 
-template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
+// Waves per SIMD the register allocation aims at: 3 (<= 168 VGPRs) for the plain
+// instantiations; the cooperative ones (many tops: LDS table, culling, solo march) hold more
+// live state and spill at 168, so they get 2 (M4 +12 %, profiles/r02_s3/NOTE_waves.txt).
 #ifndef SMCRT_WAVES_PER_EU
 #define SMCRT_WAVES_PER_EU 3
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES_PER_EU))) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
+#ifndef SMCRT_WAVES_PER_EU_COOP
+#define SMCRT_WAVES_PER_EU_COOP 2
+#endif
+template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCRT_WAVES_PER_EU_COOP : SMCRT_WAVES_PER_EU))) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
                                                         const ProgOp* __restrict__ prog,
                                                         const smcrt_detector* __restrict__ dets,
                                                         const int64_t* __restrict__ det_off,
