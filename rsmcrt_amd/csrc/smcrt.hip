@@ -83,8 +83,11 @@ constexpr int SOLO_LANES = SMCRT_SOLO_LANES;
 #ifndef SMCRT_WAVES_PER_EU_COOP
 #define SMCRT_WAVES_PER_EU_COOP 2
 #endif
+#ifndef SMCRT_WAVES_PER_EU_XSRC
+#define SMCRT_WAVES_PER_EU_XSRC SMCRT_WAVES_PER_EU
+#endif
 template <bool LDS_FACES, int GM, bool XSRC, bool COOP>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCRT_WAVES_PER_EU_COOP : SMCRT_WAVES_PER_EU))) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCRT_WAVES_PER_EU_COOP : (XSRC ? SMCRT_WAVES_PER_EU_XSRC : SMCRT_WAVES_PER_EU)))) void transport_kernel(KParams K, const smcrt_sdf_node* __restrict__ nodes,
                                                         const ProgOp* __restrict__ prog,
                                                         const smcrt_detector* __restrict__ dets,
                                                         const int64_t* __restrict__ det_off,
