@@ -367,7 +367,10 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 // The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
-constexpr uint32_t BUCKET_BATCH = 64;                    // ids a wave takes at a time
+#ifndef SMCRT_BUCKET_BATCH
+#define SMCRT_BUCKET_BATCH 64
+#endif
+constexpr uint32_t BUCKET_BATCH = SMCRT_BUCKET_BATCH;    // ids a wave takes at a time (<= 64)
 constexpr uint32_t BUCKET_ID_NONE = 0xFFFFFFu;           // no bucket (24-bit id field)
 constexpr uint32_t BUCKET_ID_EXHAUSTED = 0xFFFFFEu;      // pool full: the tile's deposits use atomics
 constexpr uint32_t TILE_INVALID = 0xFFFFFFFFu;           // bucket_tile of an id never used
