@@ -343,7 +343,9 @@ def escape_bench(args):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each). Without a launcher, bench.py starts the ranks itself "
+                         "(rsmcrt_amd/launch.py); under torch.distributed.run it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="m1", choices=WORKLOADS)
@@ -368,20 +370,46 @@ def main():
     ap.add_argument("--esc-nz", type=int, default=10)
     args = ap.parse_args()
 
+    from rsmcrt_amd import launch
+    if not launch.under_launcher():
+        gpus = 1 if args.gpus is None else args.gpus
+        if gpus != 1:
+            # no launcher: start one rank per GPU here, before anything touches the GPU
+            if args.workload == "escape":
+                log("[bench] the escape workload runs on one GPU; drop --gpus")
+                sys.exit(2)
+            try:
+                rc = launch.spawn(gpus, [sys.executable, os.path.abspath(__file__), *sys.argv[1:]])
+            except launch.LaunchError as e:
+                log(f"[bench] {e}")
+                sys.exit(2)
+            sys.exit(rc)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        log(f"[bench] --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+        sys.exit(2)
+
     if args.workload == "escape":
+        if world != 1:
+            log("[bench] the escape workload runs on one GPU")
+            sys.exit(2)
         escape_bench(args)
         return
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ngpu = torch.cuda.device_count()
+    if local >= ngpu:
+        log(f"[bench] rank {rank} wants GPU {local} but only {ngpu} GPUs are visible")
+        sys.exit(2)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=world)
+        assert dist.get_world_size() == world
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -453,10 +481,12 @@ def main():
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    mine = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    per_rank = [mine.clone() for _ in range(world)]
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+        dist.all_gather(per_rank, mine)
+    per_rank_s = [float(x.item()) for x in per_rank]
+    elapsed = max(per_rank_s)  # the max over ranks
     log(f"[bench] {args.workload}: {args.steps} timed steps in {elapsed:.2f} s")
     kt = eng.kernel_times()  # HIP events around each kernel group, on the launch stream
     eng.set_timing(False)
@@ -474,7 +504,7 @@ def main():
 
     out = None
     if rank == 0:
-        per_rank = 1.0 / world
+        per_rank = 1.0 / world  # (counters were summed over the ranks)
         deposits = float(cdelta[abi.CTR["deposits"]]) * per_rank  # per rank, over the timed steps
         dep_per_launch = deposits / launches
         # algorithmic HBM bytes of the transport kernel: 8 B per jmean deposit (SURVEY.md
@@ -500,6 +530,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (Philox photon streams; scenes from setupGeometry.f90 / SURVEY §8(d))",
+            "rank_seconds": per_rank_s,
             "config": {"workload": desc,
                        "grid": [g.nx, g.ny, g.nz], "photons_per_step_per_gpu": B, "photons_timed": photons,
                        "parallelism": f"photon-index shards x{world}" + (

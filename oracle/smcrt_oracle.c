@@ -1506,9 +1506,20 @@ ORACLE_API int oracle_run(const smcrt_sdf_node* nodes, int32_t n_nodes, const in
   memset(&C, 0, sizeof C);
   C.S = &S;
   C.flags = cfg->flags;
-  C.jmean = (io->jmean || io->jmean_f64) ? calloc((size_t)nv, sizeof(double)) : NULL;
-  C.absorb = (io->absorb || io->absorb_f64) ? calloc((size_t)nv, sizeof(double)) : NULL;
-  C.emission = (io->emission || io->emission_f64) ? calloc((size_t)nv, sizeof(double)) : NULL;
+  /* A grid asked for in fp64 only is accumulated in place: no per-call scratch grid, so a
+   * caller that runs a job in many small calls (bench.py's CPU legs) pays nothing per call.
+   * fp32 grids get a scratch fp64 sum that is added once at the end, as smcrt_run does. */
+  float* gf[3] = {io->jmean, io->absorb, io->emission};
+  double* gd[3] = {io->jmean_f64, io->absorb_f64, io->emission_f64};
+  double* g[3] = {NULL, NULL, NULL};
+  int own[3] = {0, 0, 0};
+  for (int t = 0; t < 3; ++t) {
+    if (gf[t]) { g[t] = calloc((size_t)nv, sizeof(double)); own[t] = 1; }
+    else g[t] = gd[t];
+  }
+  C.jmean = g[0];
+  C.absorb = g[1];
+  C.emission = g[2];
   C.det = io->det_bins;
   C.moments = io->moments;
   C.plan = use_plan ? &plan : NULL;
@@ -1517,11 +1528,8 @@ ORACLE_API int oracle_run(const smcrt_sdf_node* nodes, int32_t n_nodes, const in
     smcrt_photon_record* rec = (io->records && (cfg->flags & SMCRT_FLAG_RECORD_PHOTONS)) ? &io->records[j] : NULL;
     run_photon(&C, src, cfg->first_photon + j, cfg->seed, ds, ds + n_top, rec);
   }
-  double* g[3] = {C.jmean, C.absorb, C.emission};
-  float* gf[3] = {io->jmean, io->absorb, io->emission};
-  double* gd[3] = {io->jmean_f64, io->absorb_f64, io->emission_f64};
   for (int t = 0; t < 3; ++t) {
-    if (!g[t]) continue;
+    if (!own[t]) continue;
     for (int64_t i = 0; i < nv; ++i) {
       if (gf[t]) gf[t][i] = (float)((double)gf[t][i] + g[t][i]);
       if (gd[t]) gd[t][i] += g[t][i];

@@ -1,0 +1,105 @@
+"""One process per GPU without an external launcher.
+
+`python bench.py --gpus N` (no torchrun) must still measure N GPUs. The parent process never
+initialises HIP: it counts the devices (torch.cuda.device_count() does not initialise the
+GPU on this image), fails loudly when fewer than N are visible, then starts N copies of the
+same command with the environment torch.distributed.run would give them (RANK, LOCAL_RANK,
+WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and exits with the first
+non-zero child status (0 when every rank succeeds). Children inherit stdout/stderr, so rank
+0's JSON line is the parent's output.
+
+The reference's equivalent is the OpenMP team of run_MCRT (kernelsMod.f90:1833-1861) plus
+the intended MPI reduce (:2351-2357); here each rank is one GPU.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+
+class LaunchError(RuntimeError):
+    pass
+
+
+def under_launcher() -> bool:
+    """True when a launcher (torch.distributed.run, mpirun wrapper, or this module) already
+    set the rank environment."""
+    return "WORLD_SIZE" in os.environ and "RANK" in os.environ
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_gpus() -> int:
+    """Visible HIP devices, counted without initialising the GPU."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def rank_env(rank: int, world: int, port: int, base=None) -> dict:
+    env = dict(os.environ if base is None else base)
+    env.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                "LOCAL_WORLD_SIZE": str(world), "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(port)})
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    return env
+
+
+def spawn(world: int, argv, need_gpus: bool = True, timeout: float | None = None, env=None) -> int:
+    """Run `argv` as `world` ranks on this node and wait for them. Returns the exit status
+    (the first non-zero one; the other ranks are then terminated). Raises LaunchError when
+    need_gpus and fewer than `world` GPUs are visible."""
+    if world < 1:
+        raise LaunchError(f"--gpus must be >= 1 (got {world})")
+    if need_gpus:
+        n = visible_gpus()
+        if n < world:
+            raise LaunchError(f"--gpus {world} asked for {world} GPUs but only {n} "
+                              f"{'is' if n == 1 else 'are'} visible on this node")
+    port = free_port()
+    procs = [subprocess.Popen(list(argv), env=rank_env(r, world, port, env), start_new_session=True)
+             for r in range(world)]
+    t0 = time.monotonic()
+    status = 0
+    live = set(range(world))
+    try:
+        while live:
+            for r in sorted(live):
+                rc = procs[r].poll()
+                if rc is None:
+                    continue
+                live.discard(r)
+                if rc != 0 and status == 0:
+                    status = rc
+                    print(f"[launch] rank {r} exited with status {rc}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:  # (each rank leads its own process group)
+                        try:
+                            os.killpg(procs[q].pid, signal.SIGTERM)
+                        except ProcessLookupError:
+                            pass
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                for q in live:
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                for q in live:
+                    procs[q].wait()
+                raise LaunchError(f"ranks {sorted(live)} still running after {timeout} s")
+            if live:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.wait()
+    if status < 0:  # killed by a signal: report it as a shell would
+        status = 128 - status
+    return status

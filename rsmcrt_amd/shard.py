@@ -15,16 +15,23 @@ def first_photon(step: int, rank: int, world: int, batch: int, base: int = 0) ->
 
 
 def reduce_tallies(tensors, dist, group=None) -> None:
-    """Sum tally buffers over ranks in place with ONE collective: the tensors are packed into
-    one fp64 buffer (integer counters travel as doubles, exact below 2^53), all-reduced, and
-    copied back. On GPUs the engine's own smcrt_reduce_device_tallies does the same inside
-    libsmcrt over RCCL; this torch form serves gloo (CPU) process groups."""
+    """Sum tally buffers over ranks in place: the floating-point tensors are packed into one
+    fp64 buffer and the integer ones (counters) into one int64 buffer, one all-reduce each,
+    then copied back. Every tensor must be contiguous (it is reduced through a view). On GPUs
+    the engine's own smcrt_reduce_device_tallies does the same inside libsmcrt over RCCL;
+    this torch form serves gloo (CPU) process groups."""
     import torch
-    flat = [t.reshape(-1) for t in tensors]
-    buf = torch.cat([f.to(torch.float64) for f in flat])
-    dist.all_reduce(buf, group=group)
-    at = 0
-    for f in flat:
-        n = f.numel()
-        f.copy_(buf[at:at + n].to(f.dtype))
-        at += n
+    for t in tensors:
+        if not t.is_contiguous():
+            raise ValueError("reduce_tallies needs contiguous tensors (a copy would not reach the caller)")
+    for is_float, dtype in ((True, torch.float64), (False, torch.int64)):
+        part = [t.view(-1) for t in tensors if t.is_floating_point() == is_float]
+        if not part:
+            continue
+        buf = torch.cat([f.to(dtype) for f in part])
+        dist.all_reduce(buf, group=group)
+        at = 0
+        for f in part:
+            n = f.numel()
+            f.copy_(buf[at:at + n].to(f.dtype))
+            at += n
