@@ -361,7 +361,8 @@ def main():
     ap.add_argument("--no-deposit", action="store_true", help="diagnostic: pathlength deposition off")
     ap.add_argument("--sync-fold", action="store_true", help="diagnostic: each step waits for its own fold")
     ap.add_argument("--overlap", type=int, default=1, choices=(0, 1),
-                    help="1: steps run on the scene's two internal streams (SMCRT_FLAG_OVERLAP), so a "
+                    help="1: steps rotate over the scene's internal streams (SMCRT_FLAG_OVERLAP: up to four, two "
+                         "with record pools above 24 GiB), so a "
                          "step's slowest photons finish beside the next step")
     ap.add_argument("--source", default="default", choices=["default", "uniform"],
                     help="diagnostic: uniform = parallelogram source over the z=0.99 plane")

@@ -1,6 +1,9 @@
 ! example_scat_test.f90 — the reference's end-to-end scatter KAT (test/end_to_end/test_scat.f90:
 ! 33-38, res/scat_test.toml via test_kernel) driven from Fortran through smcrt_mod.
-! Usage: example_scat_test [nphotons]; prints "nscatt/photon = <value>" (KAT: 57.5 +- 0.5).
+! Usage: example_scat_test [nphotons [n_gpus]]; prints "nscatt/photon = <value>" (KAT: 57.5 +- 0.5).
+! n_gpus > 0 runs the photons through smcrt_multi_run on devices 0 .. n_gpus-1 (run_MCRT's
+! n_gpus setting, INTEGRATION.md §2.1) instead of smcrt_run on device 0; the counters it prints
+! are the same either way.
 program example_scat_test
     use smcrt_mod
     implicit none
@@ -12,12 +15,13 @@ program example_scat_test
     type(smcrt_source)     :: src
     type(smcrt_run_config) :: cfg
     type(smcrt_tallies)    :: io
-    type(c_ptr)            :: scene
+    type(c_ptr)            :: scene, multi
+    integer(c_int32_t)     :: n_gpus
     real(c_float), allocatable, target :: jmean(:, :, :)
     real(c_double), target     :: nscatt
     integer(c_int64_t), target :: counters(SMCRT_NCOUNTERS)
     real(c_double) :: ident(16)
-    integer :: ierr, nargs
+    integer :: ierr, nargs, i
     character(len=32) :: arg
     integer(c_int64_t) :: nphotons
 
@@ -26,6 +30,11 @@ program example_scat_test
     if (nargs >= 1) then
         call get_command_argument(1, arg)
         read(arg, *) nphotons
+    end if
+    n_gpus = 0
+    if (nargs >= 2) then
+        call get_command_argument(2, arg)
+        read(arg, *) n_gpus
     end if
 
     ident = 0._c_double
@@ -44,9 +53,14 @@ program example_scat_test
     allocate(jmean(grid%nx, grid%ny, grid%nz))
     jmean = 0._c_float
 
-    ierr = smcrt_scene_create(nodes, 2_c_int32_t, top, 2_c_int32_t, grid, dets, 0_c_int32_t, 0_c_int32_t, scene)
+    if (n_gpus > 0) then
+        ierr = smcrt_multi_create(nodes, 2_c_int32_t, top, 2_c_int32_t, grid, dets, 0_c_int32_t, c_null_ptr, &
+                                  n_gpus, multi)
+    else
+        ierr = smcrt_scene_create(nodes, 2_c_int32_t, top, 2_c_int32_t, grid, dets, 0_c_int32_t, 0_c_int32_t, scene)
+    end if
     if (ierr /= SMCRT_OK) then
-        print *, "smcrt_scene_create failed: ", smcrt_error_message()
+        print *, "scene upload failed: ", smcrt_error_message()
         error stop 1
     end if
 
@@ -59,14 +73,26 @@ program example_scat_test
     io%jmean = c_loc(jmean)
     io%nscatt = c_loc(nscatt)
     io%counters = c_loc(counters)
-    ierr = smcrt_run(scene, src, cfg, io)
+    if (n_gpus > 0) then
+        ierr = smcrt_multi_run(multi, src, cfg, io)
+    else
+        ierr = smcrt_run(scene, src, cfg, io)
+    end if
     if (ierr /= SMCRT_OK) then
-        print *, "smcrt_run failed: ", smcrt_error_message()
+        print *, "run failed: ", smcrt_error_message()
         error stop 1
     end if
     ierr = smcrt_normalise_fluence(jmean, grid, nphotons)
     print '(a,f10.5)', "nscatt/photon = ", nscatt / real(nphotons, c_double)
     print '(a,i0)', "photons = ", counters(1)
-    print '(a,es14.6)', "sum(jmean normalised) = ", sum(real(jmean, c_double))
-    call smcrt_scene_destroy(scene)
+    print '(a,es24.16)', "sum(jmean normalised) = ", sum(real(jmean, c_double))
+    print '(a,es24.16)', "nscatt = ", nscatt
+    do i = 1, SMCRT_NCOUNTERS
+        print '(a,i0,a,i0)', "counter ", i - 1, " = ", counters(i)
+    end do
+    if (n_gpus > 0) then
+        call smcrt_multi_destroy(multi)
+    else
+        call smcrt_scene_destroy(scene)
+    end if
 end program example_scat_test

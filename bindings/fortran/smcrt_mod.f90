@@ -31,8 +31,13 @@ module smcrt_mod
     ! run flags
     integer(c_int32_t), parameter :: SMCRT_FLAG_PATHLENGTH = 1, SMCRT_FLAG_SURVIVAL_BIAS = 2, &
         SMCRT_FLAG_RENDER_SOURCE = 4, SMCRT_FLAG_TEST_KERNEL = 8, SMCRT_FLAG_END_EARLY = 16, &
-        SMCRT_FLAG_RECORD_PHOTONS = 32, SMCRT_FLAG_ASYNC_FOLD = 64
+        SMCRT_FLAG_RECORD_PHOTONS = 32, SMCRT_FLAG_ASYNC_FOLD = 64, SMCRT_FLAG_OVERLAP = 128
     integer, parameter :: SMCRT_NCOUNTERS = 16
+    ! multi-GPU: packed-tally fields (smcrt_pack_layout%fields), all visible devices
+    integer(c_int32_t), parameter :: SMCRT_PACK_JMEAN = 1, SMCRT_PACK_ABSORB = 2, SMCRT_PACK_EMISSION = 4, &
+        SMCRT_PACK_DET_BINS = 8
+    integer(c_int32_t), parameter :: SMCRT_ALL_DEVICES = -1
+    integer, parameter :: SMCRT_UNIQUE_ID_BYTES = 128
     ! smcrt_symmetry (escape function, kernelsMod.f90:85-1460)
     integer(c_int32_t), parameter :: SMCRT_SYM_NONE = 0, SMCRT_SYM_PRISM = 1, SMCRT_SYM_FLIPPED = 2, &
         SMCRT_SYM_UNIFORM_SLAB = 3, SMCRT_SYM_NONE_ROTATIONAL = 4, SMCRT_SYM_ROTATIONAL_360 = 5
@@ -114,6 +119,11 @@ module smcrt_mod
         real(c_double)     :: max_step_size = 1._c_double, grad_step_size = 1e-4_c_double, accuracy = 0.01_c_double
         integer(c_int64_t) :: seed = 123456789
     end type smcrt_inverse_config
+
+    type, bind(C) :: smcrt_pack_layout            ! the packed buffer of the multi-GPU reduction
+        integer(c_int64_t) :: n_voxels = 0, n_det_bins = 0
+        integer(c_int32_t) :: fields = 0, reserved = 0
+    end type smcrt_pack_layout
 
     type, bind(C) :: smcrt_kernel_times
         real(c_double)     :: transport_ms = 0._c_double, deposit_ms = 0._c_double
@@ -278,6 +288,128 @@ module smcrt_mod
             type(c_ptr), value                 :: written_path
             integer(c_int32_t), value          :: path_cap
         end function smcrt_write_checkpoint
+
+        ! ---- multi-GPU (SURVEY §8(b) n_gpus, §8(e)): the OpenMP team of run_MCRT
+        ! (kernelsMod.f90:1833-1861) and its intended mpi_reduce (:2351-2357) ----
+        ! one process, several GPUs: `devices` is c_loc of an integer(c_int32_t) array of device
+        ! ordinals, or c_null_ptr for devices 0 .. n_devices-1 (n_devices <= 0: every visible GPU)
+        integer(c_int) function smcrt_multi_create(nodes, n_nodes, top, n_top, grid, dets, n_dets, &
+                devices, n_devices, multi) bind(C, name="smcrt_multi_create")
+            import :: c_int, c_int32_t, c_ptr, smcrt_sdf_node, smcrt_grid, smcrt_detector
+            type(smcrt_sdf_node), intent(in) :: nodes(*)
+            integer(c_int32_t), value        :: n_nodes
+            integer(c_int32_t), intent(in)   :: top(*)
+            integer(c_int32_t), value        :: n_top
+            type(smcrt_grid), intent(in)     :: grid
+            type(smcrt_detector), intent(in) :: dets(*)
+            integer(c_int32_t), value        :: n_dets
+            type(c_ptr), value               :: devices
+            integer(c_int32_t), value        :: n_devices
+            type(c_ptr), intent(out)         :: multi
+        end function smcrt_multi_create
+
+        integer(c_int) function smcrt_multi_info(multi, n_devices) bind(C, name="smcrt_multi_info")
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value              :: multi
+            integer(c_int32_t), intent(out) :: n_devices
+        end function smcrt_multi_info
+
+        type(c_ptr) function smcrt_multi_scene(multi, i) bind(C, name="smcrt_multi_scene")
+            import :: c_int32_t, c_ptr
+            type(c_ptr), value        :: multi
+            integer(c_int32_t), value :: i
+        end function smcrt_multi_scene
+
+        ! smcrt_run over the devices: accumulate + collect
+        integer(c_int) function smcrt_multi_run(multi, src, cfg, io) bind(C, name="smcrt_multi_run")
+            import :: c_int, c_ptr, smcrt_source, smcrt_run_config, smcrt_tallies
+            type(c_ptr), value                 :: multi
+            type(smcrt_source), intent(in)     :: src
+            type(smcrt_run_config), intent(in) :: cfg
+            type(smcrt_tallies), intent(in)    :: io
+        end function smcrt_multi_run
+
+        ! photons handed to the devices in chunks, accumulated on the devices (no collective)
+        integer(c_int) function smcrt_multi_accumulate(multi, src, cfg) bind(C, name="smcrt_multi_accumulate")
+            import :: c_int, c_ptr, smcrt_source, smcrt_run_config
+            type(c_ptr), value                 :: multi
+            type(smcrt_source), intent(in)     :: src
+            type(smcrt_run_config), intent(in) :: cfg
+        end function smcrt_multi_accumulate
+
+        ! ONE packed RCCL reduce of every device's accumulators, added into io
+        integer(c_int) function smcrt_multi_collect(multi, io) bind(C, name="smcrt_multi_collect")
+            import :: c_int, c_ptr, smcrt_tallies
+            type(c_ptr), value              :: multi
+            type(smcrt_tallies), intent(in) :: io
+        end function smcrt_multi_collect
+
+        integer(c_int) function smcrt_multi_device_photons(multi, photons) bind(C, name="smcrt_multi_device_photons")
+            import :: c_int, c_int64_t, c_ptr
+            type(c_ptr), value              :: multi
+            integer(c_int64_t), intent(out) :: photons(*)
+        end function smcrt_multi_device_photons
+
+        subroutine smcrt_multi_destroy(multi) bind(C, name="smcrt_multi_destroy")
+            import :: c_ptr
+            type(c_ptr), value :: multi
+        end subroutine smcrt_multi_destroy
+
+        ! one process per GPU (mpirun): rank 0 makes the id and broadcasts its bytes (e.g. with
+        ! MPI_Bcast), every rank joins on its device, runs smcrt_run_device into device buffers
+        ! and sums them with ONE packed collective (root < 0: all-reduce; else reduce to root)
+        integer(c_int) function smcrt_comm_unique_id(id) bind(C, name="smcrt_comm_unique_id")
+            import :: c_int, c_int8_t
+            integer(c_int8_t), intent(out) :: id(*)
+        end function smcrt_comm_unique_id
+
+        integer(c_int) function smcrt_comm_init_rank(id, n_ranks, rank, device, comm) &
+                bind(C, name="smcrt_comm_init_rank")
+            import :: c_int, c_int8_t, c_int32_t, c_ptr
+            integer(c_int8_t), intent(in) :: id(*)
+            integer(c_int32_t), value     :: n_ranks, rank, device
+            type(c_ptr), intent(out)      :: comm
+        end function smcrt_comm_init_rank
+
+        subroutine smcrt_comm_destroy(comm) bind(C, name="smcrt_comm_destroy")
+            import :: c_ptr
+            type(c_ptr), value :: comm
+        end subroutine smcrt_comm_destroy
+
+        integer(c_int) function smcrt_reduce_device_tallies(scene, comm, dev, root, stream) &
+                bind(C, name="smcrt_reduce_device_tallies")
+            import :: c_int, c_int32_t, c_ptr, smcrt_device_tallies
+            type(c_ptr), value                     :: scene, comm
+            type(smcrt_device_tallies), intent(in) :: dev
+            integer(c_int32_t), value              :: root
+            type(c_ptr), value                     :: stream
+        end function smcrt_reduce_device_tallies
+
+        integer(c_int) function smcrt_scene_fence(scene, stream) bind(C, name="smcrt_scene_fence")
+            import :: c_int, c_ptr
+            type(c_ptr), value :: scene, stream
+        end function smcrt_scene_fence
+
+        ! the packed layout on the host (to move a rank's tallies through MPI instead of RCCL)
+        integer(c_int) function smcrt_pack_size(layout, n) bind(C, name="smcrt_pack_size")
+            import :: c_int, c_int64_t, smcrt_pack_layout
+            type(smcrt_pack_layout), intent(in) :: layout
+            integer(c_int64_t), intent(out)     :: n
+        end function smcrt_pack_size
+
+        integer(c_int) function smcrt_pack_host(layout, t, buf) bind(C, name="smcrt_pack_host")
+            import :: c_int, c_double, smcrt_pack_layout, smcrt_tallies
+            type(smcrt_pack_layout), intent(in) :: layout
+            type(smcrt_tallies), intent(in)     :: t
+            real(c_double), intent(out)         :: buf(*)
+        end function smcrt_pack_host
+
+        integer(c_int) function smcrt_unpack_host(layout, buf, t) bind(C, name="smcrt_unpack_host")
+            import :: c_int, c_double, smcrt_pack_layout, smcrt_tallies
+            type(smcrt_pack_layout), intent(in) :: layout
+            real(c_double), intent(in)          :: buf(*)
+            type(smcrt_tallies), intent(in)     :: t
+        end function smcrt_unpack_host
 
         integer(c_int) function smcrt_normalise_fluence(grid_data, grid, nphotons) &
                 bind(C, name="smcrt_normalise_fluence")

@@ -202,8 +202,9 @@ enum {
   SMCRT_FLAG_RECORD_PHOTONS = 1u << 5, /* fill smcrt_tallies.records (debug/parity) */
   SMCRT_FLAG_ASYNC_FOLD = 1u << 6,     /* smcrt_run_device: the jmean fold may finish after later work
                                           on the stream; jmean is complete after smcrt_scene_fence */
-  SMCRT_FLAG_OVERLAP = 1u << 7         /* smcrt_run_device: launches run on the scene's two internal
-                                          streams, each after the caller's earlier work, so launch k+1
+  SMCRT_FLAG_OVERLAP = 1u << 7         /* smcrt_run_device: launches rotate over up to four internal
+                                          streams of the scene (two with SMCRT_SLOTS=2 or record pools
+                                          above 24 GiB), each after the caller's earlier work, so launch k+1
                                           fills the GPU while launch k's slowest photons finish; every
                                           tally is complete in `stream` order only after
                                           smcrt_scene_fence (implies SMCRT_FLAG_ASYNC_FOLD) */
@@ -508,10 +509,15 @@ int smcrt_reduce_device_tallies(smcrt_scene* scene, smcrt_comm* comm, smcrt_devi
 
 /* One process, several GPUs: smcrt_run with n_gpus. smcrt_multi_create
  * uploads the scene to each of `devices` (NULL: devices 0 .. n_devices-1; n_devices <= 0:
- * every visible device); smcrt_multi_run gives device g the photons
- * [first + g*N/n, first + (g+1)*N/n) and sums the devices' tallies onto the first device with
- * one packed RCCL reduce, then accumulates them into `io` as smcrt_run does. Results do not
- * depend on the number of devices (up to the fp64 summation order of jmean). */
+ * every visible device) and gives each device resident fp64 accumulators.
+ * smcrt_multi_accumulate runs photons [first, first + N) in chunks handed to whichever device
+ * has a free launch slot (overlapped launches, nothing waited for); smcrt_multi_collect sums
+ * every device's accumulators onto the first device with ONE packed RCCL reduce, adds them
+ * into `io` as smcrt_run does and zeroes the accumulators. A job split into batches therefore
+ * pays one collective when it collects (per checkpoint, or once), not one per batch.
+ * smcrt_multi_run = accumulate + collect. Results do not depend on the number of devices or
+ * on which device ran which chunk (up to the fp64 summation order of jmean); counters and
+ * integer tallies are exact. Photon records are refused (use smcrt_run). */
 typedef struct smcrt_multi smcrt_multi;
 int smcrt_multi_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t* top, int32_t n_top,
                        const smcrt_grid* grid, const smcrt_detector* dets, int32_t n_dets,
@@ -520,6 +526,10 @@ int smcrt_multi_info(const smcrt_multi* multi, int32_t* n_devices);
 /* The scene on device slot i (0 <= i < n_devices), e.g. for smcrt_scene_set_optprops. */
 smcrt_scene* smcrt_multi_scene(smcrt_multi* multi, int32_t i);
 int smcrt_multi_run(smcrt_multi* multi, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io);
+int smcrt_multi_accumulate(smcrt_multi* multi, const smcrt_source* src, const smcrt_run_config* cfg);
+int smcrt_multi_collect(smcrt_multi* multi, smcrt_tallies* io);
+/* Photons each device ran since the last collect (n_devices entries; load-balance diagnostic). */
+int smcrt_multi_device_photons(const smcrt_multi* multi, uint64_t* photons);
 void smcrt_multi_destroy(smcrt_multi* multi);
 
 /* ---- output formats (src/writer.f90), host-side, no GPU needed ------------------------

@@ -208,5 +208,6 @@ EXPORTED_SYMBOLS = [
     "smcrt_job_run_inverse", "smcrt_scene_fence",
     "smcrt_pack_size", "smcrt_pack_host", "smcrt_unpack_host", "smcrt_comm_unique_id", "smcrt_comm_init_rank",
     "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_multi_create", "smcrt_multi_info",
-    "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_destroy", "smcrt_job_run_devices",
+    "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_accumulate", "smcrt_multi_collect",
+    "smcrt_multi_device_photons", "smcrt_multi_destroy", "smcrt_job_run_devices",
 ]

@@ -358,19 +358,37 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 // `cur` is the tile's open bucket, `next` the bucket that follows it (taken in advance), and
 // fill the records claimed in `cur`. A deposit is one LDS add-and-return of 1 on that word,
 // which hands it its slot: fill < BUCKET_RECORDS -> cur[fill]; fill in [BUCKET_RECORDS,
-// 2*BUCKET_RECORDS) -> next[fill - BUCKET_RECORDS], so no deposit ever waits for another;
-// beyond that (a claim still pending) -> an exact fp64 atomic. The deposit that found fill at
-// exactly BUCKET_RECORDS takes the slow path: it makes `next` the open bucket, takes a fresh
-// `next` from its wave's batch of ids (BUCKET_BATCH per returning atomic) and rebases fill
-// with one compare-and-swap. Sharing the words per block (round 2: per wave before) keeps 4x
-// fewer buckets open, so their partly written cache lines fit in L2 and leave it whole.
+// 2*BUCKET_RECORDS) -> next[fill - BUCKET_RECORDS], so no deposit waits for a claim in the
+// common case. The deposit that found fill at exactly BUCKET_RECORDS takes the slow path: it
+// makes `next` the open bucket, takes a fresh `next` from its wave's batch of ids
+// (BUCKET_BATCH per returning atomic) and rebases fill with one compare-and-swap. A deposit
+// that finds fill >= 2*BUCKET_RECORDS (both buckets full while that claim is still pending)
+// places nothing: its lane waits until the claim has changed the word, then adds again.
+//
+// Why fill cannot carry into `next` (16 bits: 65536). fill only grows by deposit adds, and
+// the claim's CAS is the only thing that lowers it. At most one claim per tile is pending:
+// it is made by the one add that reads exactly BUCKET_RECORDS, and fill cannot read that
+// value again before the CAS rebases it. While it is pending, the adds read BUCKET_RECORDS ..
+// 2*BUCKET_RECORDS - 1 (each gets a slot in `next`) and then values >= 2*BUCKET_RECORDS; a
+// lane whose add read such a value places nothing and adds again only after the word has
+// changed (the CAS), so each of the block's 256 lanes makes at most one such add per pending
+// claim. Hence fill <= 2*BUCKET_RECORDS + 256 = 768 however long the claiming wave takes
+// (its returning batch atomic included), and the CAS caps it at 2*BUCKET_RECORDS before
+// subtracting BUCKET_RECORDS. The claiming wave makes its claims before any of its own lanes
+// wait, and a claim waits for nothing but its own atomics, so every wait ends.
+// Sharing the words per block (round 2: per wave before) keeps 4x fewer buckets open, so
+// their partly written cache lines fit in L2 and leave it whole.
 // The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
 #ifndef SMCRT_BUCKET_BATCH
 #define SMCRT_BUCKET_BATCH 64
 #endif
-constexpr uint32_t BUCKET_BATCH = SMCRT_BUCKET_BATCH;    // ids a wave takes at a time (<= 64)
+constexpr uint32_t BUCKET_BATCH = SMCRT_BUCKET_BATCH;    // ids a wave takes at a time
+// One deposit wave-instruction makes at most 64 claims (one per lane) and the batch must
+// cover them (bucket_slow takes at most one new batch per instruction); the retirement of
+// unused ids (one lane per id) covers at most 64 ids. Both hold exactly for 64.
+static_assert(BUCKET_BATCH == 64, "bucket id batches must be exactly one id per lane of a wave");
 constexpr uint32_t BUCKET_ID_NONE = 0xFFFFFFu;           // no bucket (24-bit id field)
 constexpr uint32_t BUCKET_ID_EXHAUSTED = 0xFFFFFEu;      // pool full: the tile's deposits use atomics
 constexpr uint32_t TILE_INVALID = 0xFFFFFFFFu;           // bucket_tile of an id never used
@@ -406,7 +424,8 @@ __device__ __forceinline__ void init_buckets(const KParams& K, const KCold* __re
 }
 
 // The rare part of a deposit instruction (wave-uniform call): the claims of the lanes that
-// found fill == BUCKET_RECORDS, and the exact atomic for lanes that found no slot.
+// found fill == BUCKET_RECORDS, and the exact atomic for lanes whose bucket does not exist
+// (pool exhausted).
 __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __restrict__ C, BucketLog& W,
                                             bool claim, bool spill, unsigned long long w, uint32_t t,
                                             uint32_t vox, double val, uint32_t& overflow, unsigned long long* bs) {
@@ -432,8 +451,11 @@ __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __res
       C->bucket_tile[nx] = t;
       atomicAdd(C->tile_nb + t, 1u);
     }
-    // cur <- next, next <- fresh, fill -= BUCKET_RECORDS; deposits that came after the next
-    // bucket filled up (fill >= 2*BUCKET_RECORDS) took the atomic path, so fill is capped
+    // debug knob (SMCRT_DEBUG_CLAIM_DELAY, tests only): hold the claim open so that other
+    // waves fill both buckets and wait
+    for (uint32_t d = 0; d < K.claim_delay; ++d) __builtin_amdgcn_s_sleep(127);
+    // cur <- next, next <- fresh, fill -= BUCKET_RECORDS; adds that found fill >=
+    // 2*BUCKET_RECORDS placed nothing (their lanes add again after this), so fill is capped
     // first and the deposit that finds BUCKET_RECORDS again opens `fresh`. Only this lane
     // changes cur/next while its claim is pending, so they are still (cur, nx) here.
     unsigned long long old = __hip_atomic_load(bs + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -452,20 +474,36 @@ __device__ __forceinline__ void bucket_slow(const KParams& K, const KCold* __res
   overflow += (uint32_t)__popcll(__ballot(spill));
 }
 
+// File one deposit per lane with dep == true (wave-uniform call).
 __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __restrict__ C, BucketLog& W, bool dep,
                                               uint32_t vox, double val, uint32_t& overflow,
                                               unsigned long long* bs) {
   if (!__ballot(dep)) return;
   const uint32_t t = vox >> TILE_SHIFT;
-  unsigned long long w = 0;
-  if (dep) w = __hip_atomic_fetch_add(bs + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const uint32_t pos = bw_fill(w);
-  const uint32_t b = pos < BUCKET_RECORDS ? bw_cur(w) : bw_next(w);
-  const bool ok = dep && pos < 2 * BUCKET_RECORDS && b < K.n_buckets;
-  if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
-  const bool claim = dep && pos == BUCKET_RECORDS;
-  const bool spill = dep && !ok;
-  if (__ballot(claim || spill)) bucket_slow(K, C, W, claim, spill, w, t, vox, val, overflow, bs);
+  bool todo = dep;
+  for (;;) {  // wave-uniform; one pass unless a lane found both of its tile's buckets full
+    unsigned long long w = 0;
+    if (todo) w = __hip_atomic_fetch_add(bs + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t pos = bw_fill(w);
+    const uint32_t b = pos < BUCKET_RECORDS ? bw_cur(w) : bw_next(w);
+    const bool slot = todo && pos < 2 * BUCKET_RECORDS;
+    const bool ok = slot && b < K.n_buckets;
+    if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
+    const bool claim = todo && pos == BUCKET_RECORDS;
+    const bool spill = slot && !ok;
+    const bool wait = todo && !slot;  // both buckets full: a claim is pending in another wave
+    if (!__ballot(claim || spill || wait)) return;
+    bucket_slow(K, C, W, claim, spill, w, t, vox, val, overflow, bs);
+    if (!__ballot(wait)) return;
+    if (wait) {  // until the pending claim has rebased the word (see the bound above)
+      unsigned long long x;
+      do {
+        __builtin_amdgcn_s_sleep(2);
+        x = __hip_atomic_load(bs + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } while (bw_fill(x) >= 2 * BUCKET_RECORDS && bw_cur(x) == bw_cur(w));
+    }
+    todo = wait;
+  }
 }
 
 // End of the kernel for one wave: retire the unused ids of its batch and add its record and

@@ -880,8 +880,8 @@ extern "C" {
 // then finalise's normalisation and writes (:2321-2416) under `outdir` (the reference's
 // fileplace): jmean/<fluence>, emission/<render_source_name>, absorb/absorb.nrrd,
 // detectors/detector_<i>.dat. `io` (may be NULL) receives the tallies as well.
-// `devices` empty: one scene on `device`; else one smcrt_multi over those GPUs (photon shards
-// + one RCCL reduce per checkpoint batch).
+// `devices` empty: one scene on `device`; else one smcrt_multi over those GPUs (photon chunks
+// handed out dynamically + one RCCL reduce per checkpoint written, or one per job).
 static int job_run_impl(smcrt_job* J0, int32_t device, const std::vector<int32_t>& devices, const char* outdir,
                         double* nscatt_out) {
   if (!J0 || !outdir) return ffail(SMCRT_ERR_INVALID_ARG, "NULL argument");
@@ -946,18 +946,36 @@ static int job_run_impl(smcrt_job* J0, int32_t device, const std::vector<int32_t
   std::memset(&cfg, 0, sizeof(cfg));
   cfg.seed = (uint64_t)J->iseed;
   cfg.flags = SMCRT_FLAG_PATHLENGTH | (J->render_source ? SMCRT_FLAG_RENDER_SOURCE : 0);
-  // checkpoint every checkpoint_every_n photons (run_MCRT, kernelsMod.f90:1865): the GPU
-  // runs batches of that size; after each, photons [0, j) are complete and jmean holds
-  // exactly their tally, written with the reference's checkpoint layout (writer.f90:426-457)
-  const int64_t every = J->ckptfreq > 0 ? J->ckptfreq : J->nphotons;
+  // checkpoints (run_MCRT, kernelsMod.f90:1862): the reference's thread 0 writes one whenever
+  // its j is a multiple of checkpoint_every_n, each replacing the last. Here the GPUs run
+  // batches of a multiple of checkpoint_every_n photons, at least MIN_BATCH per GPU (the
+  // res/*.toml files ask for every 10^4 photons, far below one launch); after each batch,
+  // photons [0, j) are complete and jmean holds exactly their tally, written with the
+  // reference's checkpoint layout (writer.f90:426-457). Without checkpoints the whole job is
+  // one batch. With several GPUs the batches accumulate on the devices and are reduced (one
+  // RCCL collective) only when a checkpoint is written and at the end.
+  constexpr int64_t MIN_BATCH = 4 << 20;
+  const int64_t every = J->ckptfreq > 0 ? J->ckptfreq : std::max<int64_t>(1, J->nphotons);
+  const int64_t want = MIN_BATCH * (int64_t)std::max<size_t>(1, devices.size());
+  const int64_t batch = J->ckptfreq > 0 ? every * ((want + every - 1) / every) : every;
+  // the last multiple of checkpoint_every_n is always a batch end, so the final checkpoint
+  // is the one the reference writes last
+  const int64_t last = J->ckptfreq > 0 ? (J->nphotons / every) * every : 0;
   std::vector<float> tmp;
   for (int64_t done = 0; done < J->nphotons && !st;) {
-    const int64_t n = std::min<int64_t>(every, J->nphotons - done);
+    const int64_t end = done < last ? std::min<int64_t>(done + batch, last) : J->nphotons;
+    const int64_t n = end - done;
     cfg.n_photons = (uint64_t)n;
     cfg.first_photon = (uint64_t)done;
-    st = scene ? smcrt_run(scene, &J->src, &cfg, &io) : smcrt_multi_run(multi, &J->src, &cfg, &io);
     done += n;
-    if (!st && done % every == 0 && J->ckptfreq > 0) {
+    const bool ckpt = J->ckptfreq > 0 && done <= last && done % every == 0;
+    if (scene) {
+      st = smcrt_run(scene, &J->src, &cfg, &io);
+    } else {
+      st = smcrt_multi_accumulate(multi, &J->src, &cfg);
+      if (!st && (ckpt || done >= J->nphotons)) st = smcrt_multi_collect(multi, &io);
+    }
+    if (!st && ckpt) {
       tmp.resize(nv);
       for (size_t i = 0; i < nv; ++i) tmp[i] = (float)jm[i];
       const size_t sl = J->toml_path.rfind('/');

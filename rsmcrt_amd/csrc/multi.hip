@@ -16,6 +16,9 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <thread>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -145,11 +148,16 @@ struct smcrt_multi {
   std::vector<int32_t> devices;
   std::vector<smcrt_scene*> scenes;
   std::vector<ncclComm_t> comms;
-  std::vector<double*> d_buf;                  // per device: the packed tallies of its shard
-  std::vector<unsigned long long*> d_ctr;      // per device: uint64 counters of its shard
-  size_t cap = 0;                              // doubles in each d_buf
+  // per device: resident fp64 accumulators in the packed layout of every field (grids, det
+  // bins, scalars, counters as doubles) and the device's uint64 counters; photons accumulate
+  // here across smcrt_multi_accumulate calls until smcrt_multi_collect reduces them
+  std::vector<double*> d_buf;
+  std::vector<unsigned long long*> d_ctr;
+  smcrt_pack_layout layout{};
+  Offsets o;
   smcrt_grid grid{};
   int64_t n_det_bins = 0;
+  std::vector<uint64_t> photons;  // photons each device ran since the last collect
   std::mutex mu;
 };
 
@@ -305,6 +313,7 @@ int smcrt_reduce_device_tallies(smcrt_scene* scene, smcrt_comm* cm, smcrt_device
 // ------------------------------------------------------------------ one process, n GPUs ----
 void smcrt_multi_destroy(smcrt_multi* m) {
   if (!m) return;
+  for (smcrt_scene* s : m->scenes) smcrt_scene_destroy(s);  // (waits for its launches first)
   for (size_t i = 0; i < m->devices.size(); ++i) {
     (void)hipSetDevice(m->devices[i]);
     if (i < m->d_buf.size() && m->d_buf[i]) (void)hipFree(m->d_buf[i]);
@@ -312,7 +321,6 @@ void smcrt_multi_destroy(smcrt_multi* m) {
   }
   for (ncclComm_t c : m->comms)
     if (c && rccl().ok) (void)rccl().comm_destroy(c);
-  for (smcrt_scene* s : m->scenes) smcrt_scene_destroy(s);
   delete m;
 }
 
@@ -356,8 +364,24 @@ int smcrt_multi_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     std::fill(m->comms.begin(), m->comms.end(), nullptr);
     return bail(fail(SMCRT_ERR_RCCL, std::string("ncclCommInitAll failed: ") + R.error_string(r)));
   }
+  m->layout.n_voxels = (int64_t)grid->nx * grid->ny * grid->nz;
+  m->layout.n_det_bins = m->n_det_bins;
+  m->layout.fields = SMCRT_PACK_JMEAN | SMCRT_PACK_ABSORB | SMCRT_PACK_EMISSION |
+                     (m->n_det_bins > 0 ? SMCRT_PACK_DET_BINS : 0u);
+  m->o = offsets(m->layout);
   m->d_buf.assign(devs.size(), nullptr);
   m->d_ctr.assign(devs.size(), nullptr);
+  m->photons.assign(devs.size(), 0);
+  for (size_t g = 0; g < devs.size(); ++g) {
+    if (hipSetDevice(devs[g]) != hipSuccess ||
+        hipMalloc((void**)&m->d_buf[g], sizeof(double) * (size_t)m->o.total) != hipSuccess ||
+        hipMalloc((void**)&m->d_ctr[g], sizeof(unsigned long long) * SMCRT_NCOUNTERS) != hipSuccess ||
+        hipMemset(m->d_buf[g], 0, sizeof(double) * (size_t)m->o.total) != hipSuccess ||
+        hipMemset(m->d_ctr[g], 0, sizeof(unsigned long long) * SMCRT_NCOUNTERS) != hipSuccess) {
+      (void)hipGetLastError();
+      return bail(fail(SMCRT_ERR_OOM, "multi: device accumulators could not be allocated"));
+    }
+  }
   *out = m;
   return SMCRT_OK;
 }
@@ -373,63 +397,75 @@ smcrt_scene* smcrt_multi_scene(smcrt_multi* m, int32_t i) {
   return m->scenes[(size_t)i];
 }
 
-int smcrt_multi_run(smcrt_multi* m, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io) {
-  g_last_error.clear();
-  if (!m || !src || !cfg || !io) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
-  if ((cfg->flags & SMCRT_FLAG_RECORD_PHOTONS) && io->records)
-    return fail(SMCRT_ERR_INVALID_ARG, "photon records are not kept by smcrt_multi_run (use smcrt_run)");
-  std::lock_guard<std::mutex> guard(m->mu);
+// The device tallies of slot g (pointers into its packed accumulator).
+static smcrt_device_tallies device_tallies(const smcrt_multi* m, size_t g) {
+  smcrt_device_tallies dt;
+  std::memset(&dt, 0, sizeof dt);
+  double* B = m->d_buf[g];
+  const Offsets& o = m->o;
+  dt.jmean = B + o.jmean;
+  dt.absorb = B + o.absorb;
+  dt.emission = B + o.emission;
+  if (o.det >= 0) dt.det_bins = B + o.det;
+  dt.nscatt = B + o.nscatt;
+  dt.moments = B + o.moments;
+  dt.counters = (uint64_t*)m->d_ctr[g];
+  return dt;
+}
+
+// Photons [first, first + n) in chunks handed to whichever device has a free launch slot
+// (guided: a chunk is half of what is left per device, at least `min_chunk`), each an
+// overlapped smcrt_run_device into that device's accumulators. A chunk's results do not
+// depend on the device it lands on (Philox streams keyed by the global photon index), so a
+// tail-bound scene keeps every GPU busy until the end instead of waiting for the slowest of
+// n static shards. Returns when every chunk is launched; nothing is waited for.
+static int accumulate_locked(smcrt_multi* m, const smcrt_source* src, const smcrt_run_config* cfg) {
+  if (cfg->flags & SMCRT_FLAG_RECORD_PHOTONS)
+    return fail(SMCRT_ERR_INVALID_ARG, "photon records are not kept by the multi-GPU path (use smcrt_run)");
+  const size_t n = m->devices.size();
+  uint64_t min_chunk = 1ull << 20;
+  if (const char* e = std::getenv("SMCRT_MULTI_CHUNK")) min_chunk = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+  smcrt_run_config c = *cfg;
+  c.flags = (cfg->flags | SMCRT_FLAG_OVERLAP | SMCRT_FLAG_ASYNC_FOLD) & ~(uint32_t)SMCRT_FLAG_RECORD_PHOTONS;
+  const uint64_t N = cfg->n_photons;
+  uint64_t issued = 0;
+  while (issued < N) {
+    bool launched = false;
+    for (size_t g = 0; g < n && issued < N; ++g) {
+      smcrt_scene* s = m->scenes[g];
+      if (smcrt::scene_inflight(s) >= smcrt::scene_depth(s)) continue;
+      const uint64_t rem = N - issued;
+      uint64_t k = std::max<uint64_t>(min_chunk, rem / (2 * n));
+      if (k > rem) k = rem;
+      c.n_photons = k;
+      c.first_photon = cfg->first_photon + issued;
+      smcrt_device_tallies dt = device_tallies(m, g);
+      const int rs = smcrt_run_device(s, src, &c, &dt, smcrt::scene_stream(s));
+      if (rs) return rs;
+      m->photons[g] += k;
+      issued += k;
+      launched = true;
+    }
+    if (!launched) std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  return SMCRT_OK;
+}
+
+// One packed RCCL reduce of every device's accumulators onto the first device, added into
+// `io` as smcrt_run adds a run's totals; the accumulators are zeroed for the next photons.
+static int collect_locked(smcrt_multi* m, smcrt_tallies* io) {
   const Rccl& R = rccl();
   if (!R.ok) return fail(SMCRT_ERR_RCCL, R.err);
   const size_t n = m->devices.size();
-  smcrt_pack_layout L{};
-  L.n_voxels = (int64_t)m->grid.nx * m->grid.ny * m->grid.nz;
-  L.n_det_bins = m->n_det_bins;
-  L.fields = ((io->jmean || io->jmean_f64) ? SMCRT_PACK_JMEAN : 0u) |
-             ((io->absorb || io->absorb_f64) ? SMCRT_PACK_ABSORB : 0u) |
-             ((io->emission || io->emission_f64) ? SMCRT_PACK_EMISSION : 0u) |
-             ((io->det_bins && L.n_det_bins > 0) ? SMCRT_PACK_DET_BINS : 0u);
-  const Offsets o = offsets(L);
-  if ((size_t)o.total > m->cap) {
-    for (size_t g = 0; g < n; ++g) {
-      HIPCHK(hipSetDevice(m->devices[g]));
-      HIPCHK(hipDeviceSynchronize());
-      if (m->d_buf[g]) HIPCHK(hipFree(m->d_buf[g]));
-      m->d_buf[g] = nullptr;
-      HIPCHK(hipMalloc((void**)&m->d_buf[g], sizeof(double) * (size_t)o.total));
-      if (!m->d_ctr[g]) HIPCHK(hipMalloc((void**)&m->d_ctr[g], sizeof(unsigned long long) * SMCRT_NCOUNTERS));
-    }
-    m->cap = (size_t)o.total;
-  }
-  // a synchronous run: each shard's folds join its stream before the reduce
-  smcrt_run_config c = *cfg;
-  c.flags &= ~(uint32_t)(SMCRT_FLAG_ASYNC_FOLD | SMCRT_FLAG_RECORD_PHOTONS);
-  const uint64_t N = cfg->n_photons;
-  for (size_t g = 0; g < n; ++g) {  // launches are asynchronous: the shards run concurrently
+  const Offsets& o = m->o;
+  for (size_t g = 0; g < n; ++g) {
     smcrt_scene* s = m->scenes[g];
     hipStream_t st = (hipStream_t)smcrt::scene_stream(s);
-    double* B = m->d_buf[g];
-    HIPCHK(hipSetDevice(m->devices[g]));
-    HIPCHK(hipMemsetAsync(B, 0, sizeof(double) * (size_t)o.total, st));
-    HIPCHK(hipMemsetAsync(m->d_ctr[g], 0, sizeof(unsigned long long) * SMCRT_NCOUNTERS, st));
-    smcrt_device_tallies dt;
-    std::memset(&dt, 0, sizeof dt);
-    if (o.jmean >= 0) dt.jmean = B + o.jmean;
-    if (o.absorb >= 0) dt.absorb = B + o.absorb;
-    if (o.emission >= 0) dt.emission = B + o.emission;
-    if (o.det >= 0) dt.det_bins = B + o.det;
-    dt.nscatt = B + o.nscatt;
-    dt.moments = B + o.moments;
-    dt.counters = (uint64_t*)m->d_ctr[g];
-    // shard g: photons [first + g*N/n, first + (g+1)*N/n) (a 128-bit product: no overflow)
-    const uint64_t lo = (uint64_t)(((unsigned __int128)N * g) / n), hi = (uint64_t)(((unsigned __int128)N * (g + 1)) / n);
-    c.first_photon = cfg->first_photon + lo;
-    c.n_photons = hi - lo;
-    const int rs = smcrt_run_device(s, src, &c, &dt, (void*)st);
-    if (rs) return rs;
+    const int fs = smcrt_scene_fence(s, st);  // every launch and fold of this device
+    if (fs) return fs;
     HIPCHK(hipSetDevice(m->devices[g]));
     hipLaunchKernelGGL(counters_to_f64, dim3(1), dim3(64), 0, st, (const unsigned long long*)m->d_ctr[g],
-                       B + o.counters);
+                       m->d_buf[g] + o.counters);
     HIPCHK(hipGetLastError());
   }
   NCCLCHK(R.group_start());
@@ -439,17 +475,57 @@ int smcrt_multi_run(smcrt_multi* m, const smcrt_source* src, const smcrt_run_con
                      (hipStream_t)smcrt::scene_stream(m->scenes[g])));
   }
   NCCLCHK(R.group_end());
-  std::vector<double> h((size_t)o.total);
   for (size_t g = n; g-- > 0;) {  // root last: its copy is the sum
     HIPCHK(hipSetDevice(m->devices[g]));
     const hipError_t e = hipStreamSynchronize((hipStream_t)smcrt::scene_stream(m->scenes[g]));
     if (e != hipSuccess)
-      return fail(SMCRT_ERR_DEVICE_FAULT, std::string("shard on device ") + std::to_string(m->devices[g]) + ": " +
+      return fail(SMCRT_ERR_DEVICE_FAULT, std::string("device ") + std::to_string(m->devices[g]) + ": " +
                                               hipGetErrorString(e));
   }
+  std::vector<double> h((size_t)o.total);
   HIPCHK(hipSetDevice(m->devices[0]));
   HIPCHK(hipMemcpy(h.data(), m->d_buf[0], sizeof(double) * h.size(), hipMemcpyDeviceToHost));
-  return smcrt_unpack_host(&L, h.data(), io);
+  for (size_t g = 0; g < n; ++g) {
+    hipStream_t st = (hipStream_t)smcrt::scene_stream(m->scenes[g]);
+    HIPCHK(hipSetDevice(m->devices[g]));
+    HIPCHK(hipMemsetAsync(m->d_buf[g], 0, sizeof(double) * (size_t)o.total, st));
+    HIPCHK(hipMemsetAsync(m->d_ctr[g], 0, sizeof(unsigned long long) * SMCRT_NCOUNTERS, st));
+    m->photons[g] = 0;
+  }
+  return smcrt_unpack_host(&m->layout, h.data(), io);  // (NULL tallies of io are skipped)
+}
+
+int smcrt_multi_accumulate(smcrt_multi* m, const smcrt_source* src, const smcrt_run_config* cfg) {
+  g_last_error.clear();
+  if (!m || !src || !cfg) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> guard(m->mu);
+  return accumulate_locked(m, src, cfg);
+}
+
+int smcrt_multi_collect(smcrt_multi* m, smcrt_tallies* io) {
+  g_last_error.clear();
+  if (!m || !io) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> guard(m->mu);
+  return collect_locked(m, io);
+}
+
+int smcrt_multi_device_photons(const smcrt_multi* m, uint64_t* photons) {
+  if (!m || !photons) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  for (size_t g = 0; g < m->photons.size(); ++g) photons[g] = m->photons[g];
+  return SMCRT_OK;
+}
+
+int smcrt_multi_run(smcrt_multi* m, const smcrt_source* src, const smcrt_run_config* cfg, smcrt_tallies* io) {
+  g_last_error.clear();
+  if (!m || !src || !cfg || !io) return fail(SMCRT_ERR_INVALID_ARG, "NULL argument");
+  if ((cfg->flags & SMCRT_FLAG_RECORD_PHOTONS) && io->records)
+    return fail(SMCRT_ERR_INVALID_ARG, "photon records are not kept by smcrt_multi_run (use smcrt_run)");
+  std::lock_guard<std::mutex> guard(m->mu);
+  smcrt_run_config c = *cfg;
+  c.flags &= ~(uint32_t)SMCRT_FLAG_RECORD_PHOTONS;
+  const int st = accumulate_locked(m, src, &c);
+  if (st) return st;
+  return collect_locked(m, io);
 }
 
 }  // extern "C"

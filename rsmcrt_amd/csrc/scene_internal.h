@@ -13,4 +13,9 @@ int scene_det_size(const smcrt_scene* s, int32_t d, int64_t* n);
 // the HIP device and the scene's own launch stream (a hipStream_t), for the multi-GPU driver
 int scene_device(const smcrt_scene* s);
 void* scene_stream(const smcrt_scene* s);
+// launches of the scene still running (SMCRT_FLAG_OVERLAP, on its internal streams), and how
+// many may be in flight at once; a multi-GPU driver hands a device more photons while
+// scene_inflight < scene_depth
+int scene_inflight(smcrt_scene* s);
+int scene_depth(const smcrt_scene* s);
 }  // namespace smcrt

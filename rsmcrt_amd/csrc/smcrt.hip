@@ -1317,6 +1317,17 @@ int smcrt::scene_node_optprops(const smcrt_scene* s, int32_t i, double out[4]) {
 int smcrt::scene_device(const smcrt_scene* s) { return s->device; }
 void* smcrt::scene_stream(const smcrt_scene* s) { return (void*)s->stream; }
 
+int smcrt::scene_inflight(smcrt_scene* s) {
+  std::lock_guard<std::mutex> g(s->mu);
+  int n = 0;
+  for (int i = 0; i < MAX_SLOTS; ++i) {
+    if (s->lpending[i] && hipEventQuery(s->lev[i]) == hipSuccess) s->lpending[i] = false;
+    n += s->lpending[i] ? 1 : 0;
+  }
+  return n;
+}
+int smcrt::scene_depth(const smcrt_scene* s) { return s->n_slots; }
+
 int smcrt::scene_det_size(const smcrt_scene* s, int32_t d, int64_t* n) {
   if (!s || d < 0 || d >= s->n_dets) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or detector");
   *n = (d + 1 < s->n_dets ? s->h_det_off[d + 1] : s->det_total) - s->h_det_off[d];
@@ -1644,6 +1655,10 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = nullptr;  // (set per launch: launch_one)
   K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
+  {
+    const char* cd = std::getenv("SMCRT_DEBUG_CLAIM_DELAY");
+    K.claim_delay = cd ? (uint32_t)std::strtoul(cd, nullptr, 10) : 0u;
+  }
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
@@ -1657,6 +1672,8 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
     for (int i = 0; i < MAX_SLOTS; ++i)
       if (s->lpending[i]) HIPCHK(hipStreamWaitEvent(stream, s->lev[i], 0));
   }
+  for (int i = 0; i < MAX_SLOTS; ++i)  // launches known to have finished need no more waits
+    if (s->lpending[i] && hipEventQuery(s->lev[i]) == hipSuccess) s->lpending[i] = false;
   for (uint64_t done = 0; done < cfg->n_photons;) {
     refine_rpp(s);
     uint64_t n = cfg->n_photons - done;

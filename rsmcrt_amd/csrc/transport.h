@@ -114,6 +114,9 @@ struct KParams {
   // bucketed deposition (deposit.h): records go straight into per-tile buckets of the pool;
   // bucket_tiles != 0 selects it (and is the tile count), n_buckets is the pool's size
   uint32_t bucket_tiles, n_buckets;
+  // debug knob (SMCRT_DEBUG_CLAIM_DELAY, tests only): s_sleep 127 this many times before a
+  // bucket claim's CAS, so that other waves fill both buckets of the tile and wait (deposit.h)
+  uint32_t claim_delay;
   // exact SDF culling (cull.h), many-top scenes in the COOP instantiation; NULL = off
   const CullGrid* __restrict__ cull;
   // the cooperative EVAL's table of primitives (CTAB_ROWS x 64 doubles, column = top - 1),

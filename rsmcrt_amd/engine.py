@@ -91,6 +91,9 @@ def load_library(path: str = LIB_PATH):
         L.smcrt_multi_scene.restype = C.c_void_p
         L.smcrt_multi_run.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.RunConfig),
                                       C.POINTER(abi.Tallies)]
+        L.smcrt_multi_accumulate.argtypes = [C.c_void_p, C.POINTER(abi.Source), C.POINTER(abi.RunConfig)]
+        L.smcrt_multi_collect.argtypes = [C.c_void_p, C.POINTER(abi.Tallies)]
+        L.smcrt_multi_device_photons.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
         L.smcrt_multi_destroy.argtypes = [C.c_void_p]
         L.smcrt_multi_destroy.restype = None
         if L.smcrt_abi_version() != abi.SMCRT_ABI_VERSION:
@@ -309,8 +312,9 @@ class Comm:
 
 
 class MultiEngine:
-    """One process driving several GPUs (smcrt_multi_*): photon shards per device, one packed
-    RCCL reduce per run. `run` has Engine.run's semantics (without photon records)."""
+    """One process driving several GPUs (smcrt_multi_*): photon chunks handed to whichever
+    device is free, accumulated on the devices, one packed RCCL reduce per `collect`. `run`
+    (= accumulate + collect) has Engine.run's semantics (without photon records)."""
 
     def __init__(self, scene, grid, dets=(), devices=None):
         L = load_library()
@@ -326,6 +330,7 @@ class MultiEngine:
         n = C.c_int32()
         _check(L.smcrt_multi_info(h, C.byref(n)))
         self.n_devices = n.value
+        self._pending = 0  # photons accumulated on the devices, not collected yet
 
     def close(self):
         if getattr(self, "_h", None):
@@ -347,8 +352,30 @@ class MultiEngine:
     def run(self, source, n_photons, seed=123456789, flags=abi.FLAG_PATHLENGTH, first_photon=0,
             result: Result | None = None) -> Result:
         res = result if result is not None else Result(self.grid, self.dets, n_photons)
-        res.n_photons += int(n_photons)
+        res.n_photons += int(n_photons) + self._pending
+        self._pending = 0
         cfg = Engine.config(n_photons, seed, flags, first_photon)
         t = res.tallies()
         _check(load_library().smcrt_multi_run(self._h, C.byref(source), C.byref(cfg), C.byref(t)))
+        return res
+
+    def accumulate(self, source, n_photons, seed=123456789, flags=abi.FLAG_PATHLENGTH, first_photon=0):
+        """Launch photons [first_photon, +n_photons) over the devices; nothing is waited for."""
+        cfg = Engine.config(n_photons, seed, flags, first_photon)
+        _check(load_library().smcrt_multi_accumulate(self._h, C.byref(source), C.byref(cfg)))
+        self._pending += int(n_photons)
+
+    def device_photons(self):
+        """Photons each device ran since the last collect."""
+        out = (C.c_uint64 * self.n_devices)()
+        _check(load_library().smcrt_multi_device_photons(self._h, out))
+        return list(out)
+
+    def collect(self, result: Result | None = None) -> Result:
+        """One packed RCCL reduce of everything accumulated since the last collect."""
+        res = result if result is not None else Result(self.grid, self.dets, 0)
+        res.n_photons += self._pending
+        self._pending = 0
+        t = res.tallies()
+        _check(load_library().smcrt_multi_collect(self._h, C.byref(t)))
         return res

@@ -22,7 +22,8 @@ TYPES = {"smcrt_sdf_node": abi.SdfNode, "smcrt_grid": abi.Grid, "smcrt_source": 
          "smcrt_spectrum": abi.Spectrum,
          "smcrt_detector": abi.Detector, "smcrt_run_config": abi.RunConfig, "smcrt_tallies": abi.Tallies,
          "smcrt_device_tallies": abi.DeviceTallies, "smcrt_kernel_times": abi.KernelTimes,
-         "smcrt_escape_config": abi.EscapeConfig, "smcrt_inverse_config": abi.InverseConfig}
+         "smcrt_escape_config": abi.EscapeConfig, "smcrt_inverse_config": abi.InverseConfig,
+         "smcrt_pack_layout": abi.PackLayout}
 
 
 def _build_module(tmp):
@@ -55,7 +56,8 @@ def test_example_links_against_engine(lib_path, tmp_path):
     subprocess.run([FC, "-O2", "-o", "example", "example_scat_test.f90", "smcrt_mod.o", f"-L{libdir}", "-lsmcrt",
                     f"-Wl,-rpath,{libdir}"], cwd=tmp_path, check=True)
     nm = subprocess.run(["nm", str(tmp_path / "example")], capture_output=True, text=True, check=True).stdout
-    for sym in ("smcrt_scene_create", "smcrt_run", "smcrt_normalise_fluence", "smcrt_scene_destroy"):
+    for sym in ("smcrt_scene_create", "smcrt_run", "smcrt_normalise_fluence", "smcrt_scene_destroy",
+                "smcrt_multi_create", "smcrt_multi_run", "smcrt_multi_destroy"):
         assert re.search(rf"\bU {sym}\b", nm), sym
 
 
@@ -72,6 +74,41 @@ def test_example_reproduces_scat_test_kat(lib_path, tmp_path, kats):
     k = kats["scat_test_nscatt"]
     assert abs(v - k["value"]) <= k["thr"], out
     assert re.search(r"photons = 100000\b", out), out
+
+
+def test_module_binds_every_multi_gpu_entry_point(lib_path, tmp_path):
+    """smcrt_mod declares the multi-GPU and communicator entry points of include/smcrt.h, each
+    bound to a symbol the library exports."""
+    src = open(os.path.join(FDIR, "smcrt_mod.f90")).read()
+    names = set(re.findall(r'bind\(C, name="(smcrt_\w+)"\)', src))
+    want = {"smcrt_multi_create", "smcrt_multi_info", "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_accumulate",
+            "smcrt_multi_collect", "smcrt_multi_device_photons", "smcrt_multi_destroy", "smcrt_comm_unique_id",
+            "smcrt_comm_init_rank", "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_scene_fence",
+            "smcrt_pack_size", "smcrt_pack_host", "smcrt_unpack_host"}
+    assert want <= names, want - names
+    lib = C.CDLL(lib_path)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+@pytest.mark.gpu
+def test_example_multi_gpu_matches_single(lib_path, tmp_path):
+    """run_MCRT's n_gpus path from Fortran: the example through smcrt_multi_run on one device
+    prints the same counters and nscatt as through smcrt_run, bit for bit (jmean to fp64 fold
+    order)."""
+    _build_module(tmp_path)
+    shutil.copy(os.path.join(FDIR, "example_scat_test.f90"), tmp_path)
+    libdir = os.path.dirname(lib_path)
+    subprocess.run([FC, "-O2", "-o", "example", "example_scat_test.f90", "smcrt_mod.o", f"-L{libdir}", "-lsmcrt",
+                    f"-Wl,-rpath,{libdir}"], cwd=tmp_path, check=True)
+    outs = [subprocess.run([str(tmp_path / "example"), "50000", g], capture_output=True, text=True, timeout=300,
+                           check=True).stdout for g in ("0", "1")]
+    def parse(o):
+        ctr = re.findall(r"counter (\d+) = (\d+)", o)
+        return dict(ctr), re.search(r"nscatt =\s*(\S+)", o).group(1), float(re.search(r"jmean normalised\) =\s*(\S+)", o).group(1))
+    (c0, n0, j0), (c1, n1, j1) = parse(outs[0]), parse(outs[1])
+    assert len(c0) == 16 and c0 == c1 and n0 == n1, outs
+    assert abs(j0 - j1) <= 1e-9 * abs(j0)
 
 
 # ---- the conversion glue (bindings/fortran/smcrt_glue.f90, INTEGRATION.md §2.2-2.4) ----------

@@ -664,3 +664,46 @@ def test_reduce_device_tallies_one_rank():
     for x, y in zip((jm, ab, ns, ctr), before):
         assert torch.equal(x, y)
     assert int(ctr[abi.CTR["photons"]]) == 100_000
+
+
+def test_bucket_claim_delayed_waits_stay_exact(monkeypatch):
+    """The bound on the bucket word's 16-bit fill (deposit.h): a debug knob holds every
+    bucket claim open for ~27 us before its CAS (SMCRT_DEBUG_CLAIM_DELAY=8, s_sleep 127 x 8),
+    so under the pencil-beam contention the block's other waves fill both buckets of the tile
+    and their lanes wait for the claim instead of adding without bound. The tallies still
+    equal the oracle's, bit for bit in every counter."""
+    monkeypatch.setenv("SMCRT_DEBUG_CLAIM_DELAY", "8")
+    sc = builders.setup_sphere(0.5, 0.01, 0.9, 1.0, 1.0)
+    src = scene.pencil_source((0.0, 0.0, -0.99), (0.0, 0.0, 1.0))
+    gpu, cpu = both(sc, scene.grid(64, 64, 64, 1, 1, 1), src, 60000)
+    compare(gpu, cpu)
+
+
+def test_multi_accumulate_dynamic_chunks_one_collect(monkeypatch):
+    """The batched multi-GPU path: photons handed to the devices in many small chunks
+    (SMCRT_MULTI_CHUNK) over several smcrt_multi_accumulate calls, overlapped launches
+    requested by the caller (SMCRT_FLAG_OVERLAP is honoured: the collect fences every launch
+    and fold), then ONE smcrt_multi_collect: the result is smcrt_run's over the same photons,
+    counters, absorb and detector bins bit-exact."""
+    from rsmcrt_amd.engine import MultiEngine
+    monkeypatch.setenv("SMCRT_MULTI_CHUNK", "7000")
+    sc = builders.skin_layers()
+    g = scene.grid(64, 64, 64, 0.05, 0.05, 0.05)
+    src = scene.pencil_source((0.0, 0.0, 0.0499), (0.0, 0.0, -1.0))
+    dets = [scene.circle_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.05, 50)]
+    fl = abi.FLAG_PATHLENGTH | abi.FLAG_OVERLAP | abi.FLAG_ASYNC_FOLD
+    with MultiEngine(sc, g, dets) as me:
+        me.accumulate(src, 60_000, seed=SEED, flags=fl, first_photon=5)
+        me.accumulate(src, 40_000, seed=SEED, flags=fl, first_photon=60_005)
+        assert sum(me.device_photons()) == 100_000
+        a = me.collect()
+        assert sum(me.device_photons()) == 0
+        b2 = me.run(src, 10_000, seed=SEED, flags=fl, first_photon=5)  # (accumulators were zeroed)
+    with Engine(sc, g, dets) as eng:
+        b = eng.run(src, 100_000, seed=SEED, first_photon=5)
+        c = eng.run(src, 10_000, seed=SEED, first_photon=5)
+    assert a.n_photons == 100_000
+    assert a.counters_dict() == b.counters_dict() and b2.counters_dict() == c.counters_dict()
+    assert np.array_equal(a.absorb, b.absorb) and np.array_equal(a.det_bins, b.det_bins)
+    np.testing.assert_allclose(a.jmean, b.jmean, rtol=1e-12, atol=1e-300)
+    assert a.nscatt[0] == b.nscatt[0]
