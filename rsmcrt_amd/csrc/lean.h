@@ -1,0 +1,620 @@
+// lean.h — the transport kernel of simple scenes, with the voxel walk decoupled from the photon.
+//
+// Same path as transport_kernel (noBiasPropagation kernelsMod.f90:1901-1976 -> tauint2
+// inttau2.f90:15-364 -> update_grids :367-465), same arithmetic, same results bit for bit,
+// for the scenes the north-star workload is made of: every top-level SDF has the same
+// refractive index (no Fresnel events: reflect_refract is never reached, :248), no detectors,
+// no survival bias, path-length deposition into buckets (deposit.h), the three plain sources.
+//
+// Why a second kernel. In transport_kernel a photon that starts a deposit segment
+// (update_grids) walks it before it may take its next step, and every lane of a wave walks its
+// own segment: a lane with a one-crossing segment idles while its neighbour walks five, and a
+// march step whose segment is longer than one trip's crossings costs another trip (M1: 57
+// segments of 3.5 crossings per photon; the walk was 65 % of the wave's time with 42.5 of 64
+// lanes busy). Here the photon does not wait for the walk:
+//   * a segment is a pure function of (start, direction, length, start cell): update_grids
+//     reads pos, dir and d_sdf and writes only jmean and the packet's cells (:401-445);
+//   * the only results the photon consumes are tflag (the walk left the grid, :437-440), the
+//     error stops (:510-516, :570-573) and the final cells (read by recordWeight at an
+//     absorption, kernelsMod.f90:2202-2220, and by the photon record).
+// So the photon hands the segment to its wave's ring of segments (LDS) and goes on. The
+// wave's lanes then walk segments from the ring, any lane any segment, refilled after every
+// crossing, so the walk runs on nearly full waves and a march step costs one trip.
+//   * A segment that provably stays inside the grid (both ends at least lean_margin from every
+//     grid face, see below) cannot set tflag, so the photon continues at once ("deferred").
+//   * Any other segment is "synchronous": the photon waits for it exactly as before and takes
+//     its tflag, error flags and cells when a walker finishes it.
+//   * The final cells of a deferred segment land in the photon's slot (pcell); a photon that
+//     must record an absorption (or its record) waits until its segments are done and reads
+//     them. Its RNG draw is taken back first, so the draw sequence is unchanged.
+//
+// Why a deferred segment cannot leave the grid: dda_step moves each coordinate either by
+// dir_a * dcell (exact up to rounding) or, on the crossing axis, to face +- delta (1e-8,
+// inttau2.f90:393). A snap puts the walk delta ahead of the straight line along that axis, so
+// after k snaps on axis a the walk is at most k * delta (+ rounding) beyond the line at the
+// same path length, and k <= n_a (the walk is monotonic along each axis). The line between
+// the segment's ends stays inside the box shrunk by lean_margin (convexity), so with
+// lean_margin_a = 2 * delta * (n_a + 2) no snap can reach a boundary face. The remaining
+// error stops need NaNs or an overshoot of one ulp at an exact tie of two wall distances
+// (probability ~1e-16 per crossing); a deferred segment that nevertheless ends in one is
+// counted in dep_ctl[5] ("lean hazards", logged by the host) instead of going unnoticed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "transport.h"
+#include "deposit.h"
+
+namespace smcrt {
+
+#ifndef SMCRT_WAVES_PER_EU_LEAN
+#define SMCRT_WAVES_PER_EU_LEAN 3
+#endif
+// crossing steps per trip of the walk phase (each refills idle walkers from the ring first)
+#ifndef SMCRT_LEAN_STEPS
+#define SMCRT_LEAN_STEPS 3
+#endif
+// crossing steps past SMCRT_LEAN_STEPS while at least SMCRT_LEAN_BUSY walkers are busy
+#ifndef SMCRT_LEAN_EXTRA
+#define SMCRT_LEAN_EXTRA 0
+#endif
+#ifndef SMCRT_LEAN_BUSY
+#define SMCRT_LEAN_BUSY 48
+#endif
+constexpr uint32_t LEAN_SLOTS = 2;               // segments a photon may have in flight
+constexpr uint32_t LEAN_RING = 64 * LEAN_SLOTS;  // ring entries per wave: every slot of every lane
+constexpr int LEAN_CELL_BITS = 20;               // per axis in a packed cell word (cell + 1)
+constexpr uint64_t LEAN_CELL_MASK = (1ull << LEAN_CELL_BITS) - 1;
+constexpr uint64_t LEAN_TFLAG = 1ull << 60, LEAN_FAULT = 1ull << 61;
+
+// Per-block LDS of the lean kernel: the four waves' segment rings (SoA, so consecutive tickets
+// hit consecutive banks), the photons' end-cell slots and busy bits, per-photon fields, and
+// per-wave counters.
+struct LeanShared {
+  double ox[4][LEAN_RING], oy[4][LEAN_RING], oz[4][LEAN_RING];  // start, corner coordinates
+  double dx[4][LEAN_RING], dy[4][LEAN_RING], dz[4][LEAN_RING];  // direction
+  double sl[4][LEAN_RING];                                      // length
+  unsigned long long cw[4][LEAN_RING];                          // start cells (packed)
+  uint32_t meta[4][LEAN_RING];  // owner lane | slot << 6 | synchronous << 7
+  unsigned long long pcell[256][LEAN_SLOTS];  // a finished segment: cells | tflag | fault
+  uint32_t busy[256];                         // bit s: slot s holds a segment in flight
+  uint32_t lu[3][256];                        // interactions, nscatt, status of the photon (LL_*)
+  uint32_t wctr[4][LC_N];                     // per-wave counters
+};
+
+__device__ __forceinline__ unsigned long long lean_pack(int32_t x, int32_t y, int32_t z) {
+  return (unsigned long long)(uint32_t)(x + 1) | ((unsigned long long)(uint32_t)(y + 1) << LEAN_CELL_BITS) |
+         ((unsigned long long)(uint32_t)(z + 1) << (2 * LEAN_CELL_BITS));
+}
+__device__ __forceinline__ int32_t lean_cell(unsigned long long w, int a) {
+  return (int32_t)((w >> (a * LEAN_CELL_BITS)) & LEAN_CELL_MASK) - 1;
+}
+
+// A walker's segment (the fields dda_step uses).
+struct WalkSeg {
+  V3 old;
+  double sd, slen;
+  int32_t xcell, ycell, zcell;
+  uint32_t dda_it;
+  bool seg, tflag, fault;
+};
+
+// The photon (registers). Counters and rare per-photon fields are in LeanShared.
+// A segment request (update_grids entry) is the photon's pos and d at the request, plus the
+// move tauint2 makes right after it (pos + d*dir, pos - d*dir or none): the move is applied
+// when the segment is handed to the ring, so the request costs no registers.
+enum : uint32_t {
+  LF_PEND = 1u,    // an EVAL was requested for the current state
+  LF_TFLAG = 2u,
+  LF_FAULT = 4u,
+  LF_REQ = 8u,     // a segment waits to be handed to the ring
+  LF_WAIT = 16u,   // waiting for a synchronous segment
+  LF_CELLS = 32u,  // xcell/ycell/zcell are the photon's cells
+  LF_MOVE_FWD = 64u, LF_MOVE_BACK = 128u,  // the move after the request
+};
+struct LeanPhoton {
+  V3 pos, dir;
+  Rng rng;
+  double tau, taurun, d, minabs;
+  int32_t layer;
+  int32_t xcell, ycell, zcell;  // valid with LF_CELLS
+  uint32_t hop, loopc, st, seq;  // seq: segments handed out (slot = seq % LEAN_SLOTS)
+  uint32_t f;                    // LF_* flags
+  __device__ __forceinline__ bool has(uint32_t b) const { return (f & b) != 0; }
+  __device__ __forceinline__ void set(uint32_t b) { f |= b; }
+  __device__ __forceinline__ void clr(uint32_t b) { f &= ~b; }
+};
+
+enum : int { LL_INTER = 0, LL_NSCATT, LL_STATUS };  // per-photon fields (LeanShared::lu)
+#define LLU(f) (sh->lu[(f)][threadIdx.x])
+
+// count one event per active lane into the wave's counter c (divergent code is fine)
+__device__ __forceinline__ void lean_count(LeanShared* sh, int c) {
+  const uint64_t m = __ballot(1);
+  if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&sh->wctr[threadIdx.x >> 6][c], (uint32_t)__popcll(m));
+}
+
+template <bool LDS_FACES, int GM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES_PER_EU_LEAN))) void lean_kernel(
+    KParams K, const smcrt_sdf_node* __restrict__ nodes, const ProgOp* __restrict__ prog,
+    const KCold* __restrict__ C) {
+  __shared__ LeanShared shm;
+  LeanShared* sh = &shm;
+  const double eps = 1e-8;  // inttau2.f90:56
+  const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
+  const bool records_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) != 0 && C->records != nullptr;
+  const int lane_id = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+
+  extern __shared__ double sh_dyn[];  // [props | faces] | the block's bucket words
+  const TopProps* props = K.props;
+  const double* xf = K.xface;
+  const double* yf = K.yface;
+  const double* zf = K.zface;
+  int dyn_off = 0;
+  if constexpr (LDS_FACES) {
+    const int np = 4 * K.n_top;
+    const double* gp = (const double*)K.props;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) sh_dyn[i] = gp[i];
+    const int nf = (K.nx + 1) + (K.ny + 1) + (K.nz + 2);
+    double* sh_faces = sh_dyn + np;
+    for (int i = threadIdx.x; i < nf; i += blockDim.x) sh_faces[i] = K.xface[i];
+    props = (const TopProps*)sh_dyn;
+    xf = sh_faces;
+    yf = sh_faces + (K.nx + 1);
+    zf = yf + (K.ny + 1);
+    dyn_off = np + nf;
+  }
+  unsigned long long* const bstate = (unsigned long long*)(sh_dyn + dyn_off);
+  init_buckets(K, C, bstate);
+  for (int c = lane_id; c < LC_N; c += 64) sh->wctr[wv][c] = 0;
+  for (int f = 0; f < 3; ++f) sh->lu[f][threadIdx.x] = 0;
+  sh->busy[threadIdx.x] = 0;
+  __syncthreads();
+
+  // lean_margin (see the header comment), per axis, corner coordinates
+  const double mx = 2.0 * eps * (double)(K.nx + 2), my = 2.0 * eps * (double)(K.ny + 2),
+               mz = 2.0 * eps * (double)(K.nz + 2);
+  const double ex = 2.0 * K.xmax - mx, ey = 2.0 * K.ymax - my, ez = 2.0 * K.zmax - mz;
+
+  LeanPhoton P;
+  P.st = ST_FETCH; P.f = LF_CELLS;
+  P.pos = P.dir = v3(0.0, 0.0, 0.0);
+  P.tau = P.taurun = P.d = P.minabs = 0.0;
+  P.layer = P.xcell = P.ycell = P.zcell = 0;
+  P.hop = P.loopc = P.seq = 0;
+  P.rng.init(0);
+  WalkSeg W;
+  W.old = v3(0.0, 0.0, 0.0);
+  W.sd = W.slen = 0.0;
+  W.xcell = W.ycell = W.zcell = 0;
+  W.dda_it = 0;
+  W.seg = W.tflag = W.fault = false;
+  V3 wdir = v3(0.0, 0.0, 0.0);
+  uint32_t wmeta = 0;
+  uint32_t head = 0, tail = 0;  // the wave's ring tickets (scalar registers)
+  BucketLog WB;
+  WB.next = WB.end = 0;
+  uint32_t overflow = 0, hazards = 0;
+  uint32_t w_dep = 0, w_sdf = 0, w_iters = 0;
+  uint64_t chunk_base = 0;
+  uint32_t chunk_left = 0;
+  bool more = true;  // photons may still come from the queue
+
+  for (;; ++w_iters) {
+    // ---- photon fetch (wave-aggregated work queue), as transport_kernel ----------------
+    {
+      uint64_t need = __ballot(P.st == ST_FETCH);
+      while (need && more) {
+        if (chunk_left == 0) {
+          unsigned long long base = 0;
+          if (lane_id == 0) base = atomicAdd(C->queue, (unsigned long long)SMCRT_FETCH_CHUNK);
+          chunk_base = __shfl(base, 0, 64);
+          const uint64_t n_photons = C->n_photons;
+          chunk_left = (chunk_base < n_photons)
+                           ? (uint32_t)((n_photons - chunk_base) < SMCRT_FETCH_CHUNK ? (n_photons - chunk_base)
+                                                                                       : SMCRT_FETCH_CHUNK)
+                           : 0u;
+          if (chunk_left == 0) { more = false; break; }
+        }
+        const uint32_t n = __popcll(need);
+        const uint32_t take = n < chunk_left ? n : chunk_left;
+        const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
+        if (P.st == ST_FETCH && rank < take) {
+          P.rng.init(C->first_photon + chunk_base + rank);
+          P.st = ST_EMIT;
+        }
+        chunk_base += take;
+        chunk_left -= take;
+        need = __ballot(P.st == ST_FETCH);
+      }
+      if (!more && P.st == ST_FETCH) P.st = ST_IDLE;
+      // done: no photon, no walk in progress, nothing in the ring
+      if (__ballot(P.st != ST_IDLE || W.seg) == 0 && head == tail) break;
+    }
+
+    // ---- EVAL: the SDF array at the photon's query point ---------------------------------
+    const bool have = (P.f & (LF_PEND | LF_REQ | LF_WAIT)) == LF_PEND;
+    EvalOut R;
+    R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
+    if (__ballot(have)) {
+      const bool mask_le = test_kernel && P.st == ST_LAYER;
+      // smallStepPos = pos + d*dir (H1, G0): recomputed, since pos, d and dir are unchanged
+      // since it was formed (no Fresnel in these scenes, so no refraction in between)
+      const V3 q = (P.st == ST_H1 || P.st == ST_G0) ? P.pos + smul(P.d, P.dir) : P.pos;
+      R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, 0, 0);
+      const bool counted = P.st == ST_H0 || P.st == ST_H1 || P.st == ST_H3 || P.st == ST_M1 || P.st == ST_G0;
+      w_sdf += __popcll(__ballot(have && counted)) * (uint32_t)K.n_top;
+      if (have) P.clr(LF_PEND);
+    }
+
+    // ---- P3: consume the EVAL result (transport_kernel's P3 without Fresnel) -------------
+    if (have) {
+      switch (P.st) {
+        case ST_LAYER:  // kernelsMod.f90:1948-1952 (test_kernel: mask ds<=0, :2136)
+          P.layer = R.maxloc;
+          if (P.layer == 0) { P.set(LF_FAULT); P.st = ST_DONE; }
+          else P.st = ST_T2;
+          break;
+        case ST_H0:  // inttau2.f90:63-84, 149-152
+          P.minabs = R.minabs;
+          P.d = R.minabs;
+          P.loopc = 0;
+          if (P.d < eps) {
+            P.d = R.minabs + 2.0 * eps;
+            P.st = ST_H1; P.set(LF_PEND);
+          } else {
+            P.st = (P.taurun >= P.tau || P.has(LF_TFLAG)) ? ST_T2END : ST_M0;
+          }
+          break;
+        case ST_H1: {  // :86-123 (the segment starts at the pre-move pos)
+          const double kap = props[P.layer - 1].kappa;
+          const double t = P.d * kap;
+          if (R.maxloc == P.layer) {
+            if (P.taurun + t < P.tau) { P.set(LF_MOVE_FWD); P.taurun = P.taurun + t; }
+            else { P.d = (P.tau - P.taurun) / kap; P.taurun = P.taurun + t; }
+          } else {
+            if (P.taurun + t < P.tau) { P.set(LF_MOVE_BACK); P.taurun = P.taurun + t; }
+            else { P.d = (P.tau - P.taurun) / kap; P.set(LF_MOVE_BACK); }
+          }
+          P.st = ST_H2;
+          P.set(LF_REQ);
+          break;
+        }
+        case ST_H3:  // :133-152
+          P.minabs = R.minabs;
+          P.d = R.minabs;
+          if (R.minv > 0.0) P.set(LF_TFLAG);
+          P.st = (P.taurun >= P.tau || P.has(LF_TFLAG)) ? ST_T2END : ST_M0;
+          break;
+        case ST_M1:  // :177-191
+          P.minabs = R.minabs;
+          P.d = R.minabs;
+          if (R.minv > 0.0) { P.set(LF_TFLAG); P.st = ST_B0; }
+          else P.st = ST_M0;
+          break;
+        case ST_G0: {  // new layer and the glancing loop, :220-245; equal n: cross, :318-328
+          const int32_t new_layer = R.maxloc;
+          if (new_layer == P.layer && R.minabs < eps) {  // (old_layer == layer here)
+            if (++P.loopc > (uint32_t)MAX_GLANCE_ITERS) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; break; }
+            P.d = P.d + eps;
+            P.set(LF_PEND);
+            break;
+          }
+          if (new_layer == 0) { P.set(LF_TFLAG); P.st = ST_T2END; break; }
+          P.layer = new_layer;
+          P.st = ST_X1;
+          P.set(LF_REQ);
+          break;
+        }
+        default:
+          break;
+      }
+    }
+
+    // ---- P4: a march step, :155-176 ------------------------------------------------------
+    if (!(P.f & (LF_REQ | LF_WAIT)) && P.st == ST_M0) {
+      if (!(P.d >= eps)) {
+        P.st = ST_B0;
+      } else if (++P.loopc > (uint32_t)MAX_MARCH_ITERS) {
+        P.set(LF_FAULT | LF_TFLAG); P.st = ST_B0;
+      } else {
+        const double kap = props[P.layer - 1].kappa;
+        const double t = P.d * kap;
+        if (P.taurun + t < P.tau) {
+          P.taurun = P.taurun + t;
+          P.st = ST_M1; P.set(LF_PEND);
+        } else {
+          P.d = (P.tau - P.taurun) / kap;
+          P.taurun = P.tau;
+          P.st = ST_B0;
+        }
+        P.set(LF_REQ | LF_MOVE_FWD);  // pos += d*dir once the segment from pos is handed out
+      }
+    }
+
+    // ---- hand the new segments to the ring (update_grids entry, :401-415) -----------------
+    if (__ballot(P.has(LF_REQ))) {
+      bool push = false, sync = false;
+      unsigned long long cw = 0;
+      V3 old = v3(0.0, 0.0, 0.0);
+      const uint32_t slot = P.seq % LEAN_SLOTS;
+      if (P.has(LF_REQ) && !(sh->busy[threadIdx.x] & (1u << slot))) {  // (else: retry next trip)
+        lean_count(sh, LC_UPD);
+        old = v3(P.pos.x + K.xmax, P.pos.y + K.ymax, P.pos.z + K.zmax);
+        const int32_t ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x, K.fex),
+                      cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y, K.fey),
+                      ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z, K.fez);
+        // tauint2's move after update_grids (inttau2.f90:98-122, 163-173)
+        if (P.has(LF_MOVE_FWD)) P.pos = P.pos + smul(P.d, P.dir);
+        else if (P.has(LF_MOVE_BACK)) P.pos = P.pos - smul(P.d, P.dir);
+        P.clr(LF_REQ | LF_MOVE_FWD | LF_MOVE_BACK);
+        if (ci == -1 || cj == -1 || ck == -1) {  // outside the grid: tflag, no walk
+          P.set(LF_TFLAG | LF_CELLS);
+          P.xcell = ci; P.ycell = cj; P.zcell = ck;
+        } else {
+          const double len = P.d;
+          const V3 e = v3(old.x + P.dir.x * len, old.y + P.dir.y * len, old.z + P.dir.z * len);
+          const bool inside = old.x >= mx && old.x <= ex && old.y >= my && old.y <= ey && old.z >= mz &&
+                              old.z <= ez && e.x >= mx && e.x <= ex && e.y >= my && e.y <= ey && e.z >= mz &&
+                              e.z <= ez;
+          push = true;
+          sync = !inside;
+          cw = lean_pack(ci, cj, ck);
+        }
+      }
+      const uint64_t pm = __ballot(push);
+      if (pm) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        if (push) {
+          const uint32_t ix = (tail + rank) & (LEAN_RING - 1);
+          sh->ox[wv][ix] = old.x; sh->oy[wv][ix] = old.y; sh->oz[wv][ix] = old.z;
+          sh->dx[wv][ix] = P.dir.x; sh->dy[wv][ix] = P.dir.y; sh->dz[wv][ix] = P.dir.z;
+          sh->sl[wv][ix] = P.d;
+          sh->cw[wv][ix] = cw;
+          sh->meta[wv][ix] = (uint32_t)lane_id | (slot << 6) | (sync ? 128u : 0u);
+          sh->busy[threadIdx.x] |= 1u << slot;
+          P.seq += 1;
+          P.clr(LF_CELLS);
+          if (sync) P.set(LF_WAIT);
+        }
+        tail += (uint32_t)__popcll(pm);
+      }
+    }
+
+    // ---- walk phase: crossings of ring segments on every lane ------------------------------
+    for (int k = 0; k < SMCRT_LEAN_STEPS + SMCRT_LEAN_EXTRA; ++k) {
+      {  // idle walkers take the oldest segments of the ring
+        const uint64_t im = __ballot(!W.seg);
+        const uint32_t avail = tail - head;
+        const uint32_t ni = (uint32_t)__popcll(im);
+        const uint32_t take = ni < avail ? ni : avail;
+        if (take) {
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+          if (!W.seg && rank < take) {
+            const uint32_t ix = (head + rank) & (LEAN_RING - 1);
+            W.old = v3(sh->ox[wv][ix], sh->oy[wv][ix], sh->oz[wv][ix]);
+            wdir = v3(sh->dx[wv][ix], sh->dy[wv][ix], sh->dz[wv][ix]);
+            W.slen = sh->sl[wv][ix];
+            const unsigned long long cw = sh->cw[wv][ix];
+            W.xcell = lean_cell(cw, 0); W.ycell = lean_cell(cw, 1); W.zcell = lean_cell(cw, 2);
+            wmeta = sh->meta[wv][ix];
+            W.sd = 0.0; W.dda_it = 0;
+            W.seg = true; W.tflag = false; W.fault = false;
+          }
+          head += take;
+        }
+      }
+      const uint64_t am = __ballot(W.seg);
+      if (!am) break;
+      if (k >= SMCRT_LEAN_STEPS && __popcll(am) < SMCRT_LEAN_BUSY) break;
+      bool dep = false;
+      uint32_t vox = 0;
+      double val = 0.0;
+      if (W.seg) dda_step<GM>(K, W, wdir, xf, yf, zf, dep, vox, val, 1.0);
+      w_dep += __popcll(__ballot(dep));
+      emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+      // a finished segment: its cells and flags to the owner's slot, then the slot is free
+      if ((am >> lane_id & 1ull) && !W.seg) {
+        const uint32_t owner = (uint32_t)(wv * 64) + (wmeta & 63u), slot = (wmeta >> 6) & 1u;
+        const bool sync = (wmeta & 128u) != 0;
+        if (!sync && (W.tflag || W.fault)) ++hazards;  // cannot happen (header comment)
+        sh->pcell[owner][slot] = lean_pack(W.xcell, W.ycell, W.zcell) | (W.tflag ? LEAN_TFLAG : 0ull) |
+                                 (W.fault ? LEAN_FAULT : 0ull);
+        atomicAnd(&sh->busy[owner], ~(1u << slot));
+      }
+    }
+
+    // ---- P5: a synchronous segment finished; after a segment: next program point ---------
+    if (P.has(LF_WAIT) && !(sh->busy[threadIdx.x] & (1u << ((P.seq - 1) % LEAN_SLOTS)))) {
+      const unsigned long long w = sh->pcell[threadIdx.x][(P.seq - 1) % LEAN_SLOTS];
+      P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
+      P.set(LF_CELLS);
+      if (w & LEAN_TFLAG) P.set(LF_TFLAG);
+      if (w & LEAN_FAULT) P.set(LF_FAULT);
+      P.clr(LF_WAIT);
+    }
+    const bool free_ = !(P.f & (LF_REQ | LF_WAIT));
+    if (free_ && (P.st == ST_H2 || P.st == ST_B0 || P.st == ST_X1)) {
+      if (P.st == ST_X1) {  // :326-335 (pos = smallStepPos)
+        P.taurun = P.taurun + P.d * props[P.layer - 1].kappa;
+        P.pos = P.pos + smul(P.d, P.dir);
+      }
+      if (P.st == ST_H2) {
+        P.st = ST_H3; P.set(LF_PEND);
+      } else if (P.st == ST_X1) {
+        P.st = P.has(LF_TFLAG) ? ST_T2END : ST_H0;
+      } else if (P.taurun >= P.tau || P.has(LF_TFLAG)) {  // B0, :204-207
+        P.st = ST_T2END;
+      } else {  // boundary probe, :213-222 (smallStepPos = pos + d*dir, formed at the EVAL)
+        P.d = P.minabs + 2.0 * eps;
+        P.loopc = 0;
+        P.st = ST_G0; P.set(LF_PEND);
+      }
+    }
+
+    // ---- P6: tauint2 write-back checks, :341-362 -----------------------------------------
+    if (free_ && P.st == ST_T2END) {
+      if (fabs(P.pos.x) > K.xmax) P.set(LF_TFLAG);
+      if (fabs(P.pos.y) > K.ymax) P.set(LF_TFLAG);
+      if (fabs(P.pos.z) > K.zmax) P.set(LF_TFLAG);
+      P.st = ST_INTERACT;
+    }
+    // the final cells of the photon's deferred segments, once they are all done
+    if (!P.has(LF_CELLS) && sh->busy[threadIdx.x] == 0) {
+      const unsigned long long w = sh->pcell[threadIdx.x][(P.seq - 1) % LEAN_SLOTS];
+      P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
+      P.set(LF_CELLS);
+    }
+
+    // ---- P7: photon events, batched as in transport_kernel ---------------------------------
+    {
+      const bool ev = free_ && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
+      const uint64_t evm = __ballot(ev);
+      const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
+      const uint32_t nev = __popcll(evm);
+      if (nev && (nev >= SMCRT_EVENT_LANES || evm == busy)) {
+        if (ev && P.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2126-2170
+          if (P.f & (LF_TFLAG | LF_FAULT)) {
+            P.st = ST_DONE;
+          } else if (LLU(LL_INTER) + 1u > (uint32_t)MAX_INTERACTIONS) {
+            ++LLU(LL_INTER);
+            P.set(LF_FAULT); P.st = ST_DONE;
+          } else {
+            const uint32_t d0 = P.rng.draws;
+            const double c0 = P.rng.cached;
+            const double ran = P.rng.next(K.key0, K.key1);
+            const TopProps pr = props[P.layer - 1];
+            const bool sc = ran < pr.albedo;
+            if (!sc && !test_kernel && !P.has(LF_CELLS)) {
+              // recordWeight needs the cells of a segment still being walked: take the draw
+              // back (the stream is counter-based) and come back once the cells are in
+              P.rng.draws = d0; P.rng.cached = c0;
+            } else {
+              ++LLU(LL_INTER);
+              if (!sc) {
+                P.set(LF_TFLAG); LLU(LL_STATUS) = 1; lean_count(sh, LC_ABSORBED);
+                if (!test_kernel) {  // recordWeight(packet, 1.0)
+                  if (P.xcell < 1 || P.xcell > K.nx || P.ycell < 1 || P.ycell > K.ny || P.zcell < 1 ||
+                      P.zcell > K.nz) P.set(LF_FAULT);
+                  else if (C->absorb) atomic_add_nr(C->absorb + lin(K, P.xcell, P.ycell, P.zcell), 1.0);
+                }
+                P.st = ST_DONE;
+              } else {
+                // scatter, photon.f90:1045-1103
+                Lane L;
+                L.dir = P.dir; L.rng = P.rng; L.fault = false; L.tflag = false;
+                scatter(K, L, pr.hgg);
+                P.dir = L.dir; P.rng = L.rng;
+                if (L.fault) P.set(LF_FAULT | LF_TFLAG);  // (renormalisation runaway)
+                const uint32_t st = ++LLU(LL_NSCATT);
+                lean_count(sh, LC_SCATTERS);
+                if (test_kernel) {
+                  if (st >= 1 && st <= 4) {
+                    double* const moments = C->moments;
+                    if (moments) {
+                      double* m = moments + 3 * (st - 1);
+                      double* m2 = moments + 12 + 3 * (st - 1);
+                      atomic_add_nr(m + 0, P.pos.x); atomic_add_nr(m + 1, P.pos.y); atomic_add_nr(m + 2, P.pos.z);
+                      atomic_add_nr(m2 + 0, P.pos.x * P.pos.x);
+                      atomic_add_nr(m2 + 1, P.pos.y * P.pos.y);
+                      atomic_add_nr(m2 + 2, P.pos.z * P.pos.z);
+                    }
+                  } else if (K.flags & SMCRT_FLAG_END_EARLY) {
+                    P.set(LF_TFLAG);
+                    LLU(LL_STATUS) = 4;
+                  }
+                }
+                P.st = ST_T2;
+              }
+            }
+          }
+        }
+        if (ev && P.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
+          lean_count(sh, LC_TAU);
+          P.tau = -det_log(P.rng.next(K.key0, K.key1));
+          P.taurun = 0.0;
+          P.hop = 0;
+          P.st = ST_H0;  // arrives in P8
+        }
+        if (ev && P.st == ST_EMIT) {  // kernelsMod.f90:1937-1945
+          P.clr(LF_FAULT); P.layer = 0;
+          LLU(LL_STATUS) = 0; LLU(LL_NSCATT) = 0; LLU(LL_INTER) = 0;
+          Lane L;
+          L.rng = P.rng; L.xcell = L.ycell = L.zcell = 0; L.layer = 0; L.tflag = false;
+          emit<GM, false>(K, C, L, 0u);
+          if (!test_kernel) {
+            int64_t tries = 0;
+            while (cell_out(K, L)) {
+              if (++tries > MAX_EMIT_TRIES) { P.set(LF_FAULT); break; }
+              lean_count(sh, LC_RETRIES);
+              emit<GM, false>(K, C, L, 0u);
+            }
+          }
+          P.pos = L.pos; P.dir = L.dir; P.rng = L.rng; P.clr(LF_TFLAG);
+          P.layer = L.layer;
+          P.xcell = L.xcell; P.ycell = L.ycell; P.zcell = L.zcell;
+          P.set(LF_CELLS);
+          if (!test_kernel && !P.has(LF_FAULT) && (K.flags & SMCRT_FLAG_RENDER_SOURCE) && C->emission)
+            atomic_add_nr(C->emission + lin(K, P.xcell, P.ycell, P.zcell), 1.0);
+          if (P.has(LF_FAULT)) P.st = ST_DONE;
+          else { P.st = ST_LAYER; P.set(LF_PEND); }
+        }
+        if (ev && P.st == ST_DONE && (P.has(LF_CELLS) || !records_on)) {  // photon finished
+          if (P.has(LF_FAULT)) { LLU(LL_STATUS) = 3; lean_count(sh, LC_FAULTS); }
+          else if (LLU(LL_STATUS) == 0) { LLU(LL_STATUS) = 2; lean_count(sh, LC_ESCAPED); }
+          lean_count(sh, LC_PHOTONS);
+          atomicAdd(&sh->wctr[wv][LC_DRAWS], P.rng.draws);
+          if (records_on) {
+            const uint64_t pid = ((uint64_t)P.rng.pid_hi << 32) | P.rng.pid_lo;
+            smcrt_photon_record* r = C->records + (pid - C->first_photon);
+            r->pos[0] = P.pos.x; r->pos[1] = P.pos.y; r->pos[2] = P.pos.z;
+            r->dir[0] = P.dir.x; r->dir[1] = P.dir.y; r->dir[2] = P.dir.z;
+            r->weight = 1.0;
+            r->cell[0] = P.xcell; r->cell[1] = P.ycell; r->cell[2] = P.zcell;
+            r->layer = P.layer;
+            r->nscatt = LLU(LL_NSCATT);
+            r->bounces = 0;
+            r->draws = P.rng.draws;
+            r->status = LLU(LL_STATUS);
+          }
+          P.clr(LF_TFLAG | LF_FAULT);
+          P.st = ST_FETCH;
+        }
+      }
+    }
+
+    // ---- P8: arrive at the hop-loop head, :61 --------------------------------------------
+    if (!(P.f & (LF_REQ | LF_WAIT | LF_PEND)) && P.st == ST_H0) {
+      if (!(P.taurun <= P.tau)) P.st = ST_T2END;
+      else if (++P.hop > (uint32_t)MAX_HOP_ITERS) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; }
+      else P.set(LF_PEND);
+    }
+  }
+
+  close_buckets(K, C, WB, w_dep - overflow, overflow);
+  __syncthreads();  // every wave of the block is done depositing
+  close_block_buckets(K, C, bstate);
+
+  // ---- per-wave counters ---------------------------------------------------------------
+  unsigned long long* const counters = C->counters;
+  const uint32_t hz = wave_sum_u32(hazards);
+  if (lane_id == 0) {
+    if (hz) atomicAdd(C->dep_ctl + 5, hz);
+    if (counters) {
+      const uint32_t* c = sh->wctr[wv];
+      const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
+                                           w_dep,         c[LC_UPD],     c[LC_TAU],      0u,             0u,
+                                           0u,            c[LC_FAULTS],  c[LC_DRAWS],    0u,             c[LC_ESCAPED],
+                                           w_iters};
+      for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
+        if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
+    }
+    double* const nscatt = C->nscatt;
+    if (nscatt && sh->wctr[wv][LC_SCATTERS]) atomic_add_nr(nscatt, (double)sh->wctr[wv][LC_SCATTERS]);
+  }
+}
+
+#undef LLU
+
+}  // namespace smcrt

@@ -37,6 +37,8 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+#include "lean.h"
+
 // The query point of each EVAL state (the exact expressions of the reference).
 __device__ __forceinline__ V3 eval_query(const Lane& L) {
   switch (L.st) {
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
             bool dep = false;
             uint32_t vox = 0;
             double val = 0.0;
-            if (lane_id == ow) dda_step<GM>(K, L, xf, yf, zf, dep, vox, val);
+            if (lane_id == ow) dda_step<GM>(K, L, L.dir, xf, yf, zf, dep, vox, val, L.weight);
             w_dep += __popcll(__ballot(dep));
             if (binned) {
               if (K.bucket_tiles) emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
@@ -534,7 +536,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
         bool dep = false;
         uint32_t vox = 0;
         double val = 0.0;
-        if (L.seg) dda_step<GM>(K, L, xf, yf, zf, dep, vox, val);
+        if (L.seg) dda_step<GM>(K, L, L.dir, xf, yf, zf, dep, vox, val, L.weight);
         w_dep += __popcll(__ballot(dep));
 #ifdef SMCRT_ABL_NO_EMIT  // timing ablation only: deposits are computed but dropped
         if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, C, W, dep, vox, val, overflow, whist); }
@@ -868,6 +870,11 @@ struct smcrt_scene {
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
   int grid_blocks_x = 0;  // the XSRC (general emitter) instantiation
+  int grid_blocks_lean = 0;  // lean_kernel (lean.h)
+  // lean_kernel serves this scene: equal refractive indices, no detectors, a few tops, bucketed
+  // deposition, axes below 2^20 cells (SMCRT_LEAN=0 keeps transport_kernel)
+  bool lean_ok = false;
+  uint64_t lean_hazards = 0;
   // source spectrum tables of the last general-emitter run (srcplan.h), device copy
   std::vector<double> h_spec;
   double* d_spec = nullptr;
@@ -958,6 +965,18 @@ static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
                                            {TK(true, 0), TK(true, 1), TK(true, 2)}};
 #undef TK
   return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : (s->coop_lanes > 0 ? 2 : 0)];
+}
+
+// lean_kernel (lean.h) of this scene's face staging and grid mode
+static const void* lean_fn(const smcrt_scene* s) {
+  static const void* const fns[2][3] = {
+      {(const void*)lean_kernel<false, 0>, (const void*)lean_kernel<false, 1>, (const void*)lean_kernel<false, 2>},
+      {(const void*)lean_kernel<true, 0>, (const void*)lean_kernel<true, 1>, (const void*)lean_kernel<true, 2>}};
+  return fns[s->lds_faces ? 1 : 0][s->grid_mode];
+}
+// its dynamic LDS: staged props + faces, then the block's bucket words
+static size_t lean_lds(const smcrt_scene* s) {
+  return (s->lds_faces ? s->face_bytes : 0) + (size_t)2 * s->n_tiles * sizeof(uint32_t);
 }
 
 // Dynamic LDS of the transport kernel: staged props + faces, detector start points, then the
@@ -1223,7 +1242,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
       if ((st = dalloc(&s->d_tile_count, s->n_tiles)) || (st = dalloc(&s->d_tile_start, s->n_tiles)))
         return cleanup_fail(st);
       for (int i = 0; i < MAX_SLOTS; ++i)
-        if ((st = dalloc(&s->d_dep_ctl[i], 4)) || (st = dalloc(&s->d_bin_counts[i], (size_t)s->n_tiles * BIN_BLOCKS)))
+        if ((st = dalloc(&s->d_dep_ctl[i], 8)) || (st = dalloc(&s->d_bin_counts[i], (size_t)s->n_tiles * BIN_BLOCKS)))
           return cleanup_fail(st);
       s->scatter_lds = scatter_lds_bytes(s->n_tiles);
       if (hipFuncSetAttribute((const void*)bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1264,7 +1283,20 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     }
     s->grid_mode = f2 ? 2 : (p2 ? 1 : 0);
   }
+  {  // lean_kernel (lean.h): scenes without Fresnel events or detectors, a few tops
+    bool ok = n_dets == 0 && s->bucketed && s->coop_lanes == 0 && grid->nx < (1 << 20) - 2 &&
+              grid->ny < (1 << 20) - 2 && grid->nz < (1 << 20) - 2;
+    for (int32_t i = 1; ok && i < n_top; ++i) ok = s->h_props[i].n == s->h_props[0].n;
+    ok = ok && lean_lds(s) + sizeof(LeanShared) <= 65536;
+    const char* le = std::getenv("SMCRT_LEAN");
+    s->lean_ok = ok && !(le && std::string(le) == "0");
+  }
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+  if (s->lean_ok) {
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lean_fn(s), 256, lean_lds(s));
+    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
+    s->grid_blocks_lean = cus * per_cu;
+  }
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
     hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, dep_words(s), x == 1));
@@ -1347,6 +1379,11 @@ static void refine_rpp(smcrt_scene* s) {
       if (pool_log)
         std::fprintf(stderr, "[pool] slot %d: %u photons, %u records, %u overflowed, %u of %llu chunks\n", sl, h[4],
                      h[3], h[1], h[0], (unsigned long long)s->pool_chunks);
+      if (h[5]) {  // lean kernel: a deferred segment ended in tflag/fault (lean.h; never expected)
+        s->lean_hazards += h[5];
+        std::fprintf(stderr, "[smcrt] lean kernel: %u deferred voxel walks ended in an error stop or left the grid "
+                     "(parity not guaranteed for those photons)\n", h[5]);
+      }
       if (h[4] > 0) {
         const double rpp = (double)(h[3] + h[1]) / (double)h[4];
         s->rpp_est = std::max(1.0, rpp);
@@ -1459,7 +1496,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   KCold* C = s->d_cold + (size_t)qi * COLD_PER_STREAM + (s->cold_seq[qi]++ % COLD_PER_STREAM);
   HIPCHK(hipMemcpyAsync(C, &Ch, sizeof(KCold), hipMemcpyHostToDevice, stream));
   if (binned) {
-    HIPCHK(hipMemsetAsync(s->d_dep_ctl[sl], 0, 4 * sizeof(uint32_t), stream));
+    HIPCHK(hipMemsetAsync(s->d_dep_ctl[sl], 0, 8 * sizeof(uint32_t), stream));
     if (K.bucket_tiles)  // per-tile bucket counts
       HIPCHK(hipMemsetAsync(s->d_bin_counts[sl], 0, (size_t)s->n_tiles * sizeof(uint32_t), stream));
     else if (K.hist_tiles)
@@ -1479,9 +1516,20 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   }
   const uint64_t waves_needed = (Ch.n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
-  const int blocks = (int)std::min<uint64_t>((uint64_t)(xsrc ? s->grid_blocks_x : s->grid_blocks),
-                                             std::max<uint64_t>(1, blocks_needed));
-  {
+  // lean_kernel (lean.h) when the scene and the run qualify: bucketed path-length deposition,
+  // unit weights (no survival bias), a plain source
+  const bool lean = !xsrc && s->lean_ok && K.bucket_tiles && (K.flags & SMCRT_FLAG_PATHLENGTH) &&
+                    !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS);
+  const int blocks = (int)std::min<uint64_t>(
+      (uint64_t)(lean ? s->grid_blocks_lean : (xsrc ? s->grid_blocks_x : s->grid_blocks)),
+      std::max<uint64_t>(1, blocks_needed));
+  if (lean) {
+    const KCold* Cc = C;
+    const smcrt_sdf_node* a_nodes = K.nodes;
+    const ProgOp* a_prog = K.prog;
+    void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&Cc};
+    HIPCHK(hipLaunchKernel(lean_fn(s), dim3(blocks), dim3(256), args, lean_lds(s), stream));
+  } else {
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;
     const ProgOp* a_prog = K.prog;
@@ -1523,6 +1571,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     HIPCHK(hipGetLastError());
     // remember how many records this launch produced (read back lazily, never waited for)
     HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl, s->d_dep_ctl[sl], 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
+    HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl + 5, s->d_dep_ctl[sl] + 5, sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
     HIPCHK(hipEventRecord(s->ctl_ev[sl], fs));
     s->ctl_pending[sl] = true;
     if (ev) HIPCHK(hipEventRecord(ev[3], fs));

@@ -745,15 +745,16 @@ __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneSha
 }
 
 // One voxel crossing of the pending segment: wall_dist + deposit + update_pos
-// (inttau2.f90:417-441, 467-584). Clears L.seg when the segment ends.
-template <int GM>
-__device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double* __restrict__ xf,
+// (inttau2.f90:417-441, 467-584). Clears L.seg when the segment ends. `L` is any state with
+// the segment fields of Lane (old, sd, slen, xcell/ycell/zcell, dda_it, seg, tflag, fault):
+// the photon's own Lane, or a walker's segment (lean.h); `dir` is the segment's direction.
+template <int GM, class S>
+__device__ __forceinline__ void dda_step(const KParams& K, S& L, const V3 dir, const double* __restrict__ xf,
                                          const double* __restrict__ yf, const double* __restrict__ zf,
-                                         bool& dep, uint32_t& dep_vox, double& dep_val) {
+                                         bool& dep, uint32_t& dep_vox, double& dep_val, double weight) {
 #ifdef SMCRT_ASM_MARKERS
   asm volatile("; @@DDA_BEGIN");
 #endif
-  const V3 dir = L.dir;
   const bool capped = ++L.dda_it > (uint32_t)MAX_DDA_ITERS;  // runaway guard: fault
   // wall_dist, :467-521: d_a = (face_a - old_a)/dir_a, dcell = min, ldir_a = (dcell == d_a).
   // Only the smallest quotient is needed exactly: the three are ranked by products with
@@ -815,7 +816,7 @@ __device__ __forceinline__ void dda_step(const KParams& K, Lane& L, const double
   // which appends a deposit record (binned path) or adds it atomically
   dep = ok;
   dep_vox = lin(K, L.xcell, L.ycell, L.zcell);
-  dep_val = (double)(float)dc * L.weight;
+  dep_val = (double)(float)dc * weight;
   // update_pos (:524-584): .false. (last step) advances all three coordinates by dc;
   // .true. snaps the first axis with ldir set to its wall +- delta (unchanged if its
   // direction is 0) and advances the other two.
