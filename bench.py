@@ -246,10 +246,11 @@ def reference_pinned(device):
         depths, fit = refval.ri_fit(kats, which)
         sim = refval.to_reference_units(sums, d.n_photons, dz)
         sig = refval.to_reference_units(np.sqrt(np.maximum(sums, 1.0)), d.n_photons, dz)
-        ok, rep = refval.compare_profile(sim, fit, depths, sig)
+        ok, rep = refval.compare_profile(sim, fit, depths, sig, refval.model_term(which))
         out[f"{which}_absorb_depth_vs_fit"] = {"photons": d.n_photons, "rel_rms": rep["rel_rms"],
                                                "integral_ratio": rep["integral_ratio"], "bins": rep["bins"],
-                                               "bins_outside_4sigma_plus_5pct": len(rep["failed"]), "pass": ok}
+                                               "model_term": refval.model_term(which),
+                                               "bins_outside_4sigma_plus_model": len(rep["failed"]), "pass": ok}
     j = Job(os.path.join(ROOT, "tests", "golden", "res", "validateFibreDect.toml"))
     d = j.desc
     g = S.grid(20, 20, 20, d.grid.xmax, d.grid.ymax, d.grid.zmax)

@@ -45,6 +45,11 @@
 #include "transport.h"
 #include "deposit.h"
 
+#ifdef SMCRT_DIAG
+extern __device__ unsigned long long g_diag[72];  // (defined in smcrt.hip)
+extern __device__ unsigned long long g_diag_t[9];
+#endif
+
 namespace smcrt {
 
 #ifndef SMCRT_WAVES_PER_EU_LEAN
@@ -134,6 +139,24 @@ __device__ __forceinline__ void lean_count(LeanShared* sh, int c) {
   if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&sh->wctr[threadIdx.x >> 6][c], (uint32_t)__popcll(m));
 }
 
+#ifdef SMCRT_DIAG
+// Diagnostic builds (-DSMCRT_DIAG): wave-uniform tallies of the lean kernel's schedule, added to
+// g_diag[0..15] at the end of each wave (the host prints them per launch), and the s_memtime
+// share of each phase in g_diag_t[1..8].
+enum : int { LD_TRIPS = 0, LD_WSTEPS, LD_WLANES, LD_PUSH, LD_SYNC, LD_BLOCKED, LD_EVALS, LD_ELANES, LD_P7,
+             LD_REVERT, LD_WAITING, LD_IDLE, LD_RING, LD_EVWAIT, LD_BUSY, LD_N };
+#define LDIAG(i, v) (ld[(i)] += (uint64_t)(v))
+#define LDIAG_T(i)                                                  \
+  do {                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();     \
+    lt[(i)] += t_ - lt_last;                                        \
+    lt_last = t_;                                                   \
+  } while (0)
+#else
+#define LDIAG(i, v) do {} while (0)
+#define LDIAG_T(i) do {} while (0)
+#endif
+
 template <bool LDS_FACES, int GM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES_PER_EU_LEAN))) void lean_kernel(
     KParams K, const smcrt_sdf_node* __restrict__ nodes, const ProgOp* __restrict__ prog,
@@ -201,7 +224,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   uint32_t chunk_left = 0;
   bool more = true;  // photons may still come from the queue
 
+#ifdef SMCRT_DIAG
+  uint64_t ld[LD_N] = {};
+  unsigned long long lt[9] = {};
+  unsigned long long lt_last = __builtin_amdgcn_s_memtime();
+#endif
   for (;; ++w_iters) {
+    LDIAG_T(8);
+    LDIAG(LD_TRIPS, 1);
     // ---- photon fetch (wave-aggregated work queue), as transport_kernel ----------------
     {
       uint64_t need = __ballot(P.st == ST_FETCH);
@@ -233,6 +263,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if (__ballot(P.st != ST_IDLE || W.seg) == 0 && head == tail) break;
     }
 
+    LDIAG(LD_WAITING, __popcll(__ballot(P.has(LF_WAIT))));
+    LDIAG(LD_IDLE, __popcll(__ballot(P.st == ST_IDLE)));
+    LDIAG(LD_BUSY, __popcll(__ballot(P.st != ST_IDLE)));
+    LDIAG_T(1);
     // ---- EVAL: the SDF array at the photon's query point ---------------------------------
     const bool have = (P.f & (LF_PEND | LF_REQ | LF_WAIT)) == LF_PEND;
     EvalOut R;
@@ -248,6 +282,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if (have) P.clr(LF_PEND);
     }
 
+    LDIAG(LD_EVALS, __ballot(have) ? 1 : 0);
+    LDIAG(LD_ELANES, __popcll(__ballot(have)));
+    LDIAG_T(2);
     // ---- P3: consume the EVAL result (transport_kernel's P3 without Fresnel) -------------
     if (have) {
       switch (P.st) {
@@ -333,6 +370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    LDIAG_T(3);
     // ---- hand the new segments to the ring (update_grids entry, :401-415) -----------------
     if (__ballot(P.has(LF_REQ))) {
       bool push = false, sync = false;
@@ -364,6 +402,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
         }
       }
       const uint64_t pm = __ballot(push);
+      LDIAG(LD_PUSH, __popcll(pm));
+      LDIAG(LD_SYNC, __popcll(__ballot(push && sync)));
+      LDIAG(LD_BLOCKED, __popcll(__ballot(P.has(LF_REQ))));
       if (pm) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
         if (push) {
@@ -382,6 +423,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    LDIAG(LD_RING, tail - head);
+    LDIAG_T(4);
     // ---- walk phase: crossings of ring segments on every lane ------------------------------
     for (int k = 0; k < SMCRT_LEAN_STEPS + SMCRT_LEAN_EXTRA; ++k) {
       {  // idle walkers take the oldest segments of the ring
@@ -408,6 +451,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       const uint64_t am = __ballot(W.seg);
       if (!am) break;
       if (k >= SMCRT_LEAN_STEPS && __popcll(am) < SMCRT_LEAN_BUSY) break;
+      LDIAG(LD_WSTEPS, 1);
+      LDIAG(LD_WLANES, __popcll(am));
       bool dep = false;
       uint32_t vox = 0;
       double val = 0.0;
@@ -425,6 +470,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    LDIAG_T(5);
     // ---- P5: a synchronous segment finished; after a segment: next program point ---------
     if (P.has(LF_WAIT) && !(sh->busy[threadIdx.x] & (1u << ((P.seq - 1) % LEAN_SLOTS)))) {
       const unsigned long long w = sh->pcell[threadIdx.x][(P.seq - 1) % LEAN_SLOTS];
@@ -467,13 +513,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       P.set(LF_CELLS);
     }
 
+    LDIAG_T(6);
     // ---- P7: photon events, batched as in transport_kernel ---------------------------------
     {
       const bool ev = free_ && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
       const uint64_t evm = __ballot(ev);
       const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
       const uint32_t nev = __popcll(evm);
-      if (nev && (nev >= SMCRT_EVENT_LANES || evm == busy)) {
+      const bool run_ev = nev && (nev >= SMCRT_EVENT_LANES || evm == busy);
+      LDIAG(LD_P7, run_ev ? 1 : 0);
+      LDIAG(LD_EVWAIT, run_ev ? 0 : nev);
+      if (run_ev) {
         if (ev && P.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2126-2170
           if (P.f & (LF_TFLAG | LF_FAULT)) {
             P.st = ST_DONE;
@@ -487,6 +537,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
             const TopProps pr = props[P.layer - 1];
             const bool sc = ran < pr.albedo;
             if (!sc && !test_kernel && !P.has(LF_CELLS)) {
+#ifdef SMCRT_DIAG
+              atomicAdd(&::g_diag[LD_REVERT], 1ull);
+#endif
               // recordWeight needs the cells of a segment still being walked: take the draw
               // back (the stream is counter-based) and come back once the cells are in
               P.rng.draws = d0; P.rng.cached = c0;
@@ -584,6 +637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    LDIAG_T(7);
     // ---- P8: arrive at the hop-loop head, :61 --------------------------------------------
     if (!(P.f & (LF_REQ | LF_WAIT | LF_PEND)) && P.st == ST_H0) {
       if (!(P.taurun <= P.tau)) P.st = ST_T2END;
@@ -592,6 +646,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     }
   }
 
+#ifdef SMCRT_DIAG
+  if (lane_id == 0) {
+    for (int i = 0; i < LD_N; ++i)
+      if (i != LD_REVERT && ld[i]) atomicAdd(&::g_diag[i], (unsigned long long)ld[i]);
+    for (int i = 1; i < 9; ++i) atomicAdd(&::g_diag_t[i], lt[i]);
+  }
+#endif
   close_buckets(K, C, WB, w_dep - overflow, overflow);
   __syncthreads();  // every wave of the block is done depositing
   close_block_buckets(K, C, bstate);

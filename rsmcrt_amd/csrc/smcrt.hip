@@ -1587,6 +1587,15 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     unsigned long long h[72];
     HIPCHK(hipStreamSynchronize(stream));
     HIPCHK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)));
+    if (lean) {  // lean_kernel's tallies (lean.h LD_*)
+      const double tr = (double)std::max(1ull, h[0]);
+      std::fprintf(stderr, "[diag-lean] wave trips %llu | walk steps/trip %.3f, busy walkers/step %.1f | pushes/trip %.2f"
+                   " (sync %.3f), blocked req/trip %.2f | EVAL phases/trip %.3f lanes/EVAL %.1f | P7 runs/trip %.3f,"
+                   " event lanes waiting/trip %.2f, reverts %llu | lanes waiting sync/trip %.2f, idle %.2f, busy %.2f |"
+                   " ring fill %.1f\n", h[0], h[1] / tr, (double)h[2] / std::max(1ull, h[1]), h[3] / tr, h[4] / tr,
+                   h[5] / tr, h[6] / tr, (double)h[7] / std::max(1ull, h[6]), h[8] / tr, h[13] / tr, h[9], h[10] / tr,
+                   h[11] / tr, h[14] / tr, h[12] / tr);
+    }
     unsigned long long lt = 0;
     for (int i = 0; i < 64; ++i) lt += h[i];
     std::fprintf(stderr, "[diag] waves %llu, longest wave %llu trips %llu ticks\n", h[70], h[68], h[69]);
@@ -1601,7 +1610,9 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     HIPCHK(hipMemcpyFromSymbol(ht, HIP_SYMBOL(g_diag_t), sizeof(ht)));
     double tt = 0;
     for (int i = 1; i < 9; ++i) tt += (double)ht[i];
-    const char* nm[9] = {"", "fetch", "eval", "p3", "p4", "dda", "p5p6", "p7", "p8"};
+    const char* nm_t[9] = {"", "fetch", "eval", "p3", "p4", "dda", "p5p6", "p7", "p8"};
+    const char* nm_l[9] = {"", "fetch", "eval", "p3p4", "push", "walk", "p5p6", "p7", "p8"};
+    const char* const* nm = lean ? nm_l : nm_t;
     std::fprintf(stderr, "[diag-time]");
     for (int i = 1; i < 9; ++i) std::fprintf(stderr, " %s=%.3f", nm[i], (double)ht[i] / tt);
     std::fprintf(stderr, "\n");

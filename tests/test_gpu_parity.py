@@ -188,7 +188,10 @@ def test_point_source_symmetry():
     octs = [j[a:a + 32, b:b + 32, c:c + 32].sum() for a in (0, 32) for b in (0, 32) for c in (0, 32)]
     octs = np.array(octs)
     assert np.all(np.abs(octs / octs.mean() - 1.0) < 0.01)
-    assert abs(j.sum() / n - 6.0) < 0.1  # ~6 cm path per photon (Survey §6 probe: 6.01-6.05)
+    # Path per photon ~6 cm: a value the survey measured by running the reference's own code
+    # (SURVEY §8(d) "[probe]": 6.05 cm/photon at 128^3), not a value the reference holds, so a
+    # loose sanity bound only; the reference-held checks are tests/test_reference_targets.py.
+    assert abs(j.sum() / n - 6.0) < 0.1
 
 
 @pytest.mark.parametrize("env", [{}, {"SMCRT_DEPOSIT": "sorted"}, {"SMCRT_FUSED_HIST": "0"},

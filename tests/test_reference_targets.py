@@ -12,9 +12,11 @@ Targets (data in tests/golden/reference_kats.json, restated in tests/refval.py):
 
 Tolerances (stated here, derived in DESIGN.md §3.4):
 * profile: every 0.02-cm bin of the plotted range with fit >= 1 % of the peak satisfies
-  |sim - fit| <= 4 sigma_MC + 5 % fit, sigma_MC the Monte Carlo standard error of the bin
-  (Poisson counts; on the GPU also the spread of three seeds, whichever is larger); and the
-  integral over the range is within 2 % (+4 sigma) of the fit's;
+  |sim - fit| <= 4 sigma_MC + m * fit, sigma_MC the Monte Carlo standard error of the bin
+  (Poisson counts; on the GPU also the spread of three seeds, whichever is larger) and m the
+  fit's own inaccuracy measured per target from 8e6 photons (tests/golden/ri_model_residual.json:
+  validation2 3.5 %, validation3 2.0 %); and the integral over the range is within 2 %
+  (+4 sigma) of the fit's;
 * fibre: |efficiency - expected| <= 4 sqrt(p (1 - p) / N) for each of the 10 detectors.
 """
 import os
@@ -52,7 +54,7 @@ def _profile_ok(kats, which, sums, n, dz, extra_sigma=None):
     sig = refval.to_reference_units(np.sqrt(np.maximum(sums, 1.0)), n, dz)
     if extra_sigma is not None:
         sig = np.maximum(sig, extra_sigma)
-    ok, rep = refval.compare_profile(sim, fit, depths, sig)
+    ok, rep = refval.compare_profile(sim, fit, depths, sig, refval.model_term(which))
     m = refval.plotted_range(depths)
     integral_sigma = float(np.sqrt(np.sum(sig[m] ** 2)) / fit[m].sum())
     ok_int = abs(rep["integral_ratio"] - 1.0) <= 0.02 + 4.0 * integral_sigma
