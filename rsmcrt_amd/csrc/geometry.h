@@ -69,7 +69,17 @@ __host__ __device__ __forceinline__ double sdf_prim_s(int32_t kind, const double
       return sqrt(p.x * p.x + p.y * p.y + p.z * p.z) - P(0);
     case SMCRT_SDF_BOX: {  // :510-525
       const V3 q = vabs(p) - v3(P(0), P(1), P(2));
-      return len(v3(dmax(q.x, 0.0), dmax(q.y, 0.0), dmax(q.z, 0.0))) + dmin(dmax(q.x, dmax(q.y, q.z)), 0.0);
+      const double mx = dmax(q.x, 0.0), my = dmax(q.y, 0.0), mz = dmax(q.z, 0.0);
+      const double s2 = mx * mx + my * my + mz * mz;  // len(max(q, 0)) = sqrt(s2)
+      double l = 0.0;
+#ifdef __HIP_DEVICE_COMPILE__
+      // a point inside the box has s2 = +0 and sqrt(+0) = +0: the (costly) fp64 square root
+      // is skipped when no lane of the wave needs it, with the same bits
+      if (__ballot(s2 != 0.0)) l = sqrt(s2);
+#else
+      l = sqrt(s2);
+#endif
+      return l + dmin(dmax(q.x, dmax(q.y, q.z)), 0.0);
     }
     case SMCRT_SDF_TORUS: {  // :527-542
       const V3 q = v3(len(v3(p.x, 0.0, p.z)) - P(0), p.y, 0.0);

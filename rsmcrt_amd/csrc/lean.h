@@ -66,8 +66,18 @@ namespace smcrt {
 #ifndef SMCRT_LEAN_BUSY
 #define SMCRT_LEAN_BUSY 48
 #endif
-constexpr uint32_t LEAN_SLOTS = 2;               // segments a photon may have in flight
-constexpr uint32_t LEAN_RING = 64 * LEAN_SLOTS;  // ring entries per wave: every slot of every lane
+constexpr uint32_t ST_ABSORB = 40;  // absorbed; recordWeight waits for the photon's cells
+#ifndef SMCRT_LEAN_SLOTS
+#define SMCRT_LEAN_SLOTS 3
+#endif
+constexpr uint32_t LEAN_SLOTS = SMCRT_LEAN_SLOTS;  // segments a photon may have in flight (<= 4)
+// Ring entries per wave. Idle walkers refill from the ring at the end of every walk phase, so
+// when segments are handed out, either the ring is empty or all 64 walkers hold one: the ring
+// then holds at most 64 * LEAN_SLOTS - 64 segments (every slot of every lane, minus those the
+// walkers hold), and never more than 64 right after an empty ring.
+constexpr uint32_t LEAN_RING = 64 * (LEAN_SLOTS - 1);
+static_assert(LEAN_SLOTS >= 2 && LEAN_SLOTS <= 4 && (LEAN_RING & (LEAN_RING - 1)) == 0,
+              "the ring index wraps with a mask");
 constexpr int LEAN_CELL_BITS = 20;               // per axis in a packed cell word (cell + 1)
 constexpr uint64_t LEAN_CELL_MASK = (1ull << LEAN_CELL_BITS) - 1;
 constexpr uint64_t LEAN_TFLAG = 1ull << 60, LEAN_FAULT = 1ull << 61;
@@ -80,7 +90,7 @@ struct LeanShared {
   double dx[4][LEAN_RING], dy[4][LEAN_RING], dz[4][LEAN_RING];  // direction
   double sl[4][LEAN_RING];                                      // length
   unsigned long long cw[4][LEAN_RING];                          // start cells (packed)
-  uint32_t meta[4][LEAN_RING];  // owner lane | slot << 6 | synchronous << 7
+  uint32_t meta[4][LEAN_RING];  // owner lane | slot << 6 | synchronous << 8
   unsigned long long pcell[256][LEAN_SLOTS];  // a finished segment: cells | tflag | fault
   uint32_t busy[256];                         // bit s: slot s holds a segment in flight
   uint32_t lu[3][256];                        // interactions, nscatt, status of the photon (LL_*)
@@ -123,7 +133,7 @@ struct LeanPhoton {
   double tau, taurun, d, minabs;
   int32_t layer;
   int32_t xcell, ycell, zcell;  // valid with LF_CELLS
-  uint32_t hop, loopc, st, seq;  // seq: segments handed out (slot = seq % LEAN_SLOTS)
+  uint32_t hop, loopc, st, seq;  // seq: the slot of the next segment (0 .. LEAN_SLOTS-1)
   uint32_t f;                    // LF_* flags
   __device__ __forceinline__ bool has(uint32_t b) const { return (f & b) != 0; }
   __device__ __forceinline__ void set(uint32_t b) { f |= b; }
@@ -376,7 +386,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       bool push = false, sync = false;
       unsigned long long cw = 0;
       V3 old = v3(0.0, 0.0, 0.0);
-      const uint32_t slot = P.seq % LEAN_SLOTS;
+      const uint32_t slot = P.seq;
       if (P.has(LF_REQ) && !(sh->busy[threadIdx.x] & (1u << slot))) {  // (else: retry next trip)
         lean_count(sh, LC_UPD);
         old = v3(P.pos.x + K.xmax, P.pos.y + K.ymax, P.pos.z + K.zmax);
@@ -413,9 +423,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           sh->dx[wv][ix] = P.dir.x; sh->dy[wv][ix] = P.dir.y; sh->dz[wv][ix] = P.dir.z;
           sh->sl[wv][ix] = P.d;
           sh->cw[wv][ix] = cw;
-          sh->meta[wv][ix] = (uint32_t)lane_id | (slot << 6) | (sync ? 128u : 0u);
-          sh->busy[threadIdx.x] |= 1u << slot;
-          P.seq += 1;
+          sh->meta[wv][ix] = (uint32_t)lane_id | (slot << 6) | (sync ? 256u : 0u);
+          atomicOr(&sh->busy[threadIdx.x], 1u << slot);
+          P.seq = P.seq + 1 == LEAN_SLOTS ? 0u : P.seq + 1;
           P.clr(LF_CELLS);
           if (sync) P.set(LF_WAIT);
         }
@@ -425,29 +435,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 
     LDIAG(LD_RING, tail - head);
     LDIAG_T(4);
-    // ---- walk phase: crossings of ring segments on every lane ------------------------------
-    for (int k = 0; k < SMCRT_LEAN_STEPS + SMCRT_LEAN_EXTRA; ++k) {
-      {  // idle walkers take the oldest segments of the ring
-        const uint64_t im = __ballot(!W.seg);
-        const uint32_t avail = tail - head;
-        const uint32_t ni = (uint32_t)__popcll(im);
-        const uint32_t take = ni < avail ? ni : avail;
-        if (take) {
-          const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
-          if (!W.seg && rank < take) {
-            const uint32_t ix = (head + rank) & (LEAN_RING - 1);
-            W.old = v3(sh->ox[wv][ix], sh->oy[wv][ix], sh->oz[wv][ix]);
-            wdir = v3(sh->dx[wv][ix], sh->dy[wv][ix], sh->dz[wv][ix]);
-            W.slen = sh->sl[wv][ix];
-            const unsigned long long cw = sh->cw[wv][ix];
-            W.xcell = lean_cell(cw, 0); W.ycell = lean_cell(cw, 1); W.zcell = lean_cell(cw, 2);
-            wmeta = sh->meta[wv][ix];
-            W.sd = 0.0; W.dda_it = 0;
-            W.seg = true; W.tflag = false; W.fault = false;
-          }
-          head += take;
+    // idle walkers take the oldest segments of the ring (wave-uniform call)
+    auto refill = [&]() {
+      const uint64_t im = __ballot(!W.seg);
+      const uint32_t avail = tail - head;
+      const uint32_t ni = (uint32_t)__popcll(im);
+      const uint32_t take = ni < avail ? ni : avail;
+      if (take) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+        if (!W.seg && rank < take) {
+          const uint32_t ix = (head + rank) & (LEAN_RING - 1);
+          W.old = v3(sh->ox[wv][ix], sh->oy[wv][ix], sh->oz[wv][ix]);
+          wdir = v3(sh->dx[wv][ix], sh->dy[wv][ix], sh->dz[wv][ix]);
+          W.slen = sh->sl[wv][ix];
+          const unsigned long long cw = sh->cw[wv][ix];
+          W.xcell = lean_cell(cw, 0); W.ycell = lean_cell(cw, 1); W.zcell = lean_cell(cw, 2);
+          wmeta = sh->meta[wv][ix];
+          W.sd = 0.0; W.dda_it = 0;
+          W.seg = true; W.tflag = false; W.fault = false;
         }
+        head += take;
       }
+    };
+    // ---- walk phase: crossings of ring segments on every lane ------------------------------
+#pragma unroll 1  // one copy of the crossing: the unrolled steps' live ranges cost occupancy
+    for (int k = 0; k < SMCRT_LEAN_STEPS + SMCRT_LEAN_EXTRA; ++k) {
+      refill();
       const uint64_t am = __ballot(W.seg);
       if (!am) break;
       if (k >= SMCRT_LEAN_STEPS && __popcll(am) < SMCRT_LEAN_BUSY) break;
@@ -456,13 +469,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       bool dep = false;
       uint32_t vox = 0;
       double val = 0.0;
+#ifdef SMCRT_LEAN_ABL_NO_WALK  // register-pressure analysis builds only
+      W.seg = false;
+#else
       if (W.seg) dda_step<GM>(K, W, wdir, xf, yf, zf, dep, vox, val, 1.0);
+#endif
       w_dep += __popcll(__ballot(dep));
       emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
       // a finished segment: its cells and flags to the owner's slot, then the slot is free
       if ((am >> lane_id & 1ull) && !W.seg) {
-        const uint32_t owner = (uint32_t)(wv * 64) + (wmeta & 63u), slot = (wmeta >> 6) & 1u;
-        const bool sync = (wmeta & 128u) != 0;
+        const uint32_t owner = (uint32_t)(wv * 64) + (wmeta & 63u), slot = (wmeta >> 6) & 3u;
+        const bool sync = (wmeta & 256u) != 0;
         if (!sync && (W.tflag || W.fault)) ++hazards;  // cannot happen (header comment)
         sh->pcell[owner][slot] = lean_pack(W.xcell, W.ycell, W.zcell) | (W.tflag ? LEAN_TFLAG : 0ull) |
                                  (W.fault ? LEAN_FAULT : 0ull);
@@ -470,10 +487,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
+    refill();  // (the ring bound above: every walker busy, or the ring empty)
     LDIAG_T(5);
     // ---- P5: a synchronous segment finished; after a segment: next program point ---------
-    if (P.has(LF_WAIT) && !(sh->busy[threadIdx.x] & (1u << ((P.seq - 1) % LEAN_SLOTS)))) {
-      const unsigned long long w = sh->pcell[threadIdx.x][(P.seq - 1) % LEAN_SLOTS];
+    if (P.has(LF_WAIT) && !(sh->busy[threadIdx.x] & (1u << ((P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS)))) {
+      const unsigned long long w = sh->pcell[threadIdx.x][(P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS];
       P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
       P.set(LF_CELLS);
       if (w & LEAN_TFLAG) P.set(LF_TFLAG);
@@ -506,14 +524,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if (fabs(P.pos.z) > K.zmax) P.set(LF_TFLAG);
       P.st = ST_INTERACT;
     }
-    // the final cells of the photon's deferred segments, once they are all done
-    if (!P.has(LF_CELLS) && sh->busy[threadIdx.x] == 0) {
-      const unsigned long long w = sh->pcell[threadIdx.x][(P.seq - 1) % LEAN_SLOTS];
+    // the final cells of the photon's deferred segments, once they are all done (read only
+    // where they are used: recordWeight of an absorption, the photon record)
+    if (!P.has(LF_CELLS) && (P.st == ST_ABSORB || (records_on && P.st == ST_DONE)) && sh->busy[threadIdx.x] == 0) {
+      const unsigned long long w = sh->pcell[threadIdx.x][(P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS];
       P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
       P.set(LF_CELLS);
     }
 
     LDIAG_T(6);
+    // recordWeight of an absorbed photon (kernelsMod.f90:2202-2220) once its cells are in
+    if (P.st == ST_ABSORB && P.has(LF_CELLS)) {
+      if (P.xcell < 1 || P.xcell > K.nx || P.ycell < 1 || P.ycell > K.ny || P.zcell < 1 || P.zcell > K.nz)
+        P.set(LF_FAULT);
+      else if (C->absorb) atomic_add_nr(C->absorb + lin(K, P.xcell, P.ycell, P.zcell), 1.0);
+      P.st = ST_DONE;
+    }
     // ---- P7: photon events, batched as in transport_kernel ---------------------------------
     {
       const bool ev = free_ && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
@@ -523,7 +549,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       const bool run_ev = nev && (nev >= SMCRT_EVENT_LANES || evm == busy);
       LDIAG(LD_P7, run_ev ? 1 : 0);
       LDIAG(LD_EVWAIT, run_ev ? 0 : nev);
+#ifdef SMCRT_LEAN_ABL_NO_P7  // register-pressure analysis builds only (tools/regs.sh)
+      if (run_ev && __ballot(P.st == 12345)) {
+#else
       if (run_ev) {
+#endif
         if (ev && P.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2126-2170
           if (P.f & (LF_TFLAG | LF_FAULT)) {
             P.st = ST_DONE;
@@ -531,28 +561,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
             ++LLU(LL_INTER);
             P.set(LF_FAULT); P.st = ST_DONE;
           } else {
-            const uint32_t d0 = P.rng.draws;
-            const double c0 = P.rng.cached;
             const double ran = P.rng.next(K.key0, K.key1);
             const TopProps pr = props[P.layer - 1];
             const bool sc = ran < pr.albedo;
-            if (!sc && !test_kernel && !P.has(LF_CELLS)) {
-#ifdef SMCRT_DIAG
-              atomicAdd(&::g_diag[LD_REVERT], 1ull);
-#endif
-              // recordWeight needs the cells of a segment still being walked: take the draw
-              // back (the stream is counter-based) and come back once the cells are in
-              P.rng.draws = d0; P.rng.cached = c0;
-            } else {
+            {
               ++LLU(LL_INTER);
               if (!sc) {
                 P.set(LF_TFLAG); LLU(LL_STATUS) = 1; lean_count(sh, LC_ABSORBED);
-                if (!test_kernel) {  // recordWeight(packet, 1.0)
-                  if (P.xcell < 1 || P.xcell > K.nx || P.ycell < 1 || P.ycell > K.ny || P.zcell < 1 ||
-                      P.zcell > K.nz) P.set(LF_FAULT);
-                  else if (C->absorb) atomic_add_nr(C->absorb + lin(K, P.xcell, P.ycell, P.zcell), 1.0);
-                }
-                P.st = ST_DONE;
+                // recordWeight(packet, 1.0) at the photon's cells: those of its last segment,
+                // which may still be walked (ST_ABSORB adds it once they are in)
+                P.st = test_kernel ? ST_DONE : ST_ABSORB;
+#ifdef SMCRT_DIAG
+                if (!P.has(LF_CELLS)) atomicAdd(&::g_diag[LD_REVERT], 1ull);
+#endif
               } else {
                 // scatter, photon.f90:1045-1103
                 Lane L;
