@@ -542,14 +542,19 @@ def main():
             # PMC HBM bytes of the whole step (transport + deposit folds) per launch.
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": traffic,
-                         "kernel": "transport_kernel", "avg_launch_ms": kern_ms, "timing": timing_src,
+                         "kernel": (pmc.get("kernel") or "transport_kernel").split("<")[0],
+                         "avg_launch_ms": kern_ms, "timing": timing_src,
                          "launches_timed": launches,
                          "algorithmic_bytes_per_launch": alg_bytes,
                          "traffic_source": traffic_src,
                          "traffic_by_kernel": pmc.get("hbm_bytes_per_launch_by_kernel"),
                          "traffic_over_algorithmic": (traffic / alg_bytes) if traffic and alg_bytes else None,
                          "deposits_per_photon": deposits / (args.steps * B),
-                         "deposit_fold_ms_per_launch": dep_ms,
+                         # the HIP-event interval from a launch's end to its fold's end: the fold
+                         # kernels (bk_scan, bk_place, bk_reduce) wait for CU slots behind the next
+                         # persistent launch, so this is mostly queueing, not fold work (the fold's
+                         # busy time is bk_reduce's ~7.5 ms in the committed rocprofv3 trace)
+                         "fold_interval_ms_per_launch": dep_ms,
                          "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) * per_rank / launches,
                          "sdf_evals_per_photon": sdf_evals / (args.steps * B),
                          "note": "the transport kernel is bound by fp64 VALU issue and divergence, not by "

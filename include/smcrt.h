@@ -356,7 +356,8 @@ typedef struct smcrt_kernel_times {
   double transport_ms;  /* transport_kernel */
   double deposit_ms;    /* binned jmean fold: bin_hist .. bin_reduce */
   int64_t launches;     /* transport launches timed */
-  int64_t reserved;
+  int64_t lean_launches; /* of all launches since the last query (timed or not), those that ran
+                            the lean kernel (Fresnel-free, detector-free scenes) */
 } smcrt_kernel_times;
 
 int smcrt_scene_set_timing(smcrt_scene* scene, int32_t enable);

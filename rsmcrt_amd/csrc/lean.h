@@ -66,6 +66,16 @@ namespace smcrt {
 #ifndef SMCRT_LEAN_BUSY
 #define SMCRT_LEAN_BUSY 48
 #endif
+// after the first crossing step of a walk phase, idle walkers refill only once this many are
+// idle (1: every step)
+#ifndef SMCRT_LEAN_REFILL_IDLE
+#define SMCRT_LEAN_REFILL_IDLE 1
+#endif
+// walkers keep their segment's direction reciprocals (formed at the refill) instead of
+// forming them at every crossing
+#ifndef SMCRT_LEAN_RCP
+#define SMCRT_LEAN_RCP 0
+#endif
 constexpr uint32_t ST_ABSORB = 40;  // absorbed; recordWeight waits for the photon's cells
 #ifndef SMCRT_LEAN_SLOTS
 #define SMCRT_LEAN_SLOTS 3
@@ -162,6 +172,9 @@ enum : int { LD_TRIPS = 0, LD_WSTEPS, LD_WLANES, LD_PUSH, LD_SYNC, LD_BLOCKED, L
     lt[(i)] += t_ - lt_last;                                        \
     lt_last = t_;                                                   \
   } while (0)
+#elif defined(SMCRT_ASM_MARKERS)  // analysis builds: phase boundaries visible in the ISA
+#define LDIAG(i, v) do {} while (0)
+#define LDIAG_T(i) asm volatile("; @@LPHASE " #i)
 #else
 #define LDIAG(i, v) do {} while (0)
 #define LDIAG_T(i) do {} while (0)
@@ -224,6 +237,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   W.dda_it = 0;
   W.seg = W.tflag = W.fault = false;
   V3 wdir = v3(0.0, 0.0, 0.0);
+#if SMCRT_LEAN_RCP
+  V3 wrcp = v3(0.0, 0.0, 0.0);  // ieee_rcp_f64 of wdir, formed once per segment at the refill
+#endif
   uint32_t wmeta = 0;
   uint32_t head = 0, tail = 0;  // the wave's ring tickets (scalar registers)
   BucketLog WB;
@@ -436,17 +452,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     LDIAG(LD_RING, tail - head);
     LDIAG_T(4);
     // idle walkers take the oldest segments of the ring (wave-uniform call)
-    auto refill = [&]() {
+    auto refill = [&](uint32_t min_idle) {
       const uint64_t im = __ballot(!W.seg);
       const uint32_t avail = tail - head;
       const uint32_t ni = (uint32_t)__popcll(im);
       const uint32_t take = ni < avail ? ni : avail;
-      if (take) {
+      if (take && ni >= min_idle) {
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
         if (!W.seg && rank < take) {
           const uint32_t ix = (head + rank) & (LEAN_RING - 1);
           W.old = v3(sh->ox[wv][ix], sh->oy[wv][ix], sh->oz[wv][ix]);
           wdir = v3(sh->dx[wv][ix], sh->dy[wv][ix], sh->dz[wv][ix]);
+#if SMCRT_LEAN_RCP
+          wrcp = v3(ieee_rcp_f64(wdir.x), ieee_rcp_f64(wdir.y), ieee_rcp_f64(wdir.z));
+#endif
           W.slen = sh->sl[wv][ix];
           const unsigned long long cw = sh->cw[wv][ix];
           W.xcell = lean_cell(cw, 0); W.ycell = lean_cell(cw, 1); W.zcell = lean_cell(cw, 2);
@@ -460,7 +479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     // ---- walk phase: crossings of ring segments on every lane ------------------------------
 #pragma unroll 1  // one copy of the crossing: the unrolled steps' live ranges cost occupancy
     for (int k = 0; k < SMCRT_LEAN_STEPS + SMCRT_LEAN_EXTRA; ++k) {
-      refill();
+      refill(k == 0 ? 1u : (uint32_t)SMCRT_LEAN_REFILL_IDLE);
       const uint64_t am = __ballot(W.seg);
       if (!am) break;
       if (k >= SMCRT_LEAN_STEPS && __popcll(am) < SMCRT_LEAN_BUSY) break;
@@ -472,10 +491,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 #ifdef SMCRT_LEAN_ABL_NO_WALK  // register-pressure analysis builds only
       W.seg = false;
 #else
+#if SMCRT_LEAN_RCP
+      if (W.seg) dda_step_r<GM>(K, W, wdir, wrcp, xf, yf, zf, dep, vox, val, 1.0);
+#else
       if (W.seg) dda_step<GM>(K, W, wdir, xf, yf, zf, dep, vox, val, 1.0);
 #endif
+#endif
       w_dep += __popcll(__ballot(dep));
+#ifndef SMCRT_LEAN_ABL_NO_EMIT  // register-pressure analysis builds only
       emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+#else
+      if (__ballot(dep) == 0x123ull) atomic_add_nr(C->jmean + vox, val);
+#endif
       // a finished segment: its cells and flags to the owner's slot, then the slot is free
       if ((am >> lane_id & 1ull) && !W.seg) {
         const uint32_t owner = (uint32_t)(wv * 64) + (wmeta & 63u), slot = (wmeta >> 6) & 3u;
@@ -487,7 +514,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       }
     }
 
-    refill();  // (the ring bound above: every walker busy, or the ring empty)
+    refill(1);  // (the ring bound above: every walker busy, or the ring empty)
+#ifdef SMCRT_LEAN_ABL_DROP_WALK  // register-pressure analysis builds only (not exact)
+    W.seg = false; W.old = wdir = v3(0.0, 0.0, 0.0); W.sd = W.slen = 0.0; wmeta = 0;
+    W.xcell = W.ycell = W.zcell = 0; W.dda_it = 0;
+#endif
     LDIAG_T(5);
     // ---- P5: a synchronous segment finished; after a segment: next program point ---------
     if (P.has(LF_WAIT) && !(sh->busy[threadIdx.x] & (1u << ((P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS)))) {
@@ -683,6 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   const uint32_t hz = wave_sum_u32(hazards);
   if (lane_id == 0) {
     if (hz) atomicAdd(C->dep_ctl + 5, hz);
+    if (C->dep_ctl && sh->wctr[wv][LC_UPD]) atomicAdd(C->dep_ctl + 6, sh->wctr[wv][LC_UPD]);  // segments
     if (counters) {
       const uint32_t* c = sh->wctr[wv];
       const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,

@@ -745,6 +745,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
   }
 #endif
   // ---- per-wave counter reduction ------------------------------------------------------
+  if (binned && K.bucket_tiles) {  // segments of this launch (the host's lean-kernel choice)
+    const uint32_t u = wave_sum_u32(LCTR(LC_UPD));
+    if (lane_id == 0 && u) atomicAdd(C->dep_ctl + 6, u);
+  }
   unsigned long long* const counters = C->counters;
   if (counters) {
     uint32_t c[SMCRT_NCOUNTERS];
@@ -875,6 +879,14 @@ struct smcrt_scene {
   // deposition, axes below 2^20 cells (SMCRT_LEAN=0 keeps transport_kernel)
   bool lean_ok = false;
   uint64_t lean_hazards = 0;
+  int64_t lean_launches = 0;  // since the last smcrt_scene_kernel_times
+  // voxel crossings per deposit segment, measured by the scene's launches (dep_ctl[6]): the
+  // lean kernel pays for decoupled walks with a refill per crossing step, which long segments
+  // do not repay (M0: 8.2 crossings per segment, -6 %; M1: 3.5, +5 %), so it is chosen only
+  // up to LEAN_MAX_XPS (SMCRT_LEAN=1 forces it, =0 disables it)
+  double xps = 0.0;
+  bool xps_measured = false;
+  int lean_mode = -1;  // -1 automatic, 0 off, 1 forced
   // source spectrum tables of the last general-emitter run (srcplan.h), device copy
   std::vector<double> h_spec;
   double* d_spec = nullptr;
@@ -927,6 +939,7 @@ struct smcrt_scene {
 };
 
 constexpr size_t MAX_TIMED = 256;
+constexpr double LEAN_MAX_XPS = 5.5;  // the lean kernel's limit in crossings per segment (above)
 constexpr uint64_t COLD_PER_STREAM = 16;
 constexpr uint64_t COLD_SLOTS = COLD_PER_STREAM * (MAX_SLOTS + 1);  // a ring per launch stream
 constexpr uint32_t MAX_FUSED_HIST_TILES = 512;  // 8 KiB of LDS per block for the wave histograms
@@ -1289,7 +1302,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     for (int32_t i = 1; ok && i < n_top; ++i) ok = s->h_props[i].n == s->h_props[0].n;
     ok = ok && lean_lds(s) + sizeof(LeanShared) <= 65536;
     const char* le = std::getenv("SMCRT_LEAN");
-    s->lean_ok = ok && !(le && std::string(le) == "0");
+    s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
+    s->lean_ok = ok && s->lean_mode != 0;
   }
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   if (s->lean_ok) {
@@ -1383,6 +1397,10 @@ static void refine_rpp(smcrt_scene* s) {
         s->lean_hazards += h[5];
         std::fprintf(stderr, "[smcrt] lean kernel: %u deferred voxel walks ended in an error stop or left the grid "
                      "(parity not guaranteed for those photons)\n", h[5]);
+      }
+      if (h[6] > 0) {  // voxel crossings per deposit segment of this scene's last launch
+        s->xps = (double)(h[3] + h[1]) / (double)h[6];
+        s->xps_measured = true;
       }
       if (h[4] > 0) {
         const double rpp = (double)(h[3] + h[1]) / (double)h[4];
@@ -1519,11 +1537,13 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   // lean_kernel (lean.h) when the scene and the run qualify: bucketed path-length deposition,
   // unit weights (no survival bias), a plain source
   const bool lean = !xsrc && s->lean_ok && K.bucket_tiles && (K.flags & SMCRT_FLAG_PATHLENGTH) &&
-                    !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS);
+                    !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
+                    (s->lean_mode == 1 || !s->xps_measured || s->xps <= LEAN_MAX_XPS);
   const int blocks = (int)std::min<uint64_t>(
       (uint64_t)(lean ? s->grid_blocks_lean : (xsrc ? s->grid_blocks_x : s->grid_blocks)),
       std::max<uint64_t>(1, blocks_needed));
   if (lean) {
+    ++s->lean_launches;
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;
     const ProgOp* a_prog = K.prog;
@@ -1571,7 +1591,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     HIPCHK(hipGetLastError());
     // remember how many records this launch produced (read back lazily, never waited for)
     HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl, s->d_dep_ctl[sl], 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
-    HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl + 5, s->d_dep_ctl[sl] + 5, sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
+    HIPCHK(hipMemcpyAsync(s->h_ctl + 8 * sl + 5, s->d_dep_ctl[sl] + 5, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, fs));
     HIPCHK(hipEventRecord(s->ctl_ev[sl], fs));
     s->ctl_pending[sl] = true;
     if (ev) HIPCHK(hipEventRecord(ev[3], fs));
@@ -2007,7 +2027,8 @@ int smcrt_scene_kernel_times(smcrt_scene* s, smcrt_kernel_times* out) {
   out->transport_ms = s->t_transport;
   out->deposit_ms = s->t_deposit;
   out->launches = s->t_launches;
-  out->reserved = 0;
+  out->lean_launches = s->lean_launches;
+  s->lean_launches = 0;
   s->t_transport = s->t_deposit = 0.0;
   s->t_launches = 0;
   return SMCRT_OK;

@@ -748,10 +748,25 @@ __device__ __forceinline__ bool start_segment(const KParams& K, Lane& L, LaneSha
 // (inttau2.f90:417-441, 467-584). Clears L.seg when the segment ends. `L` is any state with
 // the segment fields of Lane (old, sd, slen, xcell/ycell/zcell, dda_it, seg, tflag, fault):
 // the photon's own Lane, or a walker's segment (lean.h); `dir` is the segment's direction.
+// (dda_step_r: the same crossing with the direction's refined reciprocals (ieee_rcp_f64 of
+// each component) supplied by the caller, e.g. kept by a walker for its whole segment.)
+template <int GM, class S>
+__device__ __forceinline__ void dda_step_r(const KParams& K, S& L, const V3 dir, const V3 rcp,
+                                           const double* __restrict__ xf, const double* __restrict__ yf,
+                                           const double* __restrict__ zf, bool& dep, uint32_t& dep_vox,
+                                           double& dep_val, double weight);
 template <int GM, class S>
 __device__ __forceinline__ void dda_step(const KParams& K, S& L, const V3 dir, const double* __restrict__ xf,
                                          const double* __restrict__ yf, const double* __restrict__ zf,
                                          bool& dep, uint32_t& dep_vox, double& dep_val, double weight) {
+  const V3 rcp = v3(ieee_rcp_f64(dir.x), ieee_rcp_f64(dir.y), ieee_rcp_f64(dir.z));
+  dda_step_r<GM>(K, L, dir, rcp, xf, yf, zf, dep, dep_vox, dep_val, weight);
+}
+template <int GM, class S>
+__device__ __forceinline__ void dda_step_r(const KParams& K, S& L, const V3 dir, const V3 rcp3,
+                                           const double* __restrict__ xf, const double* __restrict__ yf,
+                                           const double* __restrict__ zf, bool& dep, uint32_t& dep_vox,
+                                           double& dep_val, double weight) {
 #ifdef SMCRT_ASM_MARKERS
   asm volatile("; @@DDA_BEGIN");
 #endif
@@ -773,7 +788,7 @@ __device__ __forceinline__ void dda_step(const KParams& K, S& L, const V3 dir, c
   // the compiler expands `n / d`) depends on the direction only, so it is computed once per
   // trip (the compiler hoists it out of the unrolled crossings); per crossing only the
   // numerator half (mul, residual fma, correction fma) remains.
-  const double rx = ieee_rcp_f64(dir.x), ry = ieee_rcp_f64(dir.y), rz = ieee_rcp_f64(dir.z);
+  const double rx = rcp3.x, ry = rcp3.y, rz = rcp3.z;
   const double ax = nx * rx;
   const double ay = ny * ry;
   const double az = nz * rz;
@@ -791,7 +806,11 @@ __device__ __forceinline__ void dda_step(const KParams& K, S& L, const V3 dir, c
   const double rcp = lx ? rx : (ly ? ry : rz);
   const bool fast = fast0 && fabs(num) >= 0x1.0p-500;
   double dcell;
+#ifdef SMCRT_ABL_NO_SLOWDIV  // register-pressure analysis builds only (not exact)
+  if (true) {
+#else
   if (fast) {
+#endif
     dcell = ieee_div_tail_f64(num, den, rcp);  // == num / den bit for bit
   } else {
     double dx = -999.0, dy = -999.0, dz = -999.0;

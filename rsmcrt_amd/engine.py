@@ -252,7 +252,8 @@ class Engine:
         """Device ms per kernel group since the previous call (waits for those launches)."""
         t = abi.KernelTimes()
         _check(load_library().smcrt_scene_kernel_times(self._h, C.byref(t)))
-        return {"transport_ms": t.transport_ms, "deposit_ms": t.deposit_ms, "launches": t.launches}
+        return {"transport_ms": t.transport_ms, "deposit_ms": t.deposit_ms, "launches": t.launches,
+                "lean_launches": t.lean_launches}
 
 
 def pack_layout(grid, n_det_bins: int, fields: int) -> abi.PackLayout:

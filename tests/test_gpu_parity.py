@@ -710,3 +710,42 @@ def test_multi_accumulate_dynamic_chunks_one_collect(monkeypatch):
     assert np.array_equal(a.absorb, b.absorb) and np.array_equal(a.det_bins, b.det_bins)
     np.testing.assert_allclose(a.jmean, b.jmean, rtol=1e-12, atol=1e-300)
     assert a.nscatt[0] == b.nscatt[0]
+
+
+@pytest.mark.parametrize("case", ["absorbing", "boundary-source", "test-kernel"])
+def test_lean_kernel_paths(monkeypatch, case):
+    """The lean kernel (lean.h: Fresnel-free, detector-free scenes, the voxel walk decoupled
+    from the photon) against the oracle, photon by photon, on the paths it adds:
+    * absorbing: mua = 2 (albedo 0.83), so many photons are absorbed while their last
+      segment is still being walked (ST_ABSORB waits for the cells recordWeight needs);
+    * boundary-source: a uniform source on the top face, so segments near the grid faces are
+      synchronous (the photon waits for tflag/cells) and escapes through the walk are common;
+    * test-kernel: test_kernel semantics (no re-emission, ds<=0 mask, scatter moments).
+    The scene is also run with SMCRT_LEAN=0 (transport_kernel): same counters and records."""
+    from rsmcrt_amd.engine import Engine as E
+    flags = abi.FLAG_PATHLENGTH
+    g = scene.grid(48, 48, 48, 1, 1, 1)
+    if case == "absorbing":
+        sc, src, n = builders.setup_sphere(10.0, 2.0, 0.9, 1.0, 1.0), scene.point_source(), 30000
+    elif case == "boundary-source":
+        sc = builders.setup_sphere(5.0, 0.5, 0.8, 1.0, 1.0)
+        src = scene.uniform_source((-1.0, -1.0, 0.999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+        n = 30000
+    else:
+        sc, src, n = builders.setup_scat_test(10.0), scene.point_source(), 20000
+        flags |= abi.FLAG_TEST_KERNEL
+    runs = {}
+    for lean in ("1", "0"):
+        monkeypatch.setenv("SMCRT_LEAN", lean)
+        with E(sc, g) as eng:
+            eng.kernel_times()
+            runs[lean] = eng.run(src, n, seed=SEED, flags=flags, records=True)
+            kt = eng.kernel_times()
+        assert (kt["lean_launches"] > 0) == (lean == "1"), (lean, kt)
+    cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True)
+    for r in runs.values():
+        compare(r, cpu)
+    if case == "absorbing":
+        assert cpu.counter("absorbed") > n // 2
+    if case == "test-kernel":
+        np.testing.assert_allclose(runs["1"].moments, cpu.moments, rtol=1e-12)

@@ -3,7 +3,7 @@
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 for w in ${WLS:-m1}; do
-  timeout -k 10 ${WL_T:-300} python -u bench.py --workload $w --steps ${STEPS:-2} --warmup 1 --cpu-seconds ${CPU_S:-8} \
+  timeout -k 10 ${WL_T:-300} python -u bench.py --workload $w --steps ${STEPS:-2} --warmup 1 --cpu-seconds ${CPU_S:-8} --no-ref \
     > gpurun_out/wl_$w.json 2> gpurun_out/wl_$w.err || exit $?
   echo "$w done"
 done

@@ -87,7 +87,8 @@ def main():
         print(f"{k:28s} n={d['dispatches']:3d} avg={d['avg_ms_last']:8.3f} ms ({100*d['avg_ms_last']/tot:5.1f}%)"
               f"{hb}{extra}")
     if a.traffic:
-        k = next((k for k in out if k.startswith("transport_kernel") and "hbm_bytes_per_dispatch" in out[k]), None)
+        k = next((k for k in out if k.startswith(("transport_kernel", "lean_kernel")) and
+                  "hbm_bytes_per_dispatch" in out[k]), None)
         if k:
             # the whole step: the transport kernel plus the deposit-fold kernels that follow each
             # of its launches (same dispatch count), per launch
