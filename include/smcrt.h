@@ -358,6 +358,8 @@ typedef struct smcrt_kernel_times {
   int64_t launches;     /* transport launches timed */
   int64_t lean_launches; /* of all launches since the last query (timed or not), those that ran
                             the lean kernel (Fresnel-free, detector-free scenes) */
+  int64_t far_steps;     /* march steps taken by the far-field march (long sphere-tracing runs with
+                            only the nearest SDF re-evaluated) since the last query */
 } smcrt_kernel_times;
 
 int smcrt_scene_set_timing(smcrt_scene* scene, int32_t enable);

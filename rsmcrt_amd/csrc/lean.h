@@ -312,23 +312,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
     LDIAG(LD_ELANES, __popcll(__ballot(have)));
     LDIAG_T(2);
     // ---- P3: consume the EVAL result (transport_kernel's P3 without Fresnel) -------------
-    if (have) {
+    // The three "d = minval(abs(ds))" program points, the bulk of the EVALs, as one block of
+    // selects (fewer divergent paths): H0 :63-84/149-152, H3 :133-152, M1 :177-191.
+    if (have && (P.st == ST_H0 || P.st == ST_H3 || P.st == ST_M1)) {
+      const uint32_t st0 = P.st;
+      P.minabs = R.minabs;
+      const bool small = st0 == ST_H0 && R.minabs < eps;  // on a surface: micro-step
+      const bool out = st0 != ST_H0 && R.minv > 0.0;
+      if (out) P.set(LF_TFLAG);
+      if (st0 == ST_H0) P.loopc = 0;
+      const bool done = P.taurun >= P.tau || P.has(LF_TFLAG);
+      P.d = small ? R.minabs + 2.0 * eps : R.minabs;
+      uint32_t ns = st0 == ST_M1 ? (out ? (uint32_t)ST_B0 : (uint32_t)ST_M0) : (done ? (uint32_t)ST_T2END : (uint32_t)ST_M0);
+      if (small) { ns = ST_H1; P.set(LF_PEND); }
+      P.st = ns;
+    } else if (have) {
       switch (P.st) {
         case ST_LAYER:  // kernelsMod.f90:1948-1952 (test_kernel: mask ds<=0, :2136)
           P.layer = R.maxloc;
           if (P.layer == 0) { P.set(LF_FAULT); P.st = ST_DONE; }
           else P.st = ST_T2;
-          break;
-        case ST_H0:  // inttau2.f90:63-84, 149-152
-          P.minabs = R.minabs;
-          P.d = R.minabs;
-          P.loopc = 0;
-          if (P.d < eps) {
-            P.d = R.minabs + 2.0 * eps;
-            P.st = ST_H1; P.set(LF_PEND);
-          } else {
-            P.st = (P.taurun >= P.tau || P.has(LF_TFLAG)) ? ST_T2END : ST_M0;
-          }
           break;
         case ST_H1: {  // :86-123 (the segment starts at the pre-move pos)
           const double kap = props[P.layer - 1].kappa;
@@ -344,18 +347,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
           P.set(LF_REQ);
           break;
         }
-        case ST_H3:  // :133-152
-          P.minabs = R.minabs;
-          P.d = R.minabs;
-          if (R.minv > 0.0) P.set(LF_TFLAG);
-          P.st = (P.taurun >= P.tau || P.has(LF_TFLAG)) ? ST_T2END : ST_M0;
-          break;
-        case ST_M1:  // :177-191
-          P.minabs = R.minabs;
-          P.d = R.minabs;
-          if (R.minv > 0.0) { P.set(LF_TFLAG); P.st = ST_B0; }
-          else P.st = ST_M0;
-          break;
         case ST_G0: {  // new layer and the glancing loop, :220-245; equal n: cross, :318-328
           const int32_t new_layer = R.maxloc;
           if (new_layer == P.layer && R.minabs < eps) {  // (old_layer == layer here)

@@ -38,6 +38,7 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 }
 
 #include "lean.h"
+#include "far.h"
 
 // The query point of each EVAL state (the exact expressions of the reference).
 __device__ __forceinline__ V3 eval_query(const Lane& L) {
@@ -260,10 +261,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
         while (run) {
           const V3 q = v3(readlane_f64(L.pos.x, ow), readlane_f64(L.pos.y, ow), readlane_f64(L.pos.z, ow));
           EvalOut S;
-          if (K.ctab) S = eval_coop_tab(ctab, K.n_top, q, false, 0, 0);
+          double dl = 0.0;  // this lane's ds(lane + 1) (LDS-table EVAL)
+          if (K.ctab) S = eval_coop_tab(ctab, K.n_top, q, false, 0, 0, &dl);
           else if (K.cull) S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0);
           else S = eval_sdfs(nodes, prog, K.n_prog, q, false, 0, 0);
           w_sdf += (uint32_t)K.n_top;  // ST_M1's ds array is counted (packet%cnts)
+          // far-field certificate of this EVAL (far.h): the nearest top k and the smallest
+          // |ds| of the others, for a march that has run a while
+          int fk = -1;
+          double fm2 = 0.0;
+          bool fneg = false;
+          if (K.fm_err > 0.0 && K.ctab && __builtin_amdgcn_readlane((int)L.loopc, ow) >= SMCRT_FAR_MIN_LOOP) {
+            const bool mine = lane_id < K.n_top;
+            const double ad = mine ? fabs(dl) : __builtin_inf();
+            const uint64_t km = __ballot(mine && ad == S.minabs);
+            const uint64_t bad = __ballot(mine && !(ad <= 0x1.fffffffffffffp+1023));  // NaN, inf
+            if (km && !bad) {
+              const int k = __builtin_ctzll(km);
+              const int kind = (int)ctab[20 * 64 + k] & 15;
+              if (kind == SMCRT_SDF_SPHERE || kind == SMCRT_SDF_BOX) {
+                fm2 = wave_min_f64(lane_id == k ? __builtin_inf() : ad);
+                fneg = __ballot(mine && lane_id != k && dl < 0.0) != 0;
+                fk = k;
+              }
+            }
+          }
           if (lane_id == ow) {
             L.pend = false;  // P3, ST_M1: :177-191
             L.minabs = S.minabs;
@@ -309,6 +331,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
             }
           }
           run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
+          if (run && fk >= 0) {  // the far-field march from the certificate (far.h)
+            uint32_t n = 0, nsdf = 0;
+            if (lane_id == ow) {
+              double acc = 0.0;
+              uint32_t vox = 0;
+              const double kap = props[L.layer - 1].kappa;
+              const int kind = (int)ctab[20 * 64 + fk] & 15;
+              n = kind == SMCRT_SDF_BOX
+                      ? far_march<GM, SMCRT_SDF_BOX>(K, L, ctab, fk, fm2, fneg, S.minabs, kap, xf, yf, zf, acc, vox, nsdf)
+                      : far_march<GM, SMCRT_SDF_SPHERE>(K, L, ctab, fk, fm2, fneg, S.minabs, kap, xf, yf, zf, acc, vox,
+                                                        nsdf);
+              if (n) {
+                LCTR(LC_UPD) += n;
+                double* const jm = C->jmean;
+                if (jm) atomic_add_nr(jm + vox, acc);
+                if (C->far_steps) atomicAdd(C->far_steps, (unsigned long long)n);
+              }
+            }
+            n = (uint32_t)__builtin_amdgcn_readlane((int)n, ow);
+            nsdf = (uint32_t)__builtin_amdgcn_readlane((int)nsdf, ow);
+            w_sdf += nsdf * (uint32_t)K.n_top;
+            w_dep += n;
+            run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
+          }
         }
       }
     }
@@ -844,6 +890,10 @@ struct smcrt_scene {
   int n_prog = 0;
   int coop_lanes = 0;
   double* d_ctab = nullptr;  // the cooperative EVAL's primitive table (transport.h), or NULL
+  // far-field march (far.h): KParams::fm_err / fm_step, 0 when the scene does not qualify;
+  // the running total of its steps is d_queue[MAX_SLOTS + 1]
+  double fm_err = 0.0, fm_step = 0.0;
+  unsigned long long far_reported = 0;
   // exact SDF culling (cull.h): grid + lists + the always-evaluated program, one allocation
   CullGrid* d_cull = nullptr;
   void* d_cull_data = nullptr;
@@ -1168,6 +1218,29 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
         for (int r = 0; r < 8; ++r) ctab[(12 + r) * 64 + i] = nd.param[r];
         ctab[20 * 64 + i] = (double)nd.kind + (translate_only(top[i]) ? 16.0 : 0.0);
       }
+      // The far-field march needs every top 1-Lipschitz (exact-distance primitives under
+      // translation-only transforms) and a bound on the computed values' error: a few ulps
+      // of the largest operand, taken here as 2^-44 of the scene's extent (far.h).
+      // SMCRT_FAR_MARCH=0 turns it off.
+      const char* fe = std::getenv("SMCRT_FAR_MARCH");
+      bool fm = !(fe && std::string(fe) == "0");
+      double ext = grid->xmax + grid->ymax + grid->zmax + 1.0;
+      double scale = 0.0;
+      for (int32_t i = 0; fm && i < n_top; ++i) {
+        const smcrt_sdf_node& nd = nodes[top[i]];
+        const int32_t kd = nd.kind;
+        fm = translate_only(top[i]) && (kd == SMCRT_SDF_SPHERE || kd == SMCRT_SDF_BOX || kd == SMCRT_SDF_TORUS ||
+                                        kd == SMCRT_SDF_SEGMENT || kd == SMCRT_SDF_CAPSULE);
+        double m = std::fabs(nd.transform[3]) + std::fabs(nd.transform[7]) + std::fabs(nd.transform[11]);
+        for (int r = 0; r < 8; ++r) m += std::fabs(nd.param[r]);
+        fm = fm && std::isfinite(m);
+        scale = std::max(scale, m);
+      }
+      fm = fm && std::isfinite(ext);
+      if (fm) {
+        s->fm_err = std::ldexp(scale + ext, -44);
+        s->fm_step = std::ldexp(scale + ext, -48);
+      }
     }
   }
   // exact culling of the SDF array for many-top scenes (cull.h); SMCRT_CULL=0 turns it off
@@ -1186,12 +1259,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
-      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 1)) ||
+      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 2)) ||
       (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
     return cleanup_fail(st);
   hipError_t e = hipSuccess;
+  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 2) * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemcpy(s->d_nodes, nodes, sizeof(smcrt_sdf_node) * n_nodes, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_prog, prog.data(), sizeof(ProgOp) * prog.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !ctab.empty()) {
@@ -1710,6 +1784,9 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.coop_lanes = s->coop_lanes;
   K.cull = s->d_cull;
   K.ctab = s->d_ctab;
+  const bool far = s->fm_err > 0.0 && (cfg->flags & SMCRT_FLAG_PATHLENGTH);
+  K.fm_err = far ? s->fm_err : 0.0;
+  K.fm_step = s->fm_step;
   K.inv2x = s->inv2[0]; K.inv2y = s->inv2[1]; K.inv2z = s->inv2[2];
   K.fex = s->fe[0]; K.fey = s->fe[1]; K.fez = s->fe[2];
   K.props = s->d_props;
@@ -1734,6 +1811,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.det_bins = dt.det_bins; Ch.nscatt = dt.nscatt; Ch.moments = dt.moments;
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = nullptr;  // (set per launch: launch_one)
+  Ch.far_steps = s->d_queue + MAX_SLOTS + 1;
   K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
   {
     const char* cd = std::getenv("SMCRT_DEBUG_CLAIM_DELAY");
@@ -2029,6 +2107,10 @@ int smcrt_scene_kernel_times(smcrt_scene* s, smcrt_kernel_times* out) {
   out->launches = s->t_launches;
   out->lean_launches = s->lean_launches;
   s->lean_launches = 0;
+  unsigned long long far = 0;  // (a running total: steps of launches still running count later)
+  HIPCHK(hipMemcpy(&far, s->d_queue + MAX_SLOTS + 1, sizeof(far), hipMemcpyDeviceToHost));
+  out->far_steps = (int64_t)(far - s->far_reported);
+  s->far_reported = far;
   s->t_transport = s->t_deposit = 0.0;
   s->t_launches = 0;
   return SMCRT_OK;

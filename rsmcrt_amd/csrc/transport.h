@@ -84,6 +84,7 @@ struct KCold {
   uint32_t* bucket_tile;      // bucketed path: tile of each bucket id (TILE_INVALID: unused)
   uint32_t* bucket_fill;      // bucketed path: records in each bucket
   uint32_t* tile_nb;          // bucketed path: buckets claimed per tile
+  unsigned long long* far_steps;  // march steps taken by the far-field march (far.h), running total
   SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
 
@@ -122,6 +123,10 @@ struct KParams {
   // the cooperative EVAL's table of primitives (CTAB_ROWS x 64 doubles, column = top - 1),
   // staged in LDS by the COOP instantiation; NULL when the scene does not qualify
   const double* __restrict__ ctab;
+  // far-field march (far.h), COOP instantiation with ctab: the absolute error bound of a
+  // computed top-level SDF value and the per-step bound on the rounding of p + d*dir (both
+  // from the scene's extent); fm_err == 0 turns it off
+  double fm_err, fm_step;
 };
 
 // ------------------------------------------------------------------ voxels -------
@@ -1023,8 +1028,9 @@ __device__ __forceinline__ void coop_step(CoopAcc& a) {
   coop_fold(a, b);
 }
 // The whole wave evaluates the SDF array at the wave-uniform point q (all lanes active).
+// (lane_d, if given, receives the lane's own ds(lane + 1), 0 past n_top)
 __device__ __forceinline__ EvalOut eval_coop_tab(const double* ct, int32_t n_top, V3 q, bool mask_le, int32_t capi,
-                                                 int32_t capj) {
+                                                 int32_t capj, double* lane_d = nullptr) {
   const int lane = (int)(threadIdx.x & 63);
   CoopAcc a;
   a.minabs = __builtin_inf(); a.minv = __builtin_inf(); a.best = -__builtin_inf(); a.loc = 0;
@@ -1052,6 +1058,7 @@ __device__ __forceinline__ EvalOut eval_coop_tab(const double* ct, int32_t n_top
   r.maxloc = __builtin_amdgcn_readlane(a.loc, 63);
   r.va = capi > 0 ? readlane_f64(d, capi - 1) : 0.0;
   r.vb = capj > 0 ? readlane_f64(d, capj - 1) : 0.0;
+  if (lane_d) *lane_d = d;
   return r;
 }
 

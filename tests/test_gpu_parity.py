@@ -99,6 +99,37 @@ def test_tail_machinery_wall_photons(variant, monkeypatch):
     assert cpu.counter("sdf_evals") > 300 * 41 * 500  # (long marches: the tail machinery ran)
 
 
+@pytest.mark.parametrize("case", ["gm2", "gm1", "gm0", "survival", "off"])
+def test_far_field_march(case, monkeypatch):
+    """The far-field march (far.h): a lone photon's long march re-evaluates only its nearest
+    SDF while a certificate from the last full EVAL bounds every other one. Photons within
+    1e-3 of a side wall march parallel to it for ~2/δ steps, most of them in the far-field
+    loop. Counters (SDF evaluations, deposits, grid updates), photon records and jmean must
+    equal the oracle's exactly as without it ("off": SMCRT_FAR_MARCH=0), on every grid kind
+    (GM 2: power-of-two cells, 1: power-of-two extent, 0: neither) and with the unbinned
+    (survival-bias) deposit path."""
+    if case == "off":
+        monkeypatch.setenv("SMCRT_FAR_MARCH", "0")
+    flags = abi.FLAG_PATHLENGTH | (abi.FLAG_SURVIVAL_BIAS if case == "survival" else 0)
+    g = {"gm1": scene.grid(50, 50, 50, 1, 1, 1), "gm0": scene.grid(40, 36, 44, 1.25, 1.25, 1.25)}.get(
+        case, scene.grid(32, 32, 32, 1, 1, 1))
+    sc = builders.setup_sphere_scene(builders.random_sphere_list(40))
+    src = scene.uniform_source((-1.0, -1.0, 0.9999999), (1e-3, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    n = 200
+    with Engine(sc, g) as eng:
+        eng.kernel_times()
+        gpu = eng.run(src, n, seed=SEED, flags=flags, records=True)
+        kt = eng.kernel_times()
+    cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True)
+    compare(gpu, cpu, exact_absorb=case != "survival")
+    steps = cpu.counter("grid_updates")
+    assert steps > n * 2000  # (long marches)
+    if case == "off":
+        assert kt["far_steps"] == 0, kt
+    else:
+        assert kt["far_steps"] > steps // 2, (kt, steps)  # most steps ran in the far-field loop
+
+
 def test_detectors_validation1():
     sc = builders.setup_box(90.0, 10.0, 0.75, 1.0, (100.0, 100.0, 0.02), (100.0, 100.0, 0.03))
     g = scene.grid(50, 50, 50, 50.0, 50.0, 0.015)
