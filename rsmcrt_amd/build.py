@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import os
 import shutil
+import glob
 import subprocess
 import sys
 
@@ -14,9 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libsmcrt.so")
 SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp", "multi.hip", "cull.cpp")]
-DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("transport.h", "detmath.h", "geometry.h", "deposit.h",
-                                                         "hosterr.h", "toml.h", "mat4.h", "srcplan.h", "png.h", "scene_internal.h", "cull.h")] + [
-    os.path.join(ROOT, "include", "smcrt.h")]
+DEPS = SOURCES + sorted(glob.glob(os.path.join(PKG, "csrc", "*.h"))) + [os.path.join(ROOT, "include", "smcrt.h")]
 ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no fused multiply-add, so fp64 trajectories are bit-identical to the
 # CPU restatement (oracle/), which is compiled the same way.
