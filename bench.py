@@ -53,7 +53,7 @@ def workload(name, grid_n):
         return (builders.setup_sphere_scene(builders.random_sphere_list(40)), scene.grid(n, n, n, 1.0, 1.0, 1.0),
                 scene.uniform_source((-1.0, -1.0, 0.9999999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0)),
                 [], f"M2 sphere_scene (res/sphere.toml): 40 random spheres n=1.37, uniform source z=0.9999999, "
-                f"{n}^3 grid (setupGeometry.f90:250-294)", 12_800_000)
+                f"{n}^3 grid (setupGeometry.f90:250-294)", 25_600_000)
     if name == "m3":
         n = grid_n or 128
         return (builders.setup_tran_and_jacques(), scene.grid(n, n, n, 1.0, 1.0, 1.0),
@@ -557,6 +557,10 @@ def main():
                          "fold_interval_ms_per_launch": dep_ms,
                          "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) * per_rank / launches,
                          "sdf_evals_per_photon": sdf_evals / (args.steps * B),
+                         # march steps the far-field march took: counted above as
+                         # the reference's deposits and SDF evaluations, done without a record or a
+                         # full EVAL
+                         "far_march_steps_per_launch": kt.get("far_steps", 0) / launches,
                          "note": "the transport kernel is bound by fp64 VALU issue and divergence, not by "
                                  "HBM: see valu_roofline / fp64_roofline and DESIGN.md §4.2"},
             "fp64_roofline": fp64_roofline(sc, sdf_evals / launches, kern_ms),
