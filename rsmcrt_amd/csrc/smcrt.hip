@@ -1538,11 +1538,20 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   };
   release();
   const uint64_t cap = chunks * CHUNK_RECORDS;
-  // small pools run MAX_SLOTS deep (SMCRT_SLOTS=2 keeps two), large ones two
+  // pools run MAX_SLOTS deep while MAX_SLOTS of them fit in 60 % of the device's memory (at
+  // least DEEP_SLOT_BYTES each; SMCRT_DEEP_SLOT_GIB overrides the size, SMCRT_SLOTS=2 keeps
+  // two), larger ones two: tail-bound scenes need the depth to fill the CUs a launch's last
+  // photons leave idle
   {
     const char* ns = std::getenv("SMCRT_SLOTS");
     const int want = ns && std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS;
-    s->n_slots = cap * 8 <= DEEP_SLOT_BYTES ? want : 2;
+    uint64_t deep = DEEP_SLOT_BYTES;
+    size_t mfree = 0, mtotal = 0;
+    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess)
+      deep = std::max<uint64_t>(deep, (uint64_t)(0.6 * (double)mtotal) / MAX_SLOTS);
+    const char* dg = std::getenv("SMCRT_DEEP_SLOT_GIB");
+    if (dg) deep = (uint64_t)std::strtoull(dg, nullptr, 10) << 30;
+    s->n_slots = cap * 8 <= deep ? want : 2;
     s->slot = 0;    // (the device is idle here: every slot and stream is free)
     s->lturn = 0;
     s->last_slot = -1;
