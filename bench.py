@@ -25,6 +25,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# eight hardware queues for the scene's streams, set before torch starts the HIP runtime
+# (rsmcrt_amd/__init__.py explains; a caller's own setting wins)
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 WORKLOADS = ("m0", "m1", "m2", "m3", "m4", "m5", "escape")
 
@@ -552,9 +555,12 @@ def main():
                          "deposits_per_photon": deposits / (args.steps * B),
                          # the HIP-event interval from a launch's end to its fold's end: the fold
                          # kernels (bk_scan, bk_place, bk_reduce) wait for CU slots behind the next
-                         # persistent launch, so this is mostly queueing, not fold work (the fold's
-                         # busy time is bk_reduce's ~7.5 ms in the committed rocprofv3 trace)
+                         # persistent launch, so this is mostly queueing, not fold work
                          "fold_interval_ms_per_launch": dep_ms,
+                         # the fold's own work: bk_reduce's workgroup run times (in-kernel wall
+                         # clock) summed and divided by the CU count, i.e. the whole-chip time the
+                         # fold takes from the transport kernel per launch
+                         "fold_cu_ms_per_launch": kt.get("fold_cu_ms", 0.0) / launches,
                          "wave_iterations_per_launch": float(cdelta[abi.CTR["wave_iters"]]) * per_rank / launches,
                          "sdf_evals_per_photon": sdf_evals / (args.steps * B),
                          # march steps the far-field march took: counted above as

@@ -128,6 +128,7 @@ module smcrt_mod
     type, bind(C) :: smcrt_kernel_times
         real(c_double)     :: transport_ms = 0._c_double, deposit_ms = 0._c_double
         integer(c_int64_t) :: launches = 0, lean_launches = 0, far_steps = 0
+        real(c_double)     :: fold_cu_ms = 0._c_double
     end type smcrt_kernel_times
 
     interface

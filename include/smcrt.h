@@ -360,6 +360,10 @@ typedef struct smcrt_kernel_times {
                             the lean kernel (Fresnel-free, detector-free scenes) */
   int64_t far_steps;     /* march steps taken by the far-field march (long sphere-tracing runs with
                             only the nearest SDF re-evaluated) since the last query */
+  double fold_cu_ms;     /* the deposit fold's own work since the last query: the sum of its reduce
+                            workgroups' run times divided by the CU count (one workgroup fills a CU),
+                            i.e. the whole-chip time it took, without the time it queued behind
+                            transport launches (which deposit_ms includes) */
 } smcrt_kernel_times;
 
 int smcrt_scene_set_timing(smcrt_scene* scene, int32_t enable);

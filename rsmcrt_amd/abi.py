@@ -193,7 +193,7 @@ class PackLayout(C.Structure):
 
 class KernelTimes(C.Structure):
     _fields_ = [("transport_ms", C.c_double), ("deposit_ms", C.c_double), ("launches", C.c_int64),
-                ("lean_launches", C.c_int64), ("far_steps", C.c_int64)]
+                ("lean_launches", C.c_int64), ("far_steps", C.c_int64), ("fold_cu_ms", C.c_double)]
 
 
 EXPORTED_SYMBOLS = [

@@ -619,7 +619,10 @@ __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __re
                                                   const uint32_t* __restrict__ bucket_fill,
                                                   const Piece* __restrict__ pieces,
                                                   const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
-                                                  double* __restrict__ jmean) {
+                                                  double* __restrict__ jmean, unsigned long long* __restrict__ busy) {
+  // busy: a running total of this kernel's workgroup run times (wall-clock counter ticks), so
+  // the host reports the fold's own work, not the time it queues behind transport launches
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
   __shared__ double acc[TILE_VOXELS];
   // bucket ids and fills of a stage, double-buffered: the next stage's ids are loaded while
   // this stage's records are summed, and one barrier per stage suffices
@@ -673,6 +676,7 @@ __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __re
     }
     __syncthreads();
   }
+  if (threadIdx.x == 0 && busy) atomicAdd(busy, __builtin_amdgcn_s_memrealtime() - t_start);
 }
 
 // ---- bin_reduce: one tile piece per block, fp64 LDS sums added into jmean ----------------

@@ -894,6 +894,10 @@ struct smcrt_scene {
   // the running total of its steps is d_queue[MAX_SLOTS + 1]
   double fm_err = 0.0, fm_step = 0.0;
   unsigned long long far_reported = 0;
+  // the fold's workgroup run time: d_queue[MAX_SLOTS + 2] running total (s_memrealtime ticks at
+  // wall_khz), reported per CU (one bk_reduce workgroup fills a CU)
+  unsigned long long fold_ticks_reported = 0;
+  int wall_khz = 100000, n_cus = 256;
   // exact SDF culling (cull.h): grid + lists + the always-evaluated program, one allocation
   CullGrid* d_cull = nullptr;
   void* d_cull_data = nullptr;
@@ -1259,13 +1263,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
-      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 2)) ||
+      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 3)) ||
       (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
     return cleanup_fail(st);
   hipError_t e = hipSuccess;
-  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 2) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 3) * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemcpy(s->d_nodes, nodes, sizeof(smcrt_sdf_node) * n_nodes, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_prog, prog.data(), sizeof(ProgOp) * prog.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !ctab.empty()) {
@@ -1335,9 +1339,20 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
       if (hipFuncSetAttribute((const void*)bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)s->scatter_lds) != hipSuccess)
         return cleanup_fail(fail(SMCRT_ERR_HIP, "bin_scatter LDS attribute"));
+      // The fold stream gets the highest priority (SMCRT_FOLD_PRIO=0: normal). At the default
+      // priority HIP maps it onto one of the process's shared hardware queues (4 by default),
+      // behind a launch stream's persistent transport kernels, and a fold waited ~60 ms for
+      // them; a high-priority stream has its own queue, and its
+      // workgroups are dispatched first when a CU frees.
+      const char* fp = std::getenv("SMCRT_FOLD_PRIO");
+      int prio_least = 0, prio_greatest = 0;
+      const bool fold_prio = !(fp && fp[0] == '0') &&
+                             hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) == hipSuccess &&
+                             prio_greatest != prio_least;
       bool ok = hipHostMalloc((void**)&s->h_ctl, 8 * MAX_SLOTS * sizeof(uint32_t)) == hipSuccess &&
                 hipEventCreateWithFlags(&s->ev_t, hipEventDisableTiming) == hipSuccess &&
-                hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking) == hipSuccess;
+                (fold_prio ? hipStreamCreateWithPriority(&s->fstream, hipStreamNonBlocking, prio_greatest)
+                           : hipStreamCreateWithFlags(&s->fstream, hipStreamNonBlocking)) == hipSuccess;
       for (int i = 0; ok && i < MAX_SLOTS; ++i)
         ok = hipEventCreateWithFlags(&s->ctl_ev[i], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&s->ev_f[i], hipEventDisableTiming) == hipSuccess;
@@ -1380,6 +1395,11 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     s->lean_ok = ok && s->lean_mode != 0;
   }
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+  s->n_cus = cus;
+  {
+    int khz = 0;  // s_memrealtime's rate
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) s->wall_khz = khz;
+  }
   if (s->lean_ok) {
     hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lean_fn(s), 256, lean_lds(s));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
@@ -1656,7 +1676,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
       hipLaunchKernelGGL(bk_place, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_bucket_tile[sl], s->d_dep_ctl[sl],
                          K.n_buckets, s->n_tiles, s->d_tile_count, s->d_order);
       hipLaunchKernelGGL(bk_reduce, dim3(1024), dim3(1024), 0, fs, s->d_pool[sl], s->d_order, s->d_chunk_fill[sl],
-                         s->d_pieces, s->d_dep_ctl[sl], nv, Ch.jmean);
+                         s->d_pieces, s->d_dep_ctl[sl], nv, Ch.jmean, s->d_queue + MAX_SLOTS + 2);
     } else {
     if (!K.hist_tiles)  // else the transport kernel built the counts
       hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_pool[sl], s->d_chunk_fill[sl],
@@ -2120,6 +2140,10 @@ int smcrt_scene_kernel_times(smcrt_scene* s, smcrt_kernel_times* out) {
   HIPCHK(hipMemcpy(&far, s->d_queue + MAX_SLOTS + 1, sizeof(far), hipMemcpyDeviceToHost));
   out->far_steps = (int64_t)(far - s->far_reported);
   s->far_reported = far;
+  unsigned long long ticks = 0;  // bk_reduce workgroup run time (running total, wall-clock ticks)
+  HIPCHK(hipMemcpy(&ticks, s->d_queue + MAX_SLOTS + 2, sizeof(ticks), hipMemcpyDeviceToHost));
+  out->fold_cu_ms = (double)(ticks - s->fold_ticks_reported) / (double)s->wall_khz / (double)s->n_cus;
+  s->fold_ticks_reported = ticks;
   s->t_transport = s->t_deposit = 0.0;
   s->t_launches = 0;
   return SMCRT_OK;

@@ -253,7 +253,8 @@ class Engine:
         t = abi.KernelTimes()
         _check(load_library().smcrt_scene_kernel_times(self._h, C.byref(t)))
         return {"transport_ms": t.transport_ms, "deposit_ms": t.deposit_ms, "launches": t.launches,
-                "lean_launches": t.lean_launches, "far_steps": t.far_steps}
+                "lean_launches": t.lean_launches, "far_steps": t.far_steps,
+                "fold_cu_ms": t.fold_cu_ms}
 
 
 def pack_layout(grid, n_det_bins: int, fields: int) -> abi.PackLayout:

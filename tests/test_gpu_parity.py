@@ -773,6 +773,8 @@ def test_lean_kernel_paths(monkeypatch, case):
             runs[lean] = eng.run(src, n, seed=SEED, flags=flags, records=True)
             kt = eng.kernel_times()
         assert (kt["lean_launches"] > 0) == (lean == "1"), (lean, kt)
+        if lean == "1":  # the lean kernel runs only on the bucketed path: bk_reduce ran and was timed
+            assert 0.0 < kt["fold_cu_ms"] < 1e3, kt
     cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True)
     for r in runs.values():
         compare(r, cpu)
