@@ -249,11 +249,9 @@ contains
         integer(c_int32_t), intent(in) :: op
         real(c_double), optional, intent(in) :: k
         type(smcrt_sdf) :: s
-        integer :: i
         if (size(array) < 1) error stop "smcrt_model: a model needs at least one SDF"
-        do i = 1, size(array)
-            if (array(i)%node%kind == SMCRT_SDF_MODEL) error stop "smcrt_model: nested models are not supported"
-        end do
+        ! (a child may be a model again, as in the reference; smcrt_scene_create accepts three
+        ! levels of models)
         s%node%kind = SMCRT_SDF_MODEL
         s%node%op = op
         s%node%transform = reshape(smcrt_identity(), [16])
@@ -266,37 +264,48 @@ contains
     end function smcrt_model
 
     ! ------------------------------------------------------------ flattening ---------------
-    integer function smcrt_count_nodes(array) result(n)
+    recursive integer function smcrt_count_nodes(array) result(n)
         type(smcrt_sdf), intent(in) :: array(:)
         integer :: i
         n = size(array)
         do i = 1, size(array)
-            if (allocated(array(i)%children)) n = n + size(array(i)%children)
+            if (allocated(array(i)%children)) n = n + smcrt_count_nodes(array(i)%children)
         end do
     end function smcrt_count_nodes
 
     !> The SDF array as smcrt_scene_create wants it: the top-level SDFs first, in array order
     !> (top(i) = i-1), then each model's children in a contiguous run after them
-    !> (first_child, 0-based). This is the order the C++ front end and rsmcrt_amd.scene use.
+    !> (first_child, 0-based), a nested model's children after its own run. For models of
+    !> primitives this is the order the C++ front end and rsmcrt_amd.scene use.
     subroutine smcrt_flatten(array, nodes, top)
         type(smcrt_sdf), intent(in) :: array(:)
         type(smcrt_sdf_node), allocatable, intent(out) :: nodes(:)
         integer(c_int32_t), allocatable, intent(out) :: top(:)
-        integer :: i, j, k
+        integer :: i, k
         allocate(nodes(smcrt_count_nodes(array)), top(size(array)))
-        k = size(array)  ! next free slot, 0-based
         do i = 1, size(array)
             top(i) = int(i - 1, c_int32_t)
-            nodes(i) = array(i)%node
-            if (array(i)%node%kind == SMCRT_SDF_MODEL) then
-                nodes(i)%first_child = int(k, c_int32_t)
-                nodes(i)%n_children = int(size(array(i)%children), c_int32_t)
-                do j = 1, size(array(i)%children)
-                    nodes(k + j) = array(i)%children(j)%node
-                end do
-                k = k + size(array(i)%children)
-            end if
         end do
+        k = size(array)  ! next free slot, 0-based
+        call place(array, 0)
+    contains
+        recursive subroutine place(a, base)
+            type(smcrt_sdf), intent(in) :: a(:)
+            integer, intent(in) :: base  ! 0-based slot of a(1)
+            integer :: j, first
+            do j = 1, size(a)
+                nodes(base + j) = a(j)%node
+            end do
+            do j = 1, size(a)
+                if (a(j)%node%kind == SMCRT_SDF_MODEL) then
+                    first = k
+                    nodes(base + j)%first_child = int(first, c_int32_t)
+                    nodes(base + j)%n_children = int(size(a(j)%children), c_int32_t)
+                    k = k + size(a(j)%children)
+                    call place(a(j)%children, first)
+                end if
+            end do
+        end subroutine place
     end subroutine smcrt_flatten
 
     ! ------------------------------------------------------------ detectors ----------------

@@ -96,10 +96,9 @@ Bound top_bound(const smcrt_sdf_node* nodes, int32_t n_nodes, int32_t idx) {
   Bound none;
   if (nd.n_children < 1 || nd.first_child < 0 || nd.first_child + nd.n_children > n_nodes) return none;
   std::vector<Bound> ch;
-  for (int32_t c = 0; c < nd.n_children; ++c) {
+  for (int32_t c = 0; c < nd.n_children; ++c) {  // (a nested model: its own bound)
     const smcrt_sdf_node& cn = nodes[nd.first_child + c];
-    if (cn.kind == SMCRT_SDF_MODEL) return none;
-    ch.push_back(prim_bound(cn));
+    ch.push_back(cn.kind == SMCRT_SDF_MODEL ? top_bound(nodes, n_nodes, nd.first_child + c) : prim_bound(cn));
   }
   switch (nd.op) {
     case SMCRT_OP_UNION: {  // min of the children
@@ -131,7 +130,7 @@ double top_value(const smcrt_sdf_node* nodes, int32_t idx, V3 q) {
   if (nd.kind != SMCRT_SDF_MODEL) return sdf_prim(&nd, q, false);
   double acc = 0.0;
   for (int32_t c = 0; c < nd.n_children; ++c) {
-    const double v = sdf_prim(&nodes[nd.first_child + c], q, false);
+    const double v = top_value(nodes, nd.first_child + c, q);
     acc = c == 0 ? v : csg(nd.op, acc, v, nd.k);
   }
   return acc;

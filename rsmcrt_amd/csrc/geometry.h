@@ -165,14 +165,38 @@ enum : int32_t {
   PROG_CHILD_FIRST = 1, // first child of a model: acc = d
   PROG_CHILD = 2,       // later child: acc = op(acc, d)
 };
+// Nested models (a model among a model's children: eval_model recurses through
+// array(i)%value%evaluate, sdf_base.f90:146-161). A top-level model's direct primitives keep
+// PROG_CHILD_FIRST / PROG_CHILD (accumulator 0). Every other op of a nested fold is
+// PROG_NEST | depth << 4 | kind (| PROG_POP): it folds into accumulator `depth` (0 = the top's,
+// 1 and 2 = ProgAcc); a PROG_POP op folds the finished child model in accumulator depth + 1
+// into accumulator depth in place of its primitive (whose node is evaluated and ignored).
+// Three levels of models are supported; deeper nesting is rejected at scene creation.
+enum : int32_t { PROG_POP = 4, PROG_NEST = 8 };
+constexpr int PROG_MAX_DEPTH = 3;
+struct ProgAcc {
+  double a1 = 0.0, a2 = 0.0;
+};
+
 struct ProgOp {
   int32_t node;   // primitive node index
-  int32_t action; // PROG_*
+  int32_t action; // PROG_* (| PROG_NEST ...)
   int32_t top;    // 1-based top-level index completed by this op (0 if none)
   int32_t op;     // CSG op for PROG_CHILD
   double k;       // CSG parameter
   int32_t translate_only;  // the node's transform is a pure translation (see sdf_prim)
   int32_t pad;
 };
+
+// One op of a nested fold (see PROG_NEST): the model's `op` and `k` applied as eval_model
+// does, acc = op(acc, value) after the first child.
+__host__ __device__ __forceinline__ void prog_nested(const ProgOp& op, double v, double& acc, ProgAcc& n) {
+  const int32_t d = (op.action >> 4) & 3;
+  const double x = (op.action & PROG_POP) ? (d == 0 ? n.a1 : n.a2) : v;
+  const bool first = (op.action & 3) != PROG_CHILD;
+  if (d == 0) acc = first ? x : csg(op.op, acc, x, op.k);
+  else if (d == 1) n.a1 = first ? x : csg(op.op, n.a1, x, op.k);
+  else n.a2 = first ? x : csg(op.op, n.a2, x, op.k);
+}
 
 }  // namespace smcrt

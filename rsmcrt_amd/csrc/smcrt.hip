@@ -15,6 +15,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/smcrt.h"
@@ -1135,10 +1136,23 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
         return fail(SMCRT_ERR_INVALID_ARG, "model node " + std::to_string(i) + ": bad child range");
       if (nd.op < SMCRT_OP_UNION || nd.op > SMCRT_OP_INTERSECTION)
         return fail(SMCRT_ERR_INVALID_ARG, "model node " + std::to_string(i) + ": bad CSG op");
-      for (int32_t c = 0; c < nd.n_children; ++c)
-        if (nodes[nd.first_child + c].kind == SMCRT_SDF_MODEL)
-          return fail(SMCRT_ERR_UNSUPPORTED, "nested models are not supported");
     }
+  }
+  // models nested at most PROG_MAX_DEPTH levels (geometry.h PROG_NEST); this also rejects
+  // a model that contains itself
+  {
+    std::function<int(int32_t, int)> depth_ok = [&](int32_t idx, int lvl) -> int {
+      const smcrt_sdf_node& nd = nodes[idx];
+      if (nd.kind != SMCRT_SDF_MODEL) return 1;
+      if (lvl >= PROG_MAX_DEPTH) return 0;
+      for (int32_t c = 0; c < nd.n_children; ++c)
+        if (!depth_ok(nd.first_child + c, lvl + 1)) return 0;
+      return 1;
+    };
+    for (int32_t i = 0; i < n_top; ++i)
+      if (top[i] >= 0 && top[i] < n_nodes && !depth_ok(top[i], 0))
+        return fail(SMCRT_ERR_UNSUPPORTED, "top " + std::to_string(i) + ": models nested more than " +
+                                               std::to_string(PROG_MAX_DEPTH) + " levels deep are not supported");
   }
   for (int32_t i = 0; i < n_top; ++i)
     if (top[i] < 0 || top[i] >= n_nodes) return fail(SMCRT_ERR_INVALID_ARG, "top index out of range");
@@ -1194,10 +1208,27 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (nd.kind != SMCRT_SDF_MODEL) {
       prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0, translate_only(top[i]), 0});
     } else {
-      for (int32_t c = 0; c < nd.n_children; ++c)
-        prog.push_back(ProgOp{nd.first_child + c, c == 0 ? PROG_CHILD_FIRST : PROG_CHILD,
-                              c == nd.n_children - 1 ? i + 1 : 0, nd.op, nd.k,
-                              translate_only(nd.first_child + c), 0});
+      // eval_model's left fold, children in order; a child model folds into the next
+      // accumulator and a PROG_POP op then folds its value into this one (geometry.h)
+      int32_t last_prim = -1;
+      std::function<void(const smcrt_sdf_node&, int, int32_t)> flat = [&](const smcrt_sdf_node& m, int d,
+                                                                        int32_t done_top) {
+        for (int32_t c = 0; c < m.n_children; ++c) {
+          const int32_t ci = m.first_child + c;
+          const int32_t kind = c == 0 ? PROG_CHILD_FIRST : PROG_CHILD;
+          const int32_t t = c == m.n_children - 1 ? done_top : 0;
+          if (nodes[ci].kind != SMCRT_SDF_MODEL) {
+            last_prim = ci;
+            const int32_t action = d == 0 ? kind : (PROG_NEST | (d << 4) | kind);
+            prog.push_back(ProgOp{ci, action, t, m.op, m.k, translate_only(ci), 0});
+          } else {
+            flat(nodes[ci], d + 1, 0);
+            prog.push_back(ProgOp{last_prim, PROG_NEST | PROG_POP | (d << 4) | kind, t, m.op, m.k,
+                                  translate_only(last_prim), 0});
+          }
+        }
+      };
+      flat(nd, 0, i + 1);
     }
   }
   s->n_prog = (int)prog.size();
@@ -1559,12 +1590,14 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   release();
   const uint64_t cap = chunks * CHUNK_RECORDS;
   // pools run MAX_SLOTS deep while MAX_SLOTS of them fit in 60 % of the device's memory (at
-  // least DEEP_SLOT_BYTES each; SMCRT_DEEP_SLOT_GIB overrides the size, SMCRT_SLOTS=2 keeps
-  // two), larger ones two: tail-bound scenes need the depth to fill the CUs a launch's last
-  // photons leave idle
+  // least DEEP_SLOT_BYTES each; SMCRT_DEEP_SLOT_GIB overrides the size), larger ones two:
+  // tail-bound scenes need the depth to fill the CUs a launch's last photons leave idle. Scenes
+  // of the lean kernel keep two (its launches have short tails; with eight hardware queues,
+  // i.e. launches really four deep, M1 ran 207 vs 197 M photons/s at two, same box,
+  // profiles/r03_s3/hwq_slots_ab.txt). SMCRT_SLOTS=2 / =4 overrides.
   {
     const char* ns = std::getenv("SMCRT_SLOTS");
-    const int want = ns && std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS;
+    const int want = ns ? (std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS) : (s->lean_ok ? 2 : MAX_SLOTS);
     uint64_t deep = DEEP_SLOT_BYTES;
     size_t mfree = 0, mtotal = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess)

@@ -96,3 +96,32 @@ def test_no_oracle_in_product():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dp, f)).read()
                 assert not pat.search(txt), f
+
+
+def _nested(levels):
+    """One top: `levels` models nested in each other around two spheres, plus a medium box."""
+    from rsmcrt_amd.scene import Scene, box, invert, model, mono, sphere, translate
+    o = mono(5.0, 0.1, 0.8, 1.0)
+    s = model([sphere(0.3, o, 1), sphere(0.2, o, 1, transform=invert(translate((0.2, 0.0, 0.0))))], abi.OP_UNION)
+    for _ in range(levels - 1):
+        s = model([s, sphere(0.1, o, 1, transform=invert(translate((0.0, 0.3, 0.0))))], abi.OP_SMOOTH_UNION, 0.05)
+    return Scene([s, box((1.0, 1.0, 1.0), mono(1.0, 0.01, 0.0, 1.0), 2)])
+
+
+def test_nested_model_depth_checked_before_the_device(lib_path):
+    """Nested models (eval_model's recursion, sdf_base.f90:146-161) are accepted up to three
+    levels (geometry.h PROG_NEST); a fourth level is rejected with UNSUPPORTED before any
+    device call, so both are checkable without a GPU."""
+    from rsmcrt_amd import engine, scene
+    L = engine.load_library(lib_path)
+    g = scene.grid(8, 8, 8, 1, 1, 1)
+    for levels, want in ((3, (abi.OK, abi.ERR_NO_DEVICE)), (4, (abi.ERR_UNSUPPORTED,))):
+        sc = _nested(levels)
+        h = C.c_void_p()
+        st = L.smcrt_scene_create(sc.node_array(), len(sc.nodes), sc.top_array(), sc.n_top, C.byref(g), None, 0, 0,
+                                  C.byref(h))
+        assert st in want, (levels, st, L.smcrt_last_error())
+        if st == abi.OK:
+            L.smcrt_scene_destroy(h)
+        if levels == 4:
+            assert b"nested" in L.smcrt_last_error()

@@ -574,6 +574,53 @@ def test_coop_eval_models_and_many_tops():
     assert cpu.counter("fresnel") > 0
 
 
+def _nested_models(lay, opt_m):
+    """Models nested two and three levels deep (eval_model recursing into a child model,
+    sdf_base.f90:146-161), with every CSG op at some level."""
+    from rsmcrt_amd.scene import box, capsule, cylinder, invert, model, sphere, torus, translate
+    t = lambda c: invert(translate(c))  # noqa: E731
+    inner = model([sphere(0.1, opt_m, lay(), transform=t((0.3, 0.3, 0.3))),
+                   box((0.08, 0.08, 0.08), opt_m, lay(), transform=t((0.35, 0.3, 0.3)))], abi.OP_INTERSECTION)
+    two = model([model([capsule((0.2, 0.2, 0.3), (0.4, 0.4, 0.3), 0.03, opt_m, lay()),
+                        sphere(0.06, opt_m, lay(), transform=t((0.2, 0.4, 0.3)))], abi.OP_SMOOTH_UNION, 0.04),
+                 inner,
+                 sphere(0.04, opt_m, lay(), transform=t((0.4, 0.2, 0.3)))], abi.OP_UNION)
+    three = model([model([model([sphere(0.12, opt_m, lay(), transform=t((-0.3, -0.3, -0.2))),
+                                 sphere(0.09, opt_m, lay(), transform=t((-0.22, -0.3, -0.2)))], abi.OP_SUBTRACTION),
+                          torus(0.1, 0.02, opt_m, lay(), transform=t((-0.3, -0.3, -0.1)))], abi.OP_SMOOTH_UNION, 0.03),
+                   cylinder((-0.3, -0.45, -0.2), (-0.3, -0.15, -0.2), 0.03, opt_m, lay())], abi.OP_UNION)
+    return [two, three]
+
+
+@pytest.mark.parametrize("path", ["serial", "coop", "culled"])
+def test_nested_models(path):
+    """Models inside models (geometry.h PROG_NEST: one accumulator per level, a pop op folds a
+    finished child model into its parent) through each EVAL path: serial (3 tops), the
+    cooperative tail EVAL (>= 8 tops) and the culled EVAL (>= 16 boundable tops: the nested
+    models' bounds come from their children's, cull.cpp). Fresnel at every nested surface
+    (n differs). Photon records, counters and grids bit-exact against the oracle, whose
+    eval_model recursion is the reference's."""
+    from rsmcrt_amd.scene import Scene, box, invert, mono, sphere, translate
+    sdfs = []
+    lay = lambda: len(sdfs) + 1  # noqa: E731
+    opt_m = mono(5.0, 0.2, 0.5, 1.45)
+    if path == "culled":
+        sc0 = _culling_scene()
+        sdfs = list(sc0.sdfs[:-1])
+    elif path == "coop":
+        for i in range(8):
+            sdfs.append(sphere(0.05, mono(3.0, 0.1, 0.8, 1.2 + 0.02 * i), lay(),
+                               transform=invert(translate((-0.6 + 0.15 * i, 0.5, 0.0)))))
+    for m in _nested_models(lay, opt_m):
+        sdfs.append(m)
+    sdfs.append(box((2.0, 2.0, 2.0), mono(2.0, 0.05, 0.8, 1.0), lay()))
+    sc = Scene(sdfs)
+    src = scene.uniform_source((-1.0, -1.0, 0.999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    gpu, cpu = both(sc, scene.grid(32, 32, 32, 1, 1, 1), src, 3000)
+    compare(gpu, cpu)
+    assert cpu.counter("fresnel") > 0
+
+
 def _culling_scene(seed=7):
     """~60 tops for the culled EVAL (cull.h): random capsules, rotated and translated
     spheres, tori and capped cylinders, smooth-union / intersection / subtraction models, a
