@@ -1591,13 +1591,14 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   const uint64_t cap = chunks * CHUNK_RECORDS;
   // pools run MAX_SLOTS deep while MAX_SLOTS of them fit in 60 % of the device's memory (at
   // least DEEP_SLOT_BYTES each; SMCRT_DEEP_SLOT_GIB overrides the size), larger ones two:
-  // tail-bound scenes need the depth to fill the CUs a launch's last photons leave idle. Scenes
-  // of the lean kernel keep two (its launches have short tails; with eight hardware queues,
-  // i.e. launches really four deep, M1 ran 207 vs 197 M photons/s at two, same box,
-  // profiles/r03_s3/hwq_slots_ab.txt). SMCRT_SLOTS=2 / =4 overrides.
+  // tail-bound scenes (M4, M5) need the depth to fill the CUs a launch's last photons leave
+  // idle. Scenes of the lean kernel and of the far-field march keep two (with eight hardware
+  // queues, i.e. launches really four deep, two slots measured M1 211 vs 194-202 M photons/s
+  // and M2 15.5-16.4 vs 14.3-14.8 M, same box, profiles/r03_s3/hwq_slots_ab.txt).
+  // SMCRT_SLOTS=2 / =4 overrides.
   {
     const char* ns = std::getenv("SMCRT_SLOTS");
-    const int want = ns ? (std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS) : (s->lean_ok ? 2 : MAX_SLOTS);
+    const int want = ns ? (std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS) : (s->lean_ok || s->fm_err > 0.0 ? 2 : MAX_SLOTS);
     uint64_t deep = DEEP_SLOT_BYTES;
     size_t mfree = 0, mtotal = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess)
