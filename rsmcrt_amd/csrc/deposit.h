@@ -614,6 +614,21 @@ __global__ __launch_bounds__(BIN_THREADS) void bk_place(const uint32_t* __restri
 #endif
 constexpr uint32_t REDUCE_STAGE_BUCKETS = SMCRT_RED_STAGE;  // <= 1024 (one id per thread)
 constexpr int RED_UNROLL = SMCRT_RED_UNROLL;                // record loads in flight per thread
+// bk_reduce reads each record once. SMCRT_RED_NT=1 gives the loads the non-temporal hint, meant
+// to keep the fold's 25 GB stream from evicting the partly written bucket lines of the transport
+// kernels beside it: measured and not adopted (M1 same box: 210.0/210.3 vs 210.2/210.6 M
+// photons/s, the transport kernel's HBM writes 38.008 GB per launch either way,
+// profiles/r03_s3/nt_ab.txt), so the write amplification is not the fold's doing
+#ifndef SMCRT_RED_NT
+#define SMCRT_RED_NT 0
+#endif
+__device__ __forceinline__ unsigned long long red_load(const unsigned long long* p) {
+#if SMCRT_RED_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __restrict__ pool,
                                                   const uint32_t* __restrict__ order,
                                                   const uint32_t* __restrict__ bucket_fill,
@@ -654,7 +669,7 @@ __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __re
         for (int k = 0; k < RED_UNROLL; ++k) {
           const uint32_t j = s + k * 1024, kb = j >> BUCKET_SHIFT, r = j & (BUCKET_RECORDS - 1);
           v[k] = r < sfill[kb];
-          x[k] = v[k] ? pool[((uint64_t)sid[kb] << BUCKET_SHIFT) + r] : 0ull;
+          x[k] = v[k] ? red_load(pool + ((uint64_t)sid[kb] << BUCKET_SHIFT) + r) : 0ull;
         }
 #pragma unroll
         for (int k = 0; k < RED_UNROLL; ++k)
@@ -663,7 +678,7 @@ __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __re
       for (; s < slots; s += 1024) {
         const uint32_t kb = s >> BUCKET_SHIFT, r = s & (BUCKET_RECORDS - 1);
         if (r < sfill[kb]) {
-          const unsigned long long x = pool[((uint64_t)sid[kb] << BUCKET_SHIFT) + r];
+          const unsigned long long x = red_load(pool + ((uint64_t)sid[kb] << BUCKET_SHIFT) + r);
           atomicAdd(&acc[(uint32_t)(x >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x));
         }
       }

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 AB_LIBS="base nt0" BENCH_ARGS="--steps 10" bash tools/ab_libs.sh || exit 1
 for v in base nt0; do
   if [ $v = base ]; then unset SMCRT_LIB; else export SMCRT_LIB=$PWD/tools/diag_libs/libsmcrt_$v.so; fi
-  PASSES="fetch write" PROF_ARGS="--no-cpu --no-ref --steps 3 --warmup 2" bash tools/profile.sh > /dev/null || exit 1
+  PASSES="trace fetch write" PROF_ARGS="--no-cpu --no-ref --steps 3 --warmup 2" bash tools/profile.sh > /dev/null || exit 1
   echo "== $v"
   python3 tools/prof_summary.py gpurun_out/prof --last 3 --batch 16000000 | grep -E "lean|bk_reduce"
   rm -rf gpurun_out/prof
