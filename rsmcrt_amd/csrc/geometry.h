@@ -166,17 +166,12 @@ enum : int32_t {
   PROG_CHILD = 2,       // later child: acc = op(acc, d)
 };
 // Nested models (a model among a model's children: eval_model recurses through
-// array(i)%value%evaluate, sdf_base.f90:146-161). A top-level model's direct primitives keep
-// PROG_CHILD_FIRST / PROG_CHILD (accumulator 0). Every other op of a nested fold is
-// PROG_NEST | depth << 4 | kind (| PROG_POP): it folds into accumulator `depth` (0 = the top's,
-// 1 and 2 = ProgAcc); a PROG_POP op folds the finished child model in accumulator depth + 1
-// into accumulator depth in place of its primitive (whose node is evaluated and ignored).
-// Three levels of models are supported; deeper nesting is rejected at scene creation.
-enum : int32_t { PROG_POP = 4, PROG_NEST = 8 };
+// array(i)%value%evaluate, sdf_base.f90:146-161). A top-level model's children are ops of the
+// program; a child that is itself a model is one op with PROG_SUB, whose value sdf_submodel
+// folds from the child's own children (which may be models of primitives in turn). Three
+// levels of models are supported; deeper nesting is rejected at scene creation.
+enum : int32_t { PROG_SUB = 8 };
 constexpr int PROG_MAX_DEPTH = 3;
-struct ProgAcc {
-  double a1 = 0.0, a2 = 0.0;
-};
 
 struct ProgOp {
   int32_t node;   // primitive node index
@@ -188,15 +183,36 @@ struct ProgOp {
   int32_t pad;
 };
 
-// One op of a nested fold (see PROG_NEST): the model's `op` and `k` applied as eval_model
-// does, acc = op(acc, value) after the first child.
-__host__ __device__ __forceinline__ void prog_nested(const ProgOp& op, double v, double& acc, ProgAcc& n) {
-  const int32_t d = (op.action >> 4) & 3;
-  const double x = (op.action & PROG_POP) ? (d == 0 ? n.a1 : n.a2) : v;
-  const bool first = (op.action & 3) != PROG_CHILD;
-  if (d == 0) acc = first ? x : csg(op.op, acc, x, op.k);
-  else if (d == 1) n.a1 = first ? x : csg(op.op, n.a1, x, op.k);
-  else n.a2 = first ? x : csg(op.op, n.a2, x, op.k);
+// The value an op contributes: its primitive, or (PROG_SUB) its child model's value, i.e.
+// eval_model's left fold over the child's children, a grandchild model folded from its
+// primitives first. One loop with one sdf_prim site for both (a primitive op is one trip), so
+// the nesting costs the kernels no second inlined copy of the primitives. Nested children are
+// evaluated with their transforms in full (dotmat), which equals sdf_prim's translate-only
+// shortcut bit for bit (see sdf_prim_s).
+__host__ __device__ __forceinline__ double prog_value(const smcrt_sdf_node* __restrict__ nodes, int32_t node,
+                                                      int32_t action, bool translate_only, V3 q) {
+  if (!(action & PROG_SUB)) return sdf_prim(nodes + node, q, translate_only);
+  const smcrt_sdf_node* M = nodes + node;
+  double acc = 0.0, sub = 0.0;
+  int32_t c = 0, g = 0;
+  while (c < M->n_children) {
+    const smcrt_sdf_node* C = nodes + M->first_child + c;
+    const bool cm = C->kind == SMCRT_SDF_MODEL;
+    const double w = sdf_prim(cm ? nodes + C->first_child + g : C, q, false);
+    double v = w;
+    bool child_done = true;
+    if (cm) {
+      sub = g == 0 ? w : csg(C->op, sub, w, C->k);
+      v = sub;
+      child_done = ++g >= C->n_children;
+    }
+    if (child_done) {
+      acc = c == 0 ? v : csg(M->op, acc, v, M->k);
+      ++c;
+      g = 0;
+    }
+  }
+  return acc;
 }
 
 }  // namespace smcrt

@@ -1208,27 +1208,14 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (nd.kind != SMCRT_SDF_MODEL) {
       prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0, translate_only(top[i]), 0});
     } else {
-      // eval_model's left fold, children in order; a child model folds into the next
-      // accumulator and a PROG_POP op then folds its value into this one (geometry.h)
-      int32_t last_prim = -1;
-      std::function<void(const smcrt_sdf_node&, int, int32_t)> flat = [&](const smcrt_sdf_node& m, int d,
-                                                                        int32_t done_top) {
-        for (int32_t c = 0; c < m.n_children; ++c) {
-          const int32_t ci = m.first_child + c;
-          const int32_t kind = c == 0 ? PROG_CHILD_FIRST : PROG_CHILD;
-          const int32_t t = c == m.n_children - 1 ? done_top : 0;
-          if (nodes[ci].kind != SMCRT_SDF_MODEL) {
-            last_prim = ci;
-            const int32_t action = d == 0 ? kind : (PROG_NEST | (d << 4) | kind);
-            prog.push_back(ProgOp{ci, action, t, m.op, m.k, translate_only(ci), 0});
-          } else {
-            flat(nodes[ci], d + 1, 0);
-            prog.push_back(ProgOp{last_prim, PROG_NEST | PROG_POP | (d << 4) | kind, t, m.op, m.k,
-                                  translate_only(last_prim), 0});
-          }
-        }
-      };
-      flat(nd, 0, i + 1);
+      // eval_model's left fold, children in order; a child model is one PROG_SUB op
+      // (geometry.h sdf_submodel)
+      for (int32_t c = 0; c < nd.n_children; ++c) {
+        const int32_t ci = nd.first_child + c;
+        const bool sub = nodes[ci].kind == SMCRT_SDF_MODEL;
+        prog.push_back(ProgOp{ci, (c == 0 ? PROG_CHILD_FIRST : PROG_CHILD) | (sub ? PROG_SUB : 0),
+                              c == nd.n_children - 1 ? i + 1 : 0, nd.op, nd.k, sub ? 0 : translate_only(ci), 0});
+      }
     }
   }
   s->n_prog = (int)prog.size();

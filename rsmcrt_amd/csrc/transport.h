@@ -900,16 +900,14 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
   r.maxloc = 0;
   double best = -__builtin_inf();
   double acc = 0.0;
-  ProgAcc nacc;
   for (int32_t ip = 0; ip < n_prog; ++ip) {
     const ProgOp op = prog[ip];
     // the program is wave-uniform: keep node parameters on the scalar path
     const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-    const double v = sdf_prim(nodes + node, q, op.translate_only != 0);
-    if (op.action == PROG_TOP) acc = v;
-    else if (op.action == PROG_CHILD_FIRST) acc = v;
-    else if (op.action == PROG_CHILD) acc = csg(op.op, acc, v, op.k);
-    else prog_nested(op, v, acc, nacc);
+    const double v = prog_value(nodes, node, op.action, op.translate_only != 0, q);
+    if ((op.action & 3) == PROG_TOP) acc = v;
+    else if ((op.action & 3) == PROG_CHILD_FIRST) acc = v;
+    else acc = csg(op.op, acc, v, op.k);
     if (op.top > 0) {  // a top-level ds(i) is complete
       const double d = acc;
       const int32_t i = op.top;
@@ -945,13 +943,11 @@ __device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restri
     const int32_t b = prog[n_prog + i].node, e = prog[n_prog + i + 1].node;
     if (b == e) continue;  // an empty model never completes its ds(i)
     double acc = 0.0;
-    ProgAcc nacc;
     for (int32_t ip = b; ip < e; ++ip) {
       const ProgOp op = prog[ip];
-      const double v = sdf_prim(nodes + op.node, q, op.translate_only != 0);
-      if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
-      else if (op.action == PROG_CHILD) acc = csg(op.op, acc, v, op.k);
-      else prog_nested(op, v, acc, nacc);
+      const double v = prog_value(nodes, op.node, op.action, op.translate_only != 0, q);
+      if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
+      else acc = csg(op.op, acc, v, op.k);
     }
     const double d = acc;
     const int32_t t = i + 1;
@@ -1091,14 +1087,12 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     const ProgOp* __restrict__ pa = (const ProgOp*)G->prog_always;
     const int32_t na = G->n_prog_always;
     double acc = 0.0;
-    ProgAcc nacc;
     for (int32_t ip = 0; ip < na; ++ip) {
       const ProgOp op = pa[ip];
       const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-      const double v = sdf_prim(nodes + node, q, op.translate_only != 0);
-      if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
-      else if (op.action == PROG_CHILD) acc = csg(op.op, acc, v, op.k);
-      else prog_nested(op, v, acc, nacc);
+      const double v = prog_value(nodes, node, op.action, op.translate_only != 0, q);
+      if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
+      else acc = csg(op.op, acc, v, op.k);
       if (op.top > 0) {
         const double d = acc;
         const double a = fabs(d);
@@ -1127,13 +1121,11 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
       if (en.x & CULL_MODEL) {  // a model: its ops in the flattened program
         const int32_t o0 = prog[n_prog + i].node, o1 = prog[n_prog + i + 1].node;
         double acc = 0.0;
-        ProgAcc nacc;
         for (int32_t ip = o0; ip < o1; ++ip) {
           const ProgOp op = prog[ip];
-          const double v = sdf_prim(nodes + op.node, q, op.translate_only != 0);
-          if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
-          else if (op.action == PROG_CHILD) acc = csg(op.op, acc, v, op.k);
-          else prog_nested(op, v, acc, nacc);
+          const double v = prog_value(nodes, op.node, op.action, op.translate_only != 0, q);
+          if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
+          else acc = csg(op.op, acc, v, op.k);
         }
         d = acc;
       } else {
@@ -1195,14 +1187,12 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
     const ProgOp* __restrict__ pa = (const ProgOp*)G->prog_always;
     const int32_t na = G->n_prog_always;
     double acc = 0.0;
-    ProgAcc nacc;
     for (int32_t ip = 0; ip < na; ++ip) {
       const ProgOp op = pa[ip];
       const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-      const double v = sdf_prim(nodes + node, q, op.translate_only != 0);
-      if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
-      else if (op.action == PROG_CHILD) acc = csg(op.op, acc, v, op.k);
-      else prog_nested(op, v, acc, nacc);
+      const double v = prog_value(nodes, node, op.action, op.translate_only != 0, q);
+      if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
+      else acc = csg(op.op, acc, v, op.k);
       if (op.top > 0) {
         const double d = acc;
         const double a = fabs(d);
@@ -1235,13 +1225,11 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
         if (en.x & CULL_MODEL) {
           const int32_t o0 = prog[n_prog + i].node, o1 = prog[n_prog + i + 1].node;
           double acc = 0.0;
-          ProgAcc nacc;
           for (int32_t ip = o0; ip < o1; ++ip) {
             const ProgOp op = prog[ip];
-            const double v = sdf_prim(nodes + op.node, q, op.translate_only != 0);
-            if (op.action == PROG_TOP || op.action == PROG_CHILD_FIRST) acc = v;
-            else if (op.action == PROG_CHILD) acc = csg(op.op, acc, v, op.k);
-            else prog_nested(op, v, acc, nacc);
+            const double v = prog_value(nodes, op.node, op.action, op.translate_only != 0, q);
+            if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
+            else acc = csg(op.op, acc, v, op.k);
           }
           d = acc;
         } else {
