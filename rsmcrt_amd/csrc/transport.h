@@ -1073,6 +1073,9 @@ __device__ __forceinline__ EvalOut eval_coop_tab(const double* ct, int32_t n_top
 // fallbacks [3] list entries walked [4] wave-EVALs [5] wave-EVALs with a full fallback
 __device__ unsigned long long g_cull_diag[6];
 #endif
+#ifndef SMCRT_CULL_PREFETCH
+#define SMCRT_CULL_PREFETCH 1
+#endif
 __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict__ nodes,
                                                const ProgOp* __restrict__ prog, int32_t n_prog,
                                                const CullGrid* __restrict__ G, V3 q, bool have, bool mask_le,
@@ -1114,8 +1117,18 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     const uint32_t c = (uint32_t)ix + (uint32_t)G->n[0] * ((uint32_t)iy + (uint32_t)G->n[1] * (uint32_t)iz);
     const uint32_t b = G->off[c], e = G->off[c + 1];
     const uint2* __restrict__ ent = (const uint2*)G->list;
+#if SMCRT_CULL_PREFETCH
+    // the next entry's load is issued before this entry's SDF, so the list walk pays one
+    // memory latency per entry (the node's) instead of two
+    uint2 nxt = b < e ? ent[b] : make_uint2(0u, 0u);
+#endif
     for (uint32_t k = b; k < e; ++k) {  // per lane: its cell's tops, ascending
+#if SMCRT_CULL_PREFETCH
+      const uint2 en = nxt;
+      if (k + 1 < e) nxt = ent[k + 1];
+#else
       const uint2 en = ent[k];
+#endif
       const int32_t i = (int32_t)(en.x & CULL_TOP_MASK);
       double d;
       if (en.x & CULL_MODEL) {  // a model: its ops in the flattened program
