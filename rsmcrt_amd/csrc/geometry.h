@@ -189,8 +189,12 @@ struct ProgOp {
 // the nesting costs the kernels no second inlined copy of the primitives. Nested children are
 // evaluated with their transforms in full (dotmat), which equals sdf_prim's translate-only
 // shortcut bit for bit (see sdf_prim_s).
+// NEST = false (every kernel but the general instantiation, which scenes with nested models
+// always use, smcrt.hip) compiles only the primitive.
+template <bool NEST>
 __host__ __device__ __forceinline__ double prog_value(const smcrt_sdf_node* __restrict__ nodes, int32_t node,
                                                       int32_t action, bool translate_only, V3 q) {
+  if constexpr (!NEST) return sdf_prim(nodes + node, q, translate_only);
   if (!(action & PROG_SUB)) return sdf_prim(nodes + node, q, translate_only);
   const smcrt_sdf_node* M = nodes + node;
   double acc = 0.0, sub = 0.0;

@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
       } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)
         R = eval_culled(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj);
       } else {
-        R = eval_sdfs(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
+        R = eval_sdfs<XSRC>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }
       // packet%cnts counts the evaluations of tauint2's ds/dsNew arrays only (inttau2.f90:67,83,
       // 138,183,219,232): not the initial layer search, the Fresnel ds lookups or calcNormal.
@@ -838,7 +838,7 @@ __global__ __launch_bounds__(256) void classify_kernel(const smcrt_sdf_node* __r
        i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t j = i < n ? i : n - 1;  // whole waves walk the program together
     const V3 q = v3(pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]);
-    const EvalOut r = eval_sdfs(nodes, prog, n_prog, q, false, 0, 0);
+    const EvalOut r = eval_sdfs<true>(nodes, prog, n_prog, q, false, 0, 0);
     if (i < n) layer[i] = r.maxloc;
   }
 }
@@ -895,6 +895,10 @@ struct smcrt_scene {
   // the running total of its steps is d_queue[MAX_SLOTS + 1]
   double fm_err = 0.0, fm_step = 0.0;
   unsigned long long far_reported = 0;
+  // a top model has a model among its children: only the general instantiation evaluates
+  // nested models (geometry.h PROG_SUB), so such scenes always run it, with the serial EVAL
+  // (no cooperative, culled or lean paths)
+  bool nested = false;
   // the fold's workgroup run time: d_queue[MAX_SLOTS + 2] running total (s_memrealtime ticks at
   // wall_khz), reported per CU (one bk_reduce workgroup fills a CU)
   unsigned long long fold_ticks_reported = 0;
@@ -1224,7 +1228,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     prog.push_back(ProgOp{top_first[i], PROG_TOP, 0, 0, 0.0, 0, 0});
   // A sparse wave evaluates its lanes' SDF arrays one lane at a time across the wave when
   // that is cheaper than the serial per-lane chain over all n_top tops (transport.h).
-  s->coop_lanes = n_top >= 8 ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
+  for (const ProgOp& op : prog) s->nested = s->nested || (op.action & PROG_SUB) != 0;
+  s->coop_lanes = n_top >= 8 && !s->nested ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
   // The cooperative EVAL's LDS table: at most 64 tops, none of them a model (transport.h).
   // SMCRT_COOP_TAB=0 keeps the global-memory cooperative EVAL.
   std::vector<double> ctab;
@@ -1410,7 +1415,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     ok = ok && lean_lds(s) + sizeof(LeanShared) <= 65536;
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
-    s->lean_ok = ok && s->lean_mode != 0;
+    s->lean_ok = ok && s->lean_mode != 0 && !s->nested;
   }
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   s->n_cus = cus;
@@ -1789,7 +1794,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   if (cfg->n_photons == 0) return SMCRT_OK;
   // sources other than point/uniform/pencil, a sampled spectrum or batched origins: the
   // general emitter
-  const bool xsrc = src_needs_plan(src) || orun;
+  const bool xsrc = src_needs_plan(src) || orun || s->nested;
   SrcPlan plan;
   std::memset(&plan, 0, sizeof plan);
   if (xsrc) {

@@ -890,6 +890,9 @@ struct EvalOut {
 
 // `nodes` and `prog` must come from `const __restrict__` kernel parameters: that is what lets
 // the compiler prove them unclobbered and keep the wave-uniform loads on the scalar path.
+// NEST: the program may hold nested-model ops (PROG_SUB); only the general instantiation
+// evaluates such scenes (smcrt.hip), so every other caller compiles without them.
+template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ nodes,
                                              const ProgOp* __restrict__ prog, int32_t n_prog, V3 q,
                                              bool mask_le, int32_t capi, int32_t capj) {
@@ -904,7 +907,7 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
     const ProgOp op = prog[ip];
     // the program is wave-uniform: keep node parameters on the scalar path
     const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-    const double v = prog_value(nodes, node, op.action, op.translate_only != 0, q);
+    const double v = prog_value<NEST>(nodes, node, op.action, op.translate_only != 0, q);
     if ((op.action & 3) == PROG_TOP) acc = v;
     else if ((op.action & 3) == PROG_CHILD_FIRST) acc = v;
     else acc = csg(op.op, acc, v, op.k);
@@ -945,7 +948,7 @@ __device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restri
     double acc = 0.0;
     for (int32_t ip = b; ip < e; ++ip) {
       const ProgOp op = prog[ip];
-      const double v = prog_value(nodes, op.node, op.action, op.translate_only != 0, q);
+      const double v = prog_value<false>(nodes, op.node, op.action, op.translate_only != 0, q);
       if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
       else acc = csg(op.op, acc, v, op.k);
     }
@@ -1093,7 +1096,7 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     for (int32_t ip = 0; ip < na; ++ip) {
       const ProgOp op = pa[ip];
       const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-      const double v = prog_value(nodes, node, op.action, op.translate_only != 0, q);
+      const double v = prog_value<false>(nodes, node, op.action, op.translate_only != 0, q);
       if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
       else acc = csg(op.op, acc, v, op.k);
       if (op.top > 0) {
@@ -1136,7 +1139,7 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
         double acc = 0.0;
         for (int32_t ip = o0; ip < o1; ++ip) {
           const ProgOp op = prog[ip];
-          const double v = prog_value(nodes, op.node, op.action, op.translate_only != 0, q);
+          const double v = prog_value<false>(nodes, op.node, op.action, op.translate_only != 0, q);
           if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
           else acc = csg(op.op, acc, v, op.k);
         }
@@ -1203,7 +1206,7 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
     for (int32_t ip = 0; ip < na; ++ip) {
       const ProgOp op = pa[ip];
       const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-      const double v = prog_value(nodes, node, op.action, op.translate_only != 0, q);
+      const double v = prog_value<false>(nodes, node, op.action, op.translate_only != 0, q);
       if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
       else acc = csg(op.op, acc, v, op.k);
       if (op.top > 0) {
@@ -1240,7 +1243,7 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
           double acc = 0.0;
           for (int32_t ip = o0; ip < o1; ++ip) {
             const ProgOp op = prog[ip];
-            const double v = prog_value(nodes, op.node, op.action, op.translate_only != 0, q);
+            const double v = prog_value<false>(nodes, op.node, op.action, op.translate_only != 0, q);
             if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
             else acc = csg(op.op, acc, v, op.k);
           }

@@ -594,12 +594,12 @@ def _nested_models(lay, opt_m):
 
 @pytest.mark.parametrize("path", ["serial", "coop", "culled"])
 def test_nested_models(path):
-    """Models inside models (geometry.h PROG_NEST: one accumulator per level, a pop op folds a
-    finished child model into its parent) through each EVAL path: serial (3 tops), the
-    cooperative tail EVAL (>= 8 tops) and the culled EVAL (>= 16 boundable tops: the nested
-    models' bounds come from their children's, cull.cpp). Fresnel at every nested surface
-    (n differs). Photon records, counters and grids bit-exact against the oracle, whose
-    eval_model recursion is the reference's."""
+    """Models inside models (geometry.h PROG_SUB: a child model is one op whose value folds
+    its own children, a grandchild model first) in scenes of 3, 11 and ~55 tops that would
+    otherwise take the serial, cooperative and culled EVALs: a scene with nested models always
+    runs the general instantiation with the serial EVAL (smcrt.hip), so these check that
+    routing too. Fresnel at every nested surface (n differs). Photon records, counters and
+    grids bit-exact against the oracle, whose eval_model recursion is the reference's."""
     from rsmcrt_amd.scene import Scene, box, invert, mono, sphere, translate
     sdfs = []
     lay = lambda: len(sdfs) + 1  # noqa: E731
