@@ -76,6 +76,13 @@ namespace smcrt {
 #ifndef SMCRT_LEAN_RCP
 #define SMCRT_LEAN_RCP 0
 #endif
+// photon events run once this many lanes wait for one (or nothing else is left). The lean
+// kernel's other phases keep the waiting lanes' walkers busy, so it batches more than
+// transport_kernel's SMCRT_EVENT_LANES = 16: 20 measured +3.5 % on M1 (same box, two rounds,
+// profiles/r03_s3/lean_tune_ab.txt)
+#ifndef SMCRT_LEAN_EVENT_LANES
+#define SMCRT_LEAN_EVENT_LANES 20
+#endif
 constexpr uint32_t ST_ABSORB = 40;  // absorbed; recordWeight waits for the photon's cells
 #ifndef SMCRT_LEAN_SLOTS
 #define SMCRT_LEAN_SLOTS 3
@@ -568,7 +575,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       const uint64_t evm = __ballot(ev);
       const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
       const uint32_t nev = __popcll(evm);
-      const bool run_ev = nev && (nev >= SMCRT_EVENT_LANES || evm == busy);
+      const bool run_ev = nev && (nev >= SMCRT_LEAN_EVENT_LANES || evm == busy);
       LDIAG(LD_P7, run_ev ? 1 : 0);
       LDIAG(LD_EVWAIT, run_ev ? 0 : nev);
 #ifdef SMCRT_LEAN_ABL_NO_P7  // register-pressure analysis builds only (tools/regs.sh)
