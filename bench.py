@@ -93,12 +93,11 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
-def cpu_baseline(sc, g, src, dets, seconds, eng, threads, seed, chunk):
+def cpu_run(sc, g, src, dets, seconds, threads, seed, chunk):
     """The CPU restatement (oracle/, C, one photon stream per photon like the GPU) timed on
     `threads` host cores for about `seconds` of wall time: threads pull `chunk`-photon chunks
-    of the same workload (ctypes releases the GIL), so the sample is photons [0, n).
-    Then the GPU runs exactly those photons and its fluence is compared with the CPU's."""
-    import numpy as np
+    of the same workload (ctypes releases the GIL), so the sample is photons [0, n). Returns
+    the baseline object and the CPU tallies of photons [0, n)."""
     from oracle import pyoracle as O
     from rsmcrt_amd.tallies import Result
     nxt = [0]
@@ -128,19 +127,104 @@ def cpu_baseline(sc, g, src, dets, seconds, eng, threads, seed, chunk):
             "sample": f"photons [0,{n}) of the same workload, oracle/ C restatement (gcc -O2) on {threads} host "
                       f"thread{'s' if threads > 1 else ''} for {dt:.1f} s",
             "seconds": round(dt, 2)}
-    if eng is None:
-        return base, None
-    gpu = eng.run(src, n, seed=seed)
-    fc, fg = res.normalised_fluence(), gpu.normalised_fluence()
+    return base, res
+
+
+def compare_with_cpu(gpu, cpu):
+    """The GPU's tallies of photons [0, n) against the CPU restatement's of the same photons."""
+    import numpy as np
+    fc, fg = cpu.normalised_fluence(), gpu.normalised_fluence()
     rmse = float(np.sqrt(np.mean((fg - fc) ** 2)))
     rel = float(np.max(np.abs(fg - fc)) / max(1e-300, float(np.max(np.abs(fc)))))
     agree = {"jmean_rmse_vs_cpu_same_photons": rmse, "jmean_max_rel_diff_vs_cpu": rel,
-             "counters_bit_exact_vs_cpu": gpu.counters_dict() == res.counters_dict(),
-             "photons_compared": n}
-    if dets:
-        db = float(np.max(np.abs(gpu.det_bins - res.det_bins)) / max(1e-300, float(np.max(np.abs(res.det_bins)))))
+             "counters_bit_exact_vs_cpu": gpu.counters_dict() == cpu.counters_dict(),
+             "photons_compared": cpu.n_photons}
+    if cpu.det_bins.size > 1 or cpu.det_bins.any():
+        db = float(np.max(np.abs(gpu.det_bins - cpu.det_bins)) / max(1e-300, float(np.max(np.abs(cpu.det_bins)))))
         agree["det_bins_max_rel_diff_vs_cpu"] = db
+    return agree
+
+
+def cpu_baseline(sc, g, src, dets, seconds, eng, threads, seed, chunk):
+    """cpu_run, then (with an engine) the GPU runs exactly photons [0, n) and its fluence,
+    counters and detector bins are compared with the CPU's."""
+    base, res = cpu_run(sc, g, src, dets, seconds, threads, seed, chunk)
+    if eng is None:
+        return base, None
+    return base, compare_with_cpu(eng.run(src, res.n_photons, seed=seed), res)
+
+
+def sharded_cpu_parity(rank, world, cpu_leg, broadcast, sharded_gpu_run):
+    """The CPU leg and the GPU-vs-port parity of an N-rank bench line (after the timed region).
+    Rank 0 times the CPU restatement on photons [0, n) (cpu_leg() -> (baseline, CPU Result));
+    n reaches every rank (broadcast); every rank runs its share [r n / N, (r+1) n / N) of the
+    SAME photons and the shares are summed over the ranks by the engine's packed RCCL reduce
+    (sharded_gpu_run(first, count) -> the summed Result on rank 0, None elsewhere); rank 0
+    compares the sum with the CPU's tallies. Returns (baseline, parity) on rank 0, else
+    (None, None). The reference means to sum its ranks' tallies with mpi_reduce
+    (kernelsMod.f90:2351-2357)."""
+    base = cpu = None
+    n = 0
+    if rank == 0:
+        base, cpu = cpu_leg()
+        n = cpu.n_photons
+    n = int(broadcast(n))
+    lo, hi = rank * n // world, (rank + 1) * n // world
+    gpu = sharded_gpu_run(lo, hi - lo)
+    if rank != 0:
+        return None, None
+    gpu.n_photons = n
+    agree = compare_with_cpu(gpu, cpu)
+    agree["gpu_side"] = (f"photons [0,{n}) split over {world} ranks, each rank its share, summed with the "
+                         f"engine's one packed RCCL reduce (smcrt_reduce_device_tallies) onto rank 0")
     return base, agree
+
+
+def attach_cpu_leg(out, base, agree, rccl_ranks=None):
+    """The CPU leg's fields of the bench line: the baseline, the GPU-vs-port parity and, for
+    N > 1 ranks, the rank count of the RCCL communicator that summed the GPU side."""
+    out["cpu_baseline"] = base
+    out["parity"] = agree
+    if rccl_ranks is not None:
+        out["rccl_ranks"] = rccl_ranks
+    return out
+
+
+def sharded_device_run(eng, comm, src, g, dets, flags, seed, first, count, stream, rank):
+    """One rank's share [first, first + count) of a photon range into fresh device tallies,
+    then ONE packed RCCL reduce of every rank's tallies onto rank 0 (smcrt_reduce_device_tallies);
+    rank 0 gets the summed tallies as a host Result."""
+    import torch
+    from rsmcrt_amd import abi
+    from rsmcrt_amd.engine import Engine
+    from rsmcrt_amd.tallies import Result
+    dev = torch.device("cuda", torch.cuda.current_device())
+    res = Result(g, dets)
+    nv = g.nx * g.ny * g.nz
+    t = {k: torch.zeros(nv, dtype=torch.float64, device=dev) for k in ("jmean", "absorb", "emission")}
+    t["det_bins"] = torch.zeros(len(res.det_bins), dtype=torch.float64, device=dev)
+    t["nscatt"] = torch.zeros(1, dtype=torch.float64, device=dev)
+    t["counters"] = torch.zeros(abi.NCOUNTERS, dtype=torch.int64, device=dev)
+    dt = abi.DeviceTallies()
+    for k, v in t.items():
+        if k != "det_bins" or dets:
+            setattr(dt, k, v.data_ptr())
+    if count > 0:
+        eng.run_device(src, Engine.config(count, seed=seed, flags=flags, first_photon=first), dt, stream.cuda_stream)
+    eng.fence(stream.cuda_stream)
+    eng.reduce_device_tallies(comm, dt, root=0, stream=stream.cuda_stream)
+    torch.cuda.synchronize()
+    if rank != 0:
+        return None
+    shape = (g.nz, g.ny, g.nx)
+    res.jmean[...] = t["jmean"].cpu().numpy().reshape(shape)
+    res.absorb[...] = t["absorb"].cpu().numpy().reshape(shape)
+    res.emission[...] = t["emission"].cpu().numpy().reshape(shape)
+    if dets:
+        res.det_bins[...] = t["det_bins"].cpu().numpy()
+    res.nscatt[...] = t["nscatt"].cpu().numpy()
+    res.counters[...] = t["counters"].cpu().numpy().astype("uint64")
+    return res
 
 
 def pmc_summary(name, batch, grid):
@@ -573,19 +657,33 @@ def main():
             "valu_roofline": valu_roofline(pmc, kern_ms),
             "cpu_baseline": None,
         }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if not args.no_cpu:
         threads = args.cpu_threads or cpu_threads()
-        log(f"[bench] CPU leg: {args.cpu_seconds} s on {threads} threads + {args.cpu1_seconds} s on 1 core")
         chunk = max(50, min(2000, B // 1000))
-        base, agree = cpu_baseline(sc, g, src, dets, args.cpu_seconds, eng, threads, args.seed, chunk)
-        out["cpu_baseline"] = base
-        out["parity"] = agree
-        if args.cpu1_seconds > 0:
-            one, _ = cpu_baseline(sc, g, src, dets, args.cpu1_seconds, None, 1, args.seed, max(50, chunk // 8))
-            out["cpu_baseline_1core"] = one
-            out["gpu_over_cpu_1core"] = out["value"] / one["value"]
-        out["gpu_over_cpu"] = out["value"] / base["value"]
-    if rank == 0 and world == 1 and not args.no_ref:
+        if rank == 0:
+            log(f"[bench] CPU leg: {args.cpu_seconds} s on {threads} threads + {args.cpu1_seconds} s on 1 core")
+        if world == 1:
+            base, agree = cpu_baseline(sc, g, src, dets, args.cpu_seconds, eng, threads, args.seed, chunk)
+        else:  # the same photons on every rank's GPU, summed by the engine's RCCL reduce
+            def bcast(n):
+                box = [n]
+                dist.broadcast_object_list(box, src=0)
+                return box[0]
+
+            def sharded(first, count):
+                return sharded_device_run(eng, comm, src, g, dets, run_flags, args.seed, first, count, stream, rank)
+
+            base, agree = sharded_cpu_parity(
+                rank, world, lambda: cpu_run(sc, g, src, dets, args.cpu_seconds, threads, args.seed, chunk),
+                bcast, sharded)
+        if rank == 0:
+            attach_cpu_leg(out, base, agree, comm.n_ranks if world > 1 else None)
+            if args.cpu1_seconds > 0:
+                one, _ = cpu_baseline(sc, g, src, dets, args.cpu1_seconds, None, 1, args.seed, max(50, chunk // 8))
+                out["cpu_baseline_1core"] = one
+                out["gpu_over_cpu_1core"] = out["value"] / one["value"]
+            out["gpu_over_cpu"] = out["value"] / base["value"]
+    if rank == 0 and not args.no_ref:
         log("[bench] reference-pinned spatial checks (validation2/3 absorb depth, fibre efficiency)")
         out.setdefault("parity", {})["reference_pinned"] = reference_pinned(torch.cuda.current_device())
     if rank == 0:

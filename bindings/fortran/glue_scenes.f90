@@ -3,7 +3,7 @@
 ! as the flat tables smcrt_scene_create receives. tests/test_fortran_binding.py compares them
 ! field by field with the C++ TOML front end (smcrt_job_scene) on the same files.
 ! usage: glue_scenes OUTDIR  ->  OUTDIR/<name>.bin for scat_test, aptran, validation1, omg,
-! test_dects, validateFibreDect
+! test_dects, egg_test
 program glue_scenes
     use smcrt_mod
     use smcrt_glue
@@ -103,6 +103,24 @@ program glue_scenes
     ierr = smcrt_source_from("point", [0._c_double, 0._c_double, 0._c_double], [0._c_double, 0._c_double, 0._c_double], &
                              corner1, corner2, corner3, src)
     call emit("test_dects", a, d, src, ierr)
+    deallocate(a, d)
+
+    ! res/egg_test.toml: setup_egg (:149-248), numOptProp = 3 with the parser's defaults (mus 1,
+    ! mua 0, hgg 0, n 1); the albumen and shell are Moss eggs revolved about y
+    allocate(a(4), d(0))
+    a(1) = smcrt_sphere(1._c_double, smcrt_mono(1._c_double, 0._c_double, 0._c_double, 1._c_double), 1, &
+                        transform=smcrt_invert(smcrt_translate([0._c_double, 0._c_double, 0._c_double])))
+    a(2) = smcrt_revolution(smcrt_egg(2._c_double * (1 - 0.02_c_double), 1.5_c_double * (1 - 0.02_c_double), &
+                                      1.4_c_double * (1 - 0.02_c_double), &
+                                      smcrt_mono(1._c_double, 0._c_double, 0._c_double, 1._c_double), 3), &
+                            0._c_double, center=[0._c_double, 0._c_double, 0._c_double])
+    a(3) = smcrt_revolution(smcrt_egg(2._c_double, 1.5_c_double, 1.4_c_double, &
+                                      smcrt_mono(1._c_double, 0._c_double, 0._c_double, 1._c_double), 2), &
+                            0._c_double, center=[0._c_double, 0._c_double, 0._c_double])
+    a(4) = smcrt_box([5._c_double, 5._c_double, 5._c_double], zero, 4)
+    ierr = smcrt_source_from("point", [0._c_double, 0._c_double, 0._c_double], [0._c_double, 0._c_double, 0._c_double], &
+                             corner1, corner2, corner3, src)
+    call emit("egg_test", a, d, src, ierr)
     deallocate(a, d)
 
 contains

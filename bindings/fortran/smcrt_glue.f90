@@ -13,8 +13,8 @@
 !     ...
 !     call smcrt_flatten(g, nodes, top)
 !
-! tests/test_fortran_binding.py builds res/scat_test, aptran, validation1, omg and test_dects
-! with it
+! tests/test_fortran_binding.py builds res/scat_test, aptran, validation1, omg, test_dects and
+! egg_test (revolution modifiers) with it
 ! (bindings/fortran/glue_scenes.f90) and checks every field against the C++ TOML front end.
 module smcrt_glue
     use iso_c_binding
@@ -25,6 +25,8 @@ module smcrt_glue
     public :: smcrt_optprop, smcrt_mono, smcrt_sdf
     public :: smcrt_sphere, smcrt_box, smcrt_torus, smcrt_cylinder, smcrt_triprism, smcrt_segment, &
               smcrt_capsule, smcrt_cone, smcrt_egg, smcrt_plane, smcrt_model
+    public :: smcrt_revolution, smcrt_extrude, smcrt_onion, smcrt_twist, smcrt_bend, smcrt_elongate, &
+              smcrt_displacement_sine
     public :: smcrt_count_nodes, smcrt_flatten
     public :: smcrt_circle_dect, smcrt_annulus_dect, smcrt_camera, smcrt_fibre_dect
     public :: smcrt_source_from
@@ -263,6 +265,80 @@ contains
         allocate(s%children, source=array)
     end function smcrt_model
 
+    ! ------------------------------------------------------------ modifiers ----------------
+    ! sdfModifiers.f90's *_init: the modifier wraps `prim` (a primitive, model or modifier), takes
+    ! its layer and optics, and keeps the identity transform it never applies.
+    function modifier(kind, prim_sdf, param) result(s)
+        integer(c_int32_t), intent(in) :: kind
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: param(:)
+        type(smcrt_sdf) :: s
+        s%node%kind = kind
+        s%node%transform = reshape(smcrt_identity(), [16])
+        s%node%param(1:size(param)) = param
+        s%node%layer = prim_sdf%node%layer
+        s%node%mus = prim_sdf%node%mus; s%node%mua = prim_sdf%node%mua
+        s%node%hgg = prim_sdf%node%hgg; s%node%n = prim_sdf%node%n
+        s%node%n_children = 1
+        allocate(s%children(1))
+        s%children(1) = prim_sdf
+    end function modifier
+
+    function smcrt_revolution(prim_sdf, o, center) result(s)  ! revolution_init :232-259
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: o
+        real(c_double), optional, intent(in) :: center(3)
+        type(smcrt_sdf) :: s
+        real(c_double) :: c(3)
+        c = 0._c_double
+        if (present(center)) c = center
+        s = modifier(SMCRT_SDF_REVOLUTION, prim_sdf, [o, c])
+    end function smcrt_revolution
+
+    function smcrt_extrude(prim_sdf, h) result(s)  ! extrude_init :143-159
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: h
+        type(smcrt_sdf) :: s
+        s = modifier(SMCRT_SDF_EXTRUDE, prim_sdf, [h])
+    end function smcrt_extrude
+
+    function smcrt_onion(prim_sdf, thickness) result(s)  ! onion_init :261-277
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: thickness
+        type(smcrt_sdf) :: s
+        s = modifier(SMCRT_SDF_ONION, prim_sdf, [thickness])
+    end function smcrt_onion
+
+    function smcrt_twist(prim_sdf, k) result(s)  ! twist_init :126-141 (k is a default real there)
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real, intent(in) :: k
+        type(smcrt_sdf) :: s
+        s = modifier(SMCRT_SDF_TWIST, prim_sdf, [real(k, c_double)])
+    end function smcrt_twist
+
+    function smcrt_bend(prim_sdf, k) result(s)  ! bend_init :196-212
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: k
+        type(smcrt_sdf) :: s
+        s = modifier(SMCRT_SDF_BEND, prim_sdf, [k])
+    end function smcrt_bend
+
+    function smcrt_elongate(prim_sdf, size3) result(s)  ! elongate_init :161-176
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: size3(3)
+        type(smcrt_sdf) :: s
+        s = modifier(SMCRT_SDF_ELONGATE, prim_sdf, size3)
+    end function smcrt_elongate
+
+    !> displacement_init (:178-194) with the engine's built-in f(p) = a sin(fx x) sin(fy y) sin(fz z)
+    !> (the reference takes any procedure(primitive); device code cannot call a host pointer)
+    function smcrt_displacement_sine(prim_sdf, amplitude, freq) result(s)
+        type(smcrt_sdf), intent(in) :: prim_sdf
+        real(c_double), intent(in) :: amplitude, freq(3)
+        type(smcrt_sdf) :: s
+        s = modifier(SMCRT_SDF_DISPLACEMENT, prim_sdf, [real(SMCRT_DISP_SINE, c_double), amplitude, freq])
+    end function smcrt_displacement_sine
+
     ! ------------------------------------------------------------ flattening ---------------
     recursive integer function smcrt_count_nodes(array) result(n)
         type(smcrt_sdf), intent(in) :: array(:)
@@ -297,7 +373,7 @@ contains
                 nodes(base + j) = a(j)%node
             end do
             do j = 1, size(a)
-                if (a(j)%node%kind == SMCRT_SDF_MODEL) then
+                if (allocated(a(j)%children)) then  ! a model or a modifier
                     first = k
                     nodes(base + j)%first_child = int(first, c_int32_t)
                     nodes(base + j)%n_children = int(size(a(j)%children), c_int32_t)

@@ -13,6 +13,11 @@ module smcrt_mod
     integer(c_int32_t), parameter :: SMCRT_SDF_SPHERE = 1, SMCRT_SDF_BOX = 2, SMCRT_SDF_TORUS = 3, &
         SMCRT_SDF_CYLINDER = 4, SMCRT_SDF_TRIPRISM = 5, SMCRT_SDF_SEGMENT = 6, SMCRT_SDF_CAPSULE = 7, &
         SMCRT_SDF_CONE = 8, SMCRT_SDF_EGG = 9, SMCRT_SDF_PLANE = 10, SMCRT_SDF_MODEL = 11
+    ! the modifiers of sdfModifiers.f90 (ABI 4): each wraps one node
+    integer(c_int32_t), parameter :: SMCRT_SDF_REVOLUTION = 12, SMCRT_SDF_EXTRUDE = 13, SMCRT_SDF_ONION = 14, &
+        SMCRT_SDF_TWIST = 15, SMCRT_SDF_BEND = 16, SMCRT_SDF_ELONGATE = 17, SMCRT_SDF_DISPLACEMENT = 18
+    integer(c_int32_t), parameter :: SMCRT_DISP_SINE = 1
+    integer(c_int), parameter :: SMCRT_MOD_ABI_VERSION = 4  ! compare with smcrt_abi_version()
     ! smcrt_csg_op
     integer(c_int32_t), parameter :: SMCRT_OP_UNION = 0, SMCRT_OP_SMOOTH_UNION = 1, &
         SMCRT_OP_SUBTRACTION = 2, SMCRT_OP_INTERSECTION = 3
@@ -129,6 +134,7 @@ module smcrt_mod
         real(c_double)     :: transport_ms = 0._c_double, deposit_ms = 0._c_double
         integer(c_int64_t) :: launches = 0, lean_launches = 0, far_steps = 0
         real(c_double)     :: fold_cu_ms = 0._c_double
+        integer(c_int64_t) :: lean_hazards = 0  ! ABI 4
     end type smcrt_kernel_times
 
     interface
@@ -376,6 +382,12 @@ module smcrt_mod
             import :: c_ptr
             type(c_ptr), value :: comm
         end subroutine smcrt_comm_destroy
+
+        integer(c_int) function smcrt_comm_info(comm, n_ranks, rank, device) bind(C, name="smcrt_comm_info")
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value         :: comm
+            integer(c_int32_t), intent(out) :: n_ranks, rank, device
+        end function smcrt_comm_info
 
         integer(c_int) function smcrt_reduce_device_tallies(scene, comm, dev, root, stream) &
                 bind(C, name="smcrt_reduce_device_tallies")

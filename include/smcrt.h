@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SMCRT_ABI_VERSION 3
+#define SMCRT_ABI_VERSION 4
 
 typedef enum smcrt_status {
   SMCRT_OK = 0,
@@ -61,8 +61,31 @@ typedef enum smcrt_sdf_kind {
   SMCRT_SDF_CONE = 8,     /* param[0..2]=a param[3..5]=b param[6]=ra param[7]=rb sdfs.f90:650-686 */
   SMCRT_SDF_EGG = 9,      /* param[0]=r1 param[1]=r2 param[2]=h                sdfs.f90:688-718 */
   SMCRT_SDF_PLANE = 10,   /* param[0..2]=a (unit normal)                       sdfs.f90:720-735 */
-  SMCRT_SDF_MODEL = 11    /* CSG fold over children       sdf_base.f90:146-161, sdfModifiers.f90:428-491 */
+  SMCRT_SDF_MODEL = 11,   /* CSG fold over children       sdf_base.f90:146-161, sdfModifiers.f90:428-491 */
+  /* ---- ABI 4: the domain modifiers of sdfModifiers.f90. Each wraps ONE node
+     (first_child, n_children = 1), which may be a primitive, a model or another modifier; it
+     takes the layer and optical properties of that node (the *_init functions copy
+     prim%optProps and prim%layer) and ignores its own transform (the reference sets it to the
+     identity and never applies it). Models and modifiers nest at most three levels deep. */
+  SMCRT_SDF_REVOLUTION = 12, /* param[0]=o, param[1..3]=center: q = (|(p-c).xz| - o, (p-c).y, 0)   :286-303 */
+  SMCRT_SDF_EXTRUDE = 13,    /* param[0]=h: w = (d(p), |p.z| - h); min(max(w),0) + |max(w,0)|    :268-284 */
+  SMCRT_SDF_ONION = 14,      /* param[0]=thickness: |d(p)| - thickness                          :305-315 */
+  SMCRT_SDF_TWIST = 15,      /* param[0]=k: d of p rotated by k*p.z in the xy plane              :334-352
+                                (twist_init takes k as default real: pass real(k_sp, wp))      */
+  SMCRT_SDF_BEND = 16,       /* param[0]=k: d of p rotated by k*p.x in the xy plane              :354-372 */
+  SMCRT_SDF_ELONGATE = 17,   /* param[0..2]=size: q = |p| - size; d(max(q,0)) + min(max(q),0)     :317-332 */
+  SMCRT_SDF_DISPLACEMENT = 18 /* d(p) + f(p) with a built-in f (param[0] = smcrt_displacement_fn):  :374-388
+                                the reference takes any pure function of pos and ships none    */
 } smcrt_sdf_kind;
+
+/* Built-in displacement functions f(p) of SMCRT_SDF_DISPLACEMENT (param[0]); the reference's
+ * displacement_init takes an arbitrary procedure(primitive) pointer, which cannot cross to
+ * device code. The `repeat` modifier is not provided: its evaluate is an `error stop "Not
+ * implmented"` in the reference (sdfModifiers.f90:390-408). */
+typedef enum smcrt_displacement_fn {
+  SMCRT_DISP_SINE = 1 /* param[1]=amplitude a, param[2..4]=frequencies (fx, fy, fz):
+                         f(p) = ((a * sin(fx*p.x)) * sin(fy*p.y)) * sin(fz*p.z) */
+} smcrt_displacement_fn;
 
 /* CSG operators of a MODEL node (sdfModifiers.f90:428-491). */
 typedef enum smcrt_csg_op {
@@ -364,6 +387,12 @@ typedef struct smcrt_kernel_times {
                             workgroups' run times divided by the CU count (one workgroup fills a CU),
                             i.e. the whole-chip time it took, without the time it queued behind
                             transport launches (which deposit_ms includes) */
+  /* ---- ABI 4 (the struct grew from 48 to 56 bytes) ---- */
+  int64_t lean_hazards;  /* deferred lean-kernel voxel walks that ended in tflag or an
+                            error stop since the last query. Each is also counted in SMCRT_CTR_FAULTS: the
+                            photon went on as if the walk had stayed inside the grid, so it no longer
+                            follows the reference. Expected 0; only the debug knob
+                            SMCRT_DEBUG_LEAN_MARGIN=0|all (tests) provokes them. */
 } smcrt_kernel_times;
 
 int smcrt_scene_set_timing(smcrt_scene* scene, int32_t enable);
@@ -506,6 +535,9 @@ typedef struct smcrt_comm smcrt_comm;
 int smcrt_comm_unique_id(uint8_t* id /* SMCRT_UNIQUE_ID_BYTES */);
 int smcrt_comm_init_rank(const uint8_t* id, int32_t n_ranks, int32_t rank, int32_t device, smcrt_comm** out);
 void smcrt_comm_destroy(smcrt_comm* comm);
+/* ABI 4: the communicator's rank count and this rank as RCCL reports them (ncclCommCount,
+ * ncclCommUserRank), and its device (any output may be NULL). */
+int smcrt_comm_info(const smcrt_comm* comm, int32_t* n_ranks, int32_t* rank, int32_t* device);
 /* Sum every rank's device tallies (smcrt_run_device's buffers) over `comm` with ONE packed
  * collective on `stream`: an all-reduce when root < 0 (every rank gets the sums), else a
  * reduce onto rank `root` (the mpi_reduce of kernelsMod.f90:2353-2357; the other ranks'

@@ -303,6 +303,13 @@ static double csg(int32_t op, double d1, double d2, double k) {
   }
 }
 
+/* sin and cos of a twist/bend/displacement angle of any sign: sin(-x) = -sin(x), cos(-x) =
+ * cos(x), then oracle_sincos's reduction (the device's det_sincos_any, detmath.h) */
+static void oracle_sincos_any(double x, double* s, double* c) {
+  oracle_sincos(fabs(x), s, c);
+  if (x < 0.0) *s = -*s;
+}
+
 static double sdf_eval_node(const scene_t* S, int32_t idx, vec3 pos, int depth) {
   const smcrt_sdf_node* nd = &S->nodes[idx];
   const double* P = nd->param;
@@ -312,6 +319,47 @@ static double sdf_eval_node(const scene_t* S, int32_t idx, vec3 pos, int depth) 
     for (int32_t i = 1; i < nd->n_children; ++i)
       res = csg(nd->op, res, sdf_eval_node(S, nd->first_child + i, pos, depth + 1), nd->k);
     return res;
+  }
+  if (nd->kind > SMCRT_SDF_MODEL) {  /* the modifiers of sdfModifiers.f90: one wrapped node, own transform unused */
+    if (depth > 8 || nd->n_children != 1) return NAN;
+    const int32_t ch = nd->first_child;
+    switch (nd->kind) {
+      case SMCRT_SDF_REVOLUTION: {                                       /* eval_revolution :286-303 */
+        vec3 pin = vsub(pos, v3(P[1], P[2], P[3]));
+        vec3 pxz = v3(pin.x, 0.0, pin.z);
+        return sdf_eval_node(S, ch, v3(vlen(pxz) - P[0], pin.y, 0.0), depth + 1);
+      }
+      case SMCRT_SDF_EXTRUDE: {                                          /* eval_extrude :268-284 */
+        double d = sdf_eval_node(S, ch, pos, depth + 1);
+        vec3 w = v3(d, fabs(pos.z) - P[0], 0.0);
+        return fmind(fmaxd(w.x, w.y), 0.0) + vlen(vmaxs(w, 0.0));
+      }
+      case SMCRT_SDF_ONION:                                              /* eval_onion :305-315 */
+        return fabs(sdf_eval_node(S, ch, pos, depth + 1)) - P[0];
+      case SMCRT_SDF_ELONGATE: {                                         /* eval_elongate :317-332 */
+        vec3 q = vsub(vabs(pos), v3(P[0], P[1], P[2]));
+        double w = fmind(fmaxd(q.x, fmaxd(q.y, q.z)), 0.0);
+        return sdf_eval_node(S, ch, vmaxs(q, 0.0), depth + 1) + w;
+      }
+      case SMCRT_SDF_TWIST:                                              /* eval_twist :334-352 */
+      case SMCRT_SDF_BEND: {                                             /* eval_bend :354-372 */
+        double s, c;
+        oracle_sincos_any(P[0] * (nd->kind == SMCRT_SDF_TWIST ? pos.z : pos.x), &s, &c);
+        double x2 = c * pos.x - s * pos.y;
+        double y2 = s * pos.x + c * pos.y;
+        return sdf_eval_node(S, ch, v3(x2, y2, pos.z), depth + 1);
+      }
+      case SMCRT_SDF_DISPLACEMENT: {                                     /* eval_disp :374-388, built-in f */
+        double d1 = sdf_eval_node(S, ch, pos, depth + 1);
+        double sx, sy, sz, c;
+        oracle_sincos_any(P[2] * pos.x, &sx, &c);
+        oracle_sincos_any(P[3] * pos.y, &sy, &c);
+        oracle_sincos_any(P[4] * pos.z, &sz, &c);
+        return d1 + ((P[1] * sx) * sy) * sz;
+      }
+      default:
+        return NAN;
+    }
   }
   vec3 p = vdotmat(pos, nd->transform);
   switch (nd->kind) {

@@ -5,7 +5,7 @@ against the library's own view of them.
 """
 import ctypes as C
 
-SMCRT_ABI_VERSION = 3
+SMCRT_ABI_VERSION = 4
 
 # smcrt_status
 OK = 0
@@ -26,6 +26,9 @@ STATUS_NAMES = {
 # smcrt_sdf_kind (reference src/sdfs/sdfs.f90)
 SDF_SPHERE, SDF_BOX, SDF_TORUS, SDF_CYLINDER, SDF_TRIPRISM = 1, 2, 3, 4, 5
 SDF_SEGMENT, SDF_CAPSULE, SDF_CONE, SDF_EGG, SDF_PLANE, SDF_MODEL = 6, 7, 8, 9, 10, 11
+# the modifiers of src/sdfs/sdfModifiers.f90 (ABI 4): each wraps one node
+SDF_REVOLUTION, SDF_EXTRUDE, SDF_ONION, SDF_TWIST, SDF_BEND, SDF_ELONGATE, SDF_DISPLACEMENT = 12, 13, 14, 15, 16, 17, 18
+DISP_SINE = 1  # smcrt_displacement_fn
 
 # smcrt_csg_op (src/sdfs/sdfModifiers.f90:428-491)
 OP_UNION, OP_SMOOTH_UNION, OP_SUBTRACTION, OP_INTERSECTION = 0, 1, 2, 3
@@ -193,7 +196,8 @@ class PackLayout(C.Structure):
 
 class KernelTimes(C.Structure):
     _fields_ = [("transport_ms", C.c_double), ("deposit_ms", C.c_double), ("launches", C.c_int64),
-                ("lean_launches", C.c_int64), ("far_steps", C.c_int64), ("fold_cu_ms", C.c_double)]
+                ("lean_launches", C.c_int64), ("far_steps", C.c_int64), ("fold_cu_ms", C.c_double),
+                ("lean_hazards", C.c_int64)]
 
 
 EXPORTED_SYMBOLS = [
@@ -207,7 +211,7 @@ EXPORTED_SYMBOLS = [
     "smcrt_job_escape_config", "smcrt_job_inverse_config", "smcrt_job_targets", "smcrt_job_run_escape",
     "smcrt_job_run_inverse", "smcrt_scene_fence",
     "smcrt_pack_size", "smcrt_pack_host", "smcrt_unpack_host", "smcrt_comm_unique_id", "smcrt_comm_init_rank",
-    "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_multi_create", "smcrt_multi_info",
+    "smcrt_comm_info", "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_multi_create", "smcrt_multi_info",
     "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_accumulate", "smcrt_multi_collect",
     "smcrt_multi_device_photons", "smcrt_multi_destroy", "smcrt_job_run_devices",
 ]

@@ -10,7 +10,7 @@ from typing import Sequence, Tuple
 
 from . import abi
 from .scene import (Scene, box, capsule, cylinder, invert, model, mono, rotate_y, sphere, torus,
-                    translate)
+                    translate, egg, revolution)
 
 
 def setup_scat_test(tau: float) -> Scene:
@@ -66,6 +66,19 @@ def setup_sphere_scene(spheres: Sequence[Tuple[float, float, float, float]]) -> 
         sdfs.append(sphere(r, opt_sph, i + 1, transform=invert(translate((x, y, z)))))
     sdfs.append(box((2.0, 2.0, 2.0), opt_box, len(spheres) + 1))
     return Scene(sdfs)
+
+
+def setup_egg(mus, mua, hgg, n, position=(0.0, 0.0, 0.0), bounding=(2.0, 2.0, 2.0), bottom_r=2.0, top_r=1.5,
+              sep=1.4, shell=0.02, yolk_r=1.0) -> Scene:
+    """setupGeometry.f90:149-248 (geom_name='egg'): yolk sphere (layer 1), albumen and shell as
+    revolved Moss eggs (layers 3 and 2, revolution(egg, 0, center=position)), bounding box
+    (layer 4). mus/mua/hgg/n are the three-entry optical property lists (numOptProp = 3)."""
+    o = [mono(mus[i], mua[i], hgg[i], n[i]) for i in range(3)]
+    f = 1.0 - shell
+    shell_sdf = revolution(egg(bottom_r, top_r, sep, o[0], 2), 0.0, center=position)
+    albumen = revolution(egg(bottom_r * f, top_r * f, sep * f, o[1], 3), 0.0, center=position)
+    yolk = sphere(yolk_r, o[2], 1, transform=invert(translate(position)))
+    return Scene([yolk, albumen, shell_sdf, box(bounding, mono(0.0, 0.0, 0.0, 1.0), 4)])
 
 
 def random_sphere_list(num: int, seed: int = 123456789):

@@ -58,7 +58,7 @@ Bound prim_bound(const smcrt_sdf_node& nd) {
     case SMCRT_SDF_CYLINDER: seg(std::fabs(P[6])); break;
     case SMCRT_SDF_CAPSULE: seg(std::fabs(P[6])); break;
     case SMCRT_SDF_SEGMENT: seg(0.1); break;  // sdfs.f90:599-626 subtracts a fixed 0.1
-    default: return b;  // cone, egg, prism, plane: never culled
+    default: return b;  // cone, egg, prism, plane, modifiers: never culled
   }
   for (int a = 0; a < 3; ++a)
     if (!std::isfinite(lo[a]) || !std::isfinite(hi[a]) || !(lo[a] <= hi[a])) return b;
@@ -126,14 +126,7 @@ Bound top_bound(const smcrt_sdf_node* nodes, int32_t n_nodes, int32_t idx) {
 // ds of a top-level SDF at q (host; the fold of sdf_base.f90:146-161). Only used to choose
 // list lengths, never for a result.
 double top_value(const smcrt_sdf_node* nodes, int32_t idx, V3 q) {
-  const smcrt_sdf_node& nd = nodes[idx];
-  if (nd.kind != SMCRT_SDF_MODEL) return sdf_prim(&nd, q, false);
-  double acc = 0.0;
-  for (int32_t c = 0; c < nd.n_children; ++c) {
-    const double v = top_value(nodes, nd.first_child + c, q);
-    acc = c == 0 ? v : csg(nd.op, acc, v, nd.k);
-  }
-  return acc;
+  return node_value<PROG_MAX_DEPTH>(nodes, idx, q);  // (models and modifiers, geometry.h)
 }
 
 double box_dist(const double* clo, const double* chi, const Bound& b) {

@@ -69,8 +69,8 @@ struct Rng {
 };
 
 // --------------------------------------------------------------- elementary math --
-__device__ __forceinline__ uint64_t d2u(double x) { return (uint64_t)__double_as_longlong(x); }
-__device__ __forceinline__ double u2d(uint64_t u) { return __longlong_as_double((long long)u); }
+__host__ __device__ __forceinline__ uint64_t d2u(double x) { return __builtin_bit_cast(uint64_t, x); }
+__host__ __device__ __forceinline__ double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
 
 // IEEE fp64 division split in two. For `n / d` the compiler emits (gfx950):
 //   D = v_div_scale(d); r = v_rcp(D); twice { e = fma(-D, r, 1); r = fma(r, e, r) };
@@ -100,6 +100,7 @@ __device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
   __sincosf((float)x, &fs, &fc);
   *s = fs; *c = fc;
 }
+__device__ __forceinline__ void det_sincos_any(double x, double* s, double* c) { det_sincos(x, s, c); }
 #define SMCRT_HAVE_FAST_MATH 1
 #endif
 
@@ -161,7 +162,7 @@ __device__ inline double det_log(double x) {
   return dk * ln2_hi - ((s * (f - R) - dk * ln2_lo) - f);
 }
 
-__device__ __forceinline__ double ksin(double x) {
+__host__ __device__ __forceinline__ double ksin(double x) {
   const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
                S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
                S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
@@ -171,7 +172,7 @@ __device__ __forceinline__ double ksin(double x) {
   return x + v * (S1 + z * r);
 }
 
-__device__ __forceinline__ double kcos(double x) {
+__host__ __device__ __forceinline__ double kcos(double x) {
   const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
                C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
@@ -187,7 +188,7 @@ __device__ __forceinline__ double kcos(double x) {
 }
 
 // sin and cos of x in [0, 4pi] (fdlibm medium Cody-Waite reduction)
-__device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
+__host__ __device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
   const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
                pio2_1t = 6.07710050650619224932e-11;
   const int32_t n = (int32_t)(x * invpio2 + 0.5);
@@ -204,9 +205,17 @@ __device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
   }
 }
 
+// sin and cos of any angle of the twist and bend modifiers (k * p, sdfModifiers.f90:341-342,
+// :361-362): sin(-x) = -sin(x), cos(-x) = cos(x), then det_sincos's reduction, whose
+// fn * pio2_1 stays exact while |x| < 2^19 pi/2 (larger angles stay deterministic, with less
+// accuracy). The oracle restates it (oracle_sincos_any).
+__host__ __device__ __forceinline__ void det_sincos_any(double x, double* s, double* c) {
+  det_sincos(fabs(x), s, c);
+  if (x < 0.0) *s = -*s;
+}
+#endif  // SMCRT_HAVE_FAST_MATH
 
 // atan (fdlibm s_atan.c), for the fibre detector's acceptance angle (detectors.f90:386).
-#endif  // SMCRT_HAVE_FAST_MATH
 
 __device__ inline double det_atan(double x) {
   const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,

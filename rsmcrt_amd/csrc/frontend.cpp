@@ -97,9 +97,9 @@ void flatten(const std::vector<Prim>& sdfs, std::vector<smcrt_sdf_node>& nodes, 
   for (size_t q = 0; q < pending.size(); ++q) {
     const int32_t idx = pending[q].first;
     const Prim& s = *pending[q].second;
-    if (s.kind == SMCRT_SDF_MODEL) {
+    if (s.kind >= SMCRT_SDF_MODEL) {  // a model or a modifier (one child)
       smcrt_sdf_node nd = to_node(s);
-      nd.layer = s.children.front().layer;  // a model takes layer and optics of array(1)
+      nd.layer = s.children.front().layer;  // layer and optics of array(1) / of the wrapped SDF
       nd.mus = s.children.front().opt.mus; nd.mua = s.children.front().opt.mua;
       nd.hgg = s.children.front().opt.hgg; nd.n = s.children.front().opt.n;
       nd.first_child = (int32_t)nodes.size();
@@ -473,6 +473,15 @@ std::vector<Prim> setup_geometry(smcrt_job& J, const Table* root) {  // parse_ge
     J.set("sphereRadius", fmt_real(sphere_r));
   }
   if (e == "box") dict_vec3(J, g, "BoxDimensions", "BoxDimensions", 1.0, bdim);
+  double egg_p[5] = {0, 0, 0, 0, 0};  // parse_geometry.f90:271-282, the egg's keys and defaults
+  if (e == "egg") {
+    const char* en[5] = {"BottomSphereRadius", "TopSphereRadius", "SphereSep", "ShellThickness", "YolkRadius"};
+    const double ed[5] = {3.0, 3.0 * std::sqrt(2.0 - std::sqrt(2.0)), 3.0 * std::sqrt(2.0 - std::sqrt(2.0)), 0.05, 1.5};
+    for (int i = 0; i < 5; ++i) {
+      egg_p[i] = T::get_real(g, en[i], ed[i]);
+      J.set(en[i], fmt_real(egg_p[i]));
+    }
+  }
 
   const Mono zero{0.0, 0.0, 0.0, 1.0};
   std::vector<Prim> a;
@@ -527,8 +536,25 @@ std::vector<Prim> setup_geometry(smcrt_job& J, const Table* root) {  // parse_ge
     a.push_back(box(2.0, 2.0, 2.0, zero, 2));
   } else if (e == "vessels") {  // :552-652 reads res/{edges,nodes,radii}.dat, absent from the reference
     throw Fail(SMCRT_ERR_UNSUPPORTED, "vessels needs res/edges.dat, nodes.dat and radii.dat, which the reference does not ship");
-  } else if (e == "egg" || e == "logo") {
-    throw Fail(SMCRT_ERR_UNSUPPORTED, "geometry '" + e + "' needs SDF types the engine does not have (revolution / svg segments)");
+  } else if (e == "egg") {  // setup_egg, setupGeometry.f90:149-248: yolk, albumen, shell, bounding box
+    const double bot = egg_p[0], topr = egg_p[1], sep = egg_p[2], shell_t = egg_p[3], yolk_r = egg_p[4];
+    auto revolve = [&](Prim inner) {  // revolution(egg, 0, center = pos), sdfModifiers.f90:232-259
+      Prim m;
+      m.kind = SMCRT_SDF_REVOLUTION;
+      m.param = {0.0, pos[0], pos[1], pos[2]};
+      m.children.push_back(std::move(inner));
+      return m;
+    };
+    const Prim shell = revolve(prim(SMCRT_SDF_EGG, {bot, topr, sep}, Mono{op[1][0], op[0][0], op[3][0], op[4][0]}, 2));
+    const double f = 1.0 - shell_t;  // (1-ShellThickness), :228-229
+    const Prim albumen =
+        revolve(prim(SMCRT_SDF_EGG, {bot * f, topr * f, sep * f}, Mono{op[1][1], op[0][1], op[3][1], op[4][1]}, 3));
+    a.push_back(sphere(yolk_r, Mono{op[1][2], op[0][2], op[3][2], op[4][2]}, 1, invert(translate(pos[0], pos[1], pos[2]))));
+    a.push_back(albumen);
+    a.push_back(shell);
+    a.push_back(box(bound[0], bound[1], bound[2], zero, 4));
+  } else if (e == "logo") {  // setupGeometry.f90:326-328 stops itself ("not supported")
+    throw Fail(SMCRT_ERR_UNSUPPORTED, "geometry 'logo' needs the svg segment reader the reference disables");
   } else {
     throw Fail(SMCRT_ERR_INVALID_ARG, "no such routine");  // setup.f90:58-59
   }

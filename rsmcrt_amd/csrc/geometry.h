@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "../../include/smcrt.h"
+#include "detmath.h"
 
 namespace smcrt {
 
@@ -165,11 +166,12 @@ enum : int32_t {
   PROG_CHILD_FIRST = 1, // first child of a model: acc = d
   PROG_CHILD = 2,       // later child: acc = op(acc, d)
 };
-// Nested models (a model among a model's children: eval_model recurses through
-// array(i)%value%evaluate, sdf_base.f90:146-161). A top-level model's children are ops of the
-// program; a child that is itself a model is one op with PROG_SUB, whose value sdf_submodel
-// folds from the child's own children (which may be models of primitives in turn). Three
-// levels of models are supported; deeper nesting is rejected at scene creation.
+// Nested composites (a model among a model's children: eval_model recurses through
+// array(i)%value%evaluate, sdf_base.f90:146-161; or a modifier of sdfModifiers.f90, which
+// wraps one node). A top-level model's children are ops of the program; a child that is
+// itself a composite, or a top-level modifier, is one op with PROG_SUB whose value node_value
+// computes. Three levels of composites are supported; deeper trees are rejected at scene
+// creation.
 enum : int32_t { PROG_SUB = 8 };
 constexpr int PROG_MAX_DEPTH = 3;
 
@@ -183,40 +185,96 @@ struct ProgOp {
   int32_t pad;
 };
 
-// The value an op contributes: its primitive, or (PROG_SUB) its child model's value, i.e.
-// eval_model's left fold over the child's children, a grandchild model folded from its
-// primitives first. One loop with one sdf_prim site for both (a primitive op is one trip), so
-// the nesting costs the kernels no second inlined copy of the primitives. Nested children are
-// evaluated with their transforms in full (dotmat), which equals sdf_prim's translate-only
-// shortcut bit for bit (see sdf_prim_s).
-// NEST = false (every kernel but the general instantiation, which scenes with nested models
-// always use, smcrt.hip) compiles only the primitive.
+// Models and modifiers ("composite" nodes, every kind from SMCRT_SDF_MODEL on).
+__host__ __device__ __forceinline__ bool composite_kind(int32_t kind) { return kind >= SMCRT_SDF_MODEL; }
+
+// A modifier's query point for its wrapped node (sdfModifiers.f90). Revolution :286-303,
+// elongate :317-332 (max(q, 0)), twist :334-352, bend :354-372; the others pass pos through.
+__host__ __device__ __forceinline__ V3 modifier_point(const smcrt_sdf_node* __restrict__ M, V3 pos) {
+  const double* P = M->param;
+  switch (M->kind) {
+    case SMCRT_SDF_REVOLUTION: {  // p_in = pos - center; q = (length(p_in.xz) - o, p_in.y, 0)
+      const V3 pin = pos - v3(P[1], P[2], P[3]);
+      return v3(len(v3(pin.x, 0.0, pin.z)) - P[0], pin.y, 0.0);
+    }
+    case SMCRT_SDF_ELONGATE: {  // q = abs(pos) - size; the wrapped node sees max(q, 0)
+      const V3 q = vabs(pos) - v3(P[0], P[1], P[2]);
+      return v3(dmax(q.x, 0.0), dmax(q.y, 0.0), dmax(q.z, 0.0));
+    }
+    case SMCRT_SDF_TWIST:
+    case SMCRT_SDF_BEND: {  // c = cos(k*a), s = sin(k*a), a = pos%z (twist) or pos%x (bend)
+      double sn, cs;
+      det_sincos_any(P[0] * (M->kind == SMCRT_SDF_TWIST ? pos.z : pos.x), &sn, &cs);
+      return v3(cs * pos.x - sn * pos.y, sn * pos.x + cs * pos.y, pos.z);
+    }
+    default:
+      return pos;
+  }
+}
+
+// A modifier's value from its wrapped node's value d at its own query point pos.
+// Extrude :268-284, onion :305-315, elongate :317-332 (+ w), displacement :374-388.
+__host__ __device__ __forceinline__ double modifier_value(const smcrt_sdf_node* __restrict__ M, double d, V3 pos) {
+  const double* P = M->param;
+  switch (M->kind) {
+    case SMCRT_SDF_EXTRUDE: {  // w = (d, abs(pos%z) - h, 0); min(max(w%x, w%y), 0) + length(max(w, 0))
+      const double wy = fabs(pos.z) - P[0];
+      return dmin(dmax(d, wy), 0.0) + len(v3(dmax(d, 0.0), dmax(wy, 0.0), dmax(0.0, 0.0)));
+    }
+    case SMCRT_SDF_ONION:  // abs(d) - thickness
+      return fabs(d) - P[0];
+    case SMCRT_SDF_ELONGATE: {  // + min(max(q%x, max(q%y, q%z)), 0)
+      const V3 q = vabs(pos) - v3(P[0], P[1], P[2]);
+      return d + dmin(dmax(q.x, dmax(q.y, q.z)), 0.0);
+    }
+    case SMCRT_SDF_DISPLACEMENT: {  // d1 + d2, d2 = the built-in f(pos) (smcrt.h smcrt_displacement_fn)
+      double sx, sy, sz, c;
+      det_sincos_any(P[2] * pos.x, &sx, &c);
+      det_sincos_any(P[3] * pos.y, &sy, &c);
+      det_sincos_any(P[4] * pos.z, &sz, &c);
+      return d + ((P[1] * sx) * sy) * sz;
+    }
+    default:  // revolution, twist, bend: the wrapped node's value
+      return d;
+  }
+}
+
+// The value of node `idx` at pos: a primitive (its own transform), a model (eval_model's left
+// fold over its children, sdf_base.f90:146-161; the model's transform is not applied) or a
+// modifier (its wrapped node at modifier_point, then modifier_value). D is how many composite
+// levels remain (scene creation rejects deeper trees; a composite at D = 0 is NaN). One loop
+// with one recursive site serves models and modifiers alike, so each level inlines one
+// primitive. Children are evaluated with their transforms in full (dotmat), which equals
+// sdf_prim's translate-only shortcut bit for bit (see sdf_prim_s).
+template <int D>
+__host__ __device__ __forceinline__ double node_value(const smcrt_sdf_node* __restrict__ nodes, int32_t idx, V3 pos) {
+  const smcrt_sdf_node* __restrict__ nd = nodes + idx;
+  if (!composite_kind(nd->kind)) return sdf_prim(nd, pos, false);
+  if constexpr (D == 0) {
+    return __builtin_nan("");
+  } else {
+    const bool model = nd->kind == SMCRT_SDF_MODEL;
+    const int32_t n = model ? nd->n_children : 1;
+    const V3 q = model ? pos : modifier_point(nd, pos);
+    double acc = 0.0;
+    for (int32_t c = 0; c < n; ++c) {
+      const double v = node_value<D - 1>(nodes, nd->first_child + c, q);
+      acc = (c == 0 || !model) ? v : csg(nd->op, acc, v, nd->k);
+    }
+    return model ? acc : modifier_value(nd, acc, pos);
+  }
+}
+
+// The value an op contributes: its primitive, or (PROG_SUB) its composite node's value: a
+// model among a top model's children, or a top-level modifier (node_value).
+// NEST = false (every kernel but the general instantiation, which scenes with composites below
+// the top level always use, smcrt.hip) compiles only the primitive.
 template <bool NEST>
 __host__ __device__ __forceinline__ double prog_value(const smcrt_sdf_node* __restrict__ nodes, int32_t node,
                                                       int32_t action, bool translate_only, V3 q) {
   if constexpr (!NEST) return sdf_prim(nodes + node, q, translate_only);
   if (!(action & PROG_SUB)) return sdf_prim(nodes + node, q, translate_only);
-  const smcrt_sdf_node* M = nodes + node;
-  double acc = 0.0, sub = 0.0;
-  int32_t c = 0, g = 0;
-  while (c < M->n_children) {
-    const smcrt_sdf_node* C = nodes + M->first_child + c;
-    const bool cm = C->kind == SMCRT_SDF_MODEL;
-    const double w = sdf_prim(cm ? nodes + C->first_child + g : C, q, false);
-    double v = w;
-    bool child_done = true;
-    if (cm) {
-      sub = g == 0 ? w : csg(C->op, sub, w, C->k);
-      v = sub;
-      child_done = ++g >= C->n_children;
-    }
-    if (child_done) {
-      acc = c == 0 ? v : csg(M->op, acc, v, M->k);
-      ++c;
-      g = 0;
-    }
-  }
-  return acc;
+  return node_value<PROG_MAX_DEPTH>(nodes, node, q);
 }
 
 }  // namespace smcrt

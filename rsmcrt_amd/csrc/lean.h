@@ -36,8 +36,10 @@
 // the segment's ends stays inside the box shrunk by lean_margin (convexity), so with
 // lean_margin_a = 2 * delta * (n_a + 2) no snap can reach a boundary face. The remaining
 // error stops need NaNs or an overshoot of one ulp at an exact tie of two wall distances
-// (probability ~1e-16 per crossing); a deferred segment that nevertheless ends in one is
-// counted in dep_ctl[5] ("lean hazards", logged by the host) instead of going unnoticed.
+// (probability ~1e-16 per crossing); a deferred segment that nevertheless ends in one (a
+// "hazard": its photon has gone on as if the walk had stayed inside) is counted in
+// SMCRT_CTR_FAULTS and in smcrt_kernel_times.lean_hazards, never silently dropped. The debug
+// knob SMCRT_DEBUG_LEAN_MARGIN=0/all provokes hazards to test that accounting.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -187,8 +189,14 @@ enum : int { LD_TRIPS = 0, LD_WSTEPS, LD_WLANES, LD_PUSH, LD_SYNC, LD_BLOCKED, L
 #define LDIAG_T(i) do {} while (0)
 #endif
 
+// analysis builds: a hard VGPR budget (the waves-per-EU hint alone is not enforced)
+#ifdef SMCRT_LEAN_NUM_VGPR
+#define SMCRT_LEAN_VGPR_ATTR __attribute__((amdgpu_num_vgpr(SMCRT_LEAN_NUM_VGPR)))
+#else
+#define SMCRT_LEAN_VGPR_ATTR
+#endif
 template <bool LDS_FACES, int GM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES_PER_EU_LEAN))) void lean_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES_PER_EU_LEAN))) SMCRT_LEAN_VGPR_ATTR void lean_kernel(
     KParams K, const smcrt_sdf_node* __restrict__ nodes, const ProgOp* __restrict__ prog,
     const KCold* __restrict__ C) {
   __shared__ LeanShared shm;
@@ -225,10 +233,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   sh->busy[threadIdx.x] = 0;
   __syncthreads();
 
-  // lean_margin (see the header comment), per axis, corner coordinates
-  const double mx = 2.0 * eps * (double)(K.nx + 2), my = 2.0 * eps * (double)(K.ny + 2),
-               mz = 2.0 * eps * (double)(K.nz + 2);
+  // lean_margin (see the header comment), per axis, corner coordinates. The debug knob
+  // SMCRT_DEBUG_LEAN_MARGIN (K.lean_debug, tests only) drops the margin (1) or defers every
+  // segment that starts in the grid (2): the hazards that then occur must be counted.
+  const double mf = K.lean_debug ? 0.0 : 2.0 * eps;
+  const double mx = mf * (double)(K.nx + 2), my = mf * (double)(K.ny + 2), mz = mf * (double)(K.nz + 2);
   const double ex = 2.0 * K.xmax - mx, ey = 2.0 * K.ymax - my, ez = 2.0 * K.zmax - mz;
+  const bool defer_all = K.lean_debug == 2u;
 
   LeanPhoton P;
   P.st = ST_FETCH; P.f = LF_CELLS;
@@ -421,7 +432,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
                               old.z <= ez && e.x >= mx && e.x <= ex && e.y >= my && e.y <= ey && e.z >= mz &&
                               e.z <= ez;
           push = true;
-          sync = !inside;
+          sync = !inside && !defer_all;
           cw = lean_pack(ci, cj, ck);
         }
       }
@@ -505,7 +516,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if ((am >> lane_id & 1ull) && !W.seg) {
         const uint32_t owner = (uint32_t)(wv * 64) + (wmeta & 63u), slot = (wmeta >> 6) & 3u;
         const bool sync = (wmeta & 256u) != 0;
-        if (!sync && (W.tflag || W.fault)) ++hazards;  // cannot happen (header comment)
+        if (!sync && (W.tflag || W.fault)) ++hazards;  // cannot happen (header comment); counted as a fault
         sh->pcell[owner][slot] = lean_pack(W.xcell, W.ycell, W.zcell) | (W.tflag ? LEAN_TFLAG : 0ull) |
                                  (W.fault ? LEAN_FAULT : 0ull);
         atomicAnd(&sh->busy[owner], ~(1u << slot));
@@ -711,13 +722,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   unsigned long long* const counters = C->counters;
   const uint32_t hz = wave_sum_u32(hazards);
   if (lane_id == 0) {
-    if (hz) atomicAdd(C->dep_ctl + 5, hz);
+    if (hz) {  // reported: smcrt_kernel_times.lean_hazards, and SMCRT_CTR_FAULTS below
+      atomicAdd(C->dep_ctl + 5, hz);
+      atomicAdd(C->lean_hazards, (unsigned long long)hz);
+    }
     if (C->dep_ctl && sh->wctr[wv][LC_UPD]) atomicAdd(C->dep_ctl + 6, sh->wctr[wv][LC_UPD]);  // segments
     if (counters) {
       const uint32_t* c = sh->wctr[wv];
       const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
                                            w_dep,         c[LC_UPD],     c[LC_TAU],      0u,             0u,
-                                           0u,            c[LC_FAULTS],  c[LC_DRAWS],    0u,             c[LC_ESCAPED],
+                                           0u,            c[LC_FAULTS] + hz, c[LC_DRAWS], 0u,             c[LC_ESCAPED],
                                            w_iters};
       for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
         if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);

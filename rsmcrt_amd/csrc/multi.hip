@@ -48,6 +48,8 @@ struct Rccl {
   ncclResult_t (*group_start)() = nullptr;
   ncclResult_t (*group_end)() = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
+  ncclResult_t (*comm_count)(const ncclComm_t, int*) = nullptr;      // (optional: smcrt_comm_info)
+  ncclResult_t (*comm_user_rank)(const ncclComm_t, int*) = nullptr;  // (optional)
 };
 
 const Rccl& rccl() {
@@ -75,6 +77,8 @@ const Rccl& rccl() {
     r.group_start = (decltype(r.group_start))sym("ncclGroupStart");
     r.group_end = (decltype(r.group_end))sym("ncclGroupEnd");
     r.error_string = (decltype(r.error_string))sym("ncclGetErrorString");
+    r.comm_count = (decltype(r.comm_count))dlsym(h, "ncclCommCount");
+    r.comm_user_rank = (decltype(r.comm_user_rank))dlsym(h, "ncclCommUserRank");
     r.ok = r.err.empty();
   });
   return r;
@@ -246,6 +250,19 @@ int smcrt_comm_init_rank(const uint8_t* id, int32_t n_ranks, int32_t rank, int32
   cm->rank = rank;
   cm->device = device;
   *out = cm;
+  return SMCRT_OK;
+}
+
+int smcrt_comm_info(const smcrt_comm* cm, int32_t* n_ranks, int32_t* rank, int32_t* device) {
+  g_last_error.clear();
+  if (!cm) return fail(SMCRT_ERR_INVALID_ARG, "comm is NULL");
+  int n = cm->n_ranks, r = cm->rank;
+  const Rccl& R = rccl();
+  if (R.ok && R.comm_count) NCCLCHK(R.comm_count(cm->comm, &n));  // what the communicator itself reports
+  if (R.ok && R.comm_user_rank) NCCLCHK(R.comm_user_rank(cm->comm, &r));
+  if (n_ranks) *n_ranks = n;
+  if (rank) *rank = r;
+  if (device) *device = cm->device;
   return SMCRT_OK;
 }
 

@@ -895,9 +895,9 @@ struct smcrt_scene {
   // the running total of its steps is d_queue[MAX_SLOTS + 1]
   double fm_err = 0.0, fm_step = 0.0;
   unsigned long long far_reported = 0;
-  // a top model has a model among its children: only the general instantiation evaluates
-  // nested models (geometry.h PROG_SUB), so such scenes always run it, with the serial EVAL
-  // (no cooperative, culled or lean paths)
+  // a top model has a model or modifier among its children, or a top is a modifier: only the
+  // general instantiation evaluates composites below the top level (geometry.h node_value), so
+  // such scenes always run it, with the serial EVAL (no cooperative, culled or lean paths)
   bool nested = false;
   // the fold's workgroup run time: d_queue[MAX_SLOTS + 2] running total (s_memrealtime ticks at
   // wall_khz), reported per CU (one bk_reduce workgroup fills a CU)
@@ -937,7 +937,13 @@ struct smcrt_scene {
   // lean_kernel serves this scene: equal refractive indices, no detectors, a few tops, bucketed
   // deposition, axes below 2^20 cells (SMCRT_LEAN=0 keeps transport_kernel)
   bool lean_ok = false;
-  uint64_t lean_hazards = 0;
+  // deferred lean-kernel segments that ended in tflag or an error stop (lean.h "hazards"):
+  // running total d_queue[MAX_SLOTS + 3], reported by smcrt_scene_kernel_times and counted in
+  // SMCRT_CTR_FAULTS by the kernel
+  unsigned long long hazards_reported = 0;
+  // SMCRT_DEBUG_LEAN_MARGIN (tests only): 1 = "0", no margin; 2 = "all", every segment that
+  // starts in the grid is deferred (forces hazards on escaping segments)
+  uint32_t lean_debug = 0;
   int64_t lean_launches = 0;  // since the last smcrt_scene_kernel_times
   // voxel crossings per deposit segment, measured by the scene's launches (dep_ctl[6]): the
   // lean kernel pays for decoupled walks with a refill per crossing step, which long segments
@@ -1133,21 +1139,26 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     return fail(SMCRT_ERR_UNSUPPORTED, "grids of 2^32 or more voxels are not supported");
   for (int32_t i = 0; i < n_nodes; ++i) {
     const smcrt_sdf_node& nd = nodes[i];
-    if (nd.kind < SMCRT_SDF_SPHERE || nd.kind > SMCRT_SDF_MODEL)
+    if (nd.kind < SMCRT_SDF_SPHERE || nd.kind > SMCRT_SDF_DISPLACEMENT)
       return fail(SMCRT_ERR_INVALID_ARG, "node " + std::to_string(i) + ": unknown SDF kind");
     if (nd.kind == SMCRT_SDF_MODEL) {
       if (nd.n_children < 1 || nd.first_child < 0 || nd.first_child + nd.n_children > n_nodes)
         return fail(SMCRT_ERR_INVALID_ARG, "model node " + std::to_string(i) + ": bad child range");
       if (nd.op < SMCRT_OP_UNION || nd.op > SMCRT_OP_INTERSECTION)
         return fail(SMCRT_ERR_INVALID_ARG, "model node " + std::to_string(i) + ": bad CSG op");
+    } else if (composite_kind(nd.kind)) {  // a modifier wraps exactly one node
+      if (nd.n_children != 1 || nd.first_child < 0 || nd.first_child >= n_nodes)
+        return fail(SMCRT_ERR_INVALID_ARG, "modifier node " + std::to_string(i) + ": needs exactly one child");
+      if (nd.kind == SMCRT_SDF_DISPLACEMENT && nd.param[0] != (double)SMCRT_DISP_SINE)
+        return fail(SMCRT_ERR_INVALID_ARG, "displacement node " + std::to_string(i) + ": unknown function");
     }
   }
-  // models nested at most PROG_MAX_DEPTH levels (geometry.h PROG_NEST); this also rejects
-  // a model that contains itself
+  // models and modifiers nested at most PROG_MAX_DEPTH levels (geometry.h node_value); this
+  // also rejects a composite that contains itself
   {
     std::function<int(int32_t, int)> depth_ok = [&](int32_t idx, int lvl) -> int {
       const smcrt_sdf_node& nd = nodes[idx];
-      if (nd.kind != SMCRT_SDF_MODEL) return 1;
+      if (!composite_kind(nd.kind)) return 1;
       if (lvl >= PROG_MAX_DEPTH) return 0;
       for (int32_t c = 0; c < nd.n_children; ++c)
         if (!depth_ok(nd.first_child + c, lvl + 1)) return 0;
@@ -1155,7 +1166,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     };
     for (int32_t i = 0; i < n_top; ++i)
       if (top[i] >= 0 && top[i] < n_nodes && !depth_ok(top[i], 0))
-        return fail(SMCRT_ERR_UNSUPPORTED, "top " + std::to_string(i) + ": models nested more than " +
+        return fail(SMCRT_ERR_UNSUPPORTED, "top " + std::to_string(i) + ": models/modifiers nested more than " +
                                                std::to_string(PROG_MAX_DEPTH) + " levels deep are not supported");
   }
   for (int32_t i = 0; i < n_top; ++i)
@@ -1209,14 +1220,16 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   for (int32_t i = 0; i < n_top; ++i) {
     const smcrt_sdf_node& nd = nodes[top[i]];
     top_first[i] = (int32_t)prog.size();
-    if (nd.kind != SMCRT_SDF_MODEL) {
+    if (!composite_kind(nd.kind)) {
       prog.push_back(ProgOp{top[i], PROG_TOP, i + 1, 0, 0.0, translate_only(top[i]), 0});
+    } else if (nd.kind != SMCRT_SDF_MODEL) {  // a top-level modifier: one PROG_SUB op (geometry.h node_value)
+      prog.push_back(ProgOp{top[i], PROG_TOP | PROG_SUB, i + 1, 0, 0.0, 0, 0});
     } else {
-      // eval_model's left fold, children in order; a child model is one PROG_SUB op
-      // (geometry.h sdf_submodel)
+      // eval_model's left fold, children in order; a child model or modifier is one PROG_SUB
+      // op (geometry.h node_value)
       for (int32_t c = 0; c < nd.n_children; ++c) {
         const int32_t ci = nd.first_child + c;
-        const bool sub = nodes[ci].kind == SMCRT_SDF_MODEL;
+        const bool sub = composite_kind(nodes[ci].kind);
         prog.push_back(ProgOp{ci, (c == 0 ? PROG_CHILD_FIRST : PROG_CHILD) | (sub ? PROG_SUB : 0),
                               c == nd.n_children - 1 ? i + 1 : 0, nd.op, nd.k, sub ? 0 : translate_only(ci), 0});
       }
@@ -1236,7 +1249,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   {
     const char* ct = std::getenv("SMCRT_COOP_TAB");
     bool ok = s->coop_lanes > 0 && n_top <= 64 && !(ct && std::string(ct) == "0");
-    for (int32_t i = 0; ok && i < n_top; ++i) ok = nodes[top[i]].kind != SMCRT_SDF_MODEL;
+    for (int32_t i = 0; ok && i < n_top; ++i) ok = !composite_kind(nodes[top[i]].kind);
     if (ok) {
       ctab.assign(CTAB_DOUBLES, 0.0);
       for (int32_t i = 0; i < n_top; ++i) {
@@ -1286,13 +1299,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
-      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 3)) ||
+      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 4)) ||
       (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
     return cleanup_fail(st);
   hipError_t e = hipSuccess;
-  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 3) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 4) * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemcpy(s->d_nodes, nodes, sizeof(smcrt_sdf_node) * n_nodes, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_prog, prog.data(), sizeof(ProgOp) * prog.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !ctab.empty()) {
@@ -1416,6 +1429,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
     s->lean_ok = ok && s->lean_mode != 0 && !s->nested;
+    const char* dm = std::getenv("SMCRT_DEBUG_LEAN_MARGIN");
+    s->lean_debug = dm ? (std::string(dm) == "all" ? 2u : (std::string(dm) == "0" ? 1u : 0u)) : 0u;
   }
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
   s->n_cus = cus;
@@ -1510,11 +1525,6 @@ static void refine_rpp(smcrt_scene* s) {
       if (pool_log)
         std::fprintf(stderr, "[pool] slot %d: %u photons, %u records, %u overflowed, %u of %llu chunks\n", sl, h[4],
                      h[3], h[1], h[0], (unsigned long long)s->pool_chunks);
-      if (h[5]) {  // lean kernel: a deferred segment ended in tflag/fault (lean.h; never expected)
-        s->lean_hazards += h[5];
-        std::fprintf(stderr, "[smcrt] lean kernel: %u deferred voxel walks ended in an error stop or left the grid "
-                     "(parity not guaranteed for those photons)\n", h[5]);
-      }
       if (h[6] > 0) {  // voxel crossings per deposit segment of this scene's last launch
         s->xps = (double)(h[3] + h[1]) / (double)h[6];
         s->xps_measured = true;
@@ -1867,11 +1877,13 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.counters = (unsigned long long*)dt.counters;
   Ch.queue = nullptr;  // (set per launch: launch_one)
   Ch.far_steps = s->d_queue + MAX_SLOTS + 1;
+  Ch.lean_hazards = s->d_queue + MAX_SLOTS + 3;
   K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
   {
     const char* cd = std::getenv("SMCRT_DEBUG_CLAIM_DELAY");
     K.claim_delay = cd ? (uint32_t)std::strtoul(cd, nullptr, 10) : 0u;
   }
+  K.lean_debug = s->lean_debug;
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
@@ -2170,6 +2182,10 @@ int smcrt_scene_kernel_times(smcrt_scene* s, smcrt_kernel_times* out) {
   HIPCHK(hipMemcpy(&ticks, s->d_queue + MAX_SLOTS + 2, sizeof(ticks), hipMemcpyDeviceToHost));
   out->fold_cu_ms = (double)(ticks - s->fold_ticks_reported) / (double)s->wall_khz / (double)s->n_cus;
   s->fold_ticks_reported = ticks;
+  unsigned long long hz = 0;  // deferred lean segments that ended in tflag / an error stop (running total)
+  HIPCHK(hipMemcpy(&hz, s->d_queue + MAX_SLOTS + 3, sizeof(hz), hipMemcpyDeviceToHost));
+  out->lean_hazards = (int64_t)(hz - s->hazards_reported);
+  s->hazards_reported = hz;
   s->t_transport = s->t_deposit = 0.0;
   s->t_launches = 0;
   return SMCRT_OK;

@@ -85,6 +85,7 @@ struct KCold {
   uint32_t* bucket_fill;      // bucketed path: records in each bucket
   uint32_t* tile_nb;          // bucketed path: buckets claimed per tile
   unsigned long long* far_steps;  // march steps taken by the far-field march (far.h), running total
+  unsigned long long* lean_hazards;  // deferred lean segments ending in tflag / a fault (lean.h), running total
   SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
 
@@ -118,6 +119,9 @@ struct KParams {
   // debug knob (SMCRT_DEBUG_CLAIM_DELAY, tests only): s_sleep 127 this many times before a
   // bucket claim's CAS, so that other waves fill both buckets of the tile and wait (deposit.h)
   uint32_t claim_delay;
+  // debug knob (SMCRT_DEBUG_LEAN_MARGIN, tests only): 0 = lean.h's margin; 1 = no margin;
+  // 2 = every segment that starts in the grid is deferred, so escapes become counted hazards
+  uint32_t lean_debug;
   // exact SDF culling (cull.h), many-top scenes in the COOP instantiation; NULL = off
   const CullGrid* __restrict__ cull;
   // the cooperative EVAL's table of primitives (CTAB_ROWS x 64 doubles, column = top - 1),

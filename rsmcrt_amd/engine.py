@@ -79,6 +79,7 @@ def load_library(path: str = LIB_PATH):
         L.smcrt_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.smcrt_comm_init_rank.argtypes = [C.POINTER(C.c_uint8), C.c_int32, C.c_int32, C.c_int32,
                                            C.POINTER(C.c_void_p)]
+        L.smcrt_comm_info.argtypes = [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.smcrt_comm_destroy.argtypes = [C.c_void_p]
         L.smcrt_comm_destroy.restype = None
         L.smcrt_reduce_device_tallies.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(abi.DeviceTallies), C.c_int32,
@@ -254,7 +255,7 @@ class Engine:
         _check(load_library().smcrt_scene_kernel_times(self._h, C.byref(t)))
         return {"transport_ms": t.transport_ms, "deposit_ms": t.deposit_ms, "launches": t.launches,
                 "lean_launches": t.lean_launches, "far_steps": t.far_steps,
-                "fold_cu_ms": t.fold_cu_ms}
+                "fold_cu_ms": t.fold_cu_ms, "lean_hazards": t.lean_hazards}
 
 
 def pack_layout(grid, n_det_bins: int, fields: int) -> abi.PackLayout:
@@ -300,6 +301,16 @@ class Comm:
         h = C.c_void_p()
         _check(load_library().smcrt_comm_init_rank(buf, int(n_ranks), int(rank), int(device), C.byref(h)))
         self._h = h
+
+    def info(self) -> dict:
+        """The communicator's rank count and rank as RCCL reports them, and its device."""
+        n, r, d = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(load_library().smcrt_comm_info(self._h, C.byref(n), C.byref(r), C.byref(d)))
+        return {"n_ranks": n.value, "rank": r.value, "device": d.value}
+
+    @property
+    def n_ranks(self) -> int:
+        return self.info()["n_ranks"]
 
     def close(self):
         if getattr(self, "_h", None):

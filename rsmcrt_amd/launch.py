@@ -1,8 +1,8 @@
 """One process per GPU without an external launcher.
 
 `python bench.py --gpus N` (no torchrun) must still measure N GPUs. The parent process never
-initialises HIP: it counts the devices (torch.cuda.device_count() does not initialise the
-GPU on this image), fails loudly when fewer than N are visible, then starts N copies of the
+initialises HIP: it counts the devices from the KFD topology in sysfs (or amdsmi), fails
+loudly when fewer than N are visible or when neither can count them, then starts N copies of the
 same command with the environment torch.distributed.run would give them (RANK, LOCAL_RANK,
 WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and exits with the first
 non-zero child status (0 when every rank succeeds). Children inherit stdout/stderr, so rank
@@ -37,10 +37,65 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def _kfd_gpu_count():
+    """GPU agents in the KFD topology (sysfs text files; nothing is opened under /dev), or
+    None when the topology is not there. A node is a GPU when its simd_count is non-zero
+    (CPU nodes report 0) and this process may open its render node /dev/dri/renderD<minor>
+    (os.access only): a container sees the host's whole topology but only its own GPUs' render
+    nodes, which is the filter the HSA runtime applies too."""
+    try:
+        nodes = os.listdir(KFD_NODES)
+    except OSError:
+        return None
+    n = 0
+    for d in nodes:
+        try:
+            with open(os.path.join(KFD_NODES, d, "properties")) as f:
+                props = dict(l.split(None, 1) for l in f.read().splitlines() if " " in l)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0").strip() or 0) <= 0:
+            continue
+        minor = props.get("drm_render_minor", "").strip()
+        if minor and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+            continue
+        n += 1
+    return n
+
+
+def _amdsmi_gpu_count():
+    """GPUs amdsmi reports (it reads the driver's device files, never the HSA runtime), or
+    None when amdsmi is missing or fails."""
+    try:
+        import amdsmi
+        amdsmi.amdsmi_init()
+        try:
+            return len(amdsmi.amdsmi_get_processor_handles())
+        finally:
+            amdsmi.amdsmi_shut_down()
+    except Exception:
+        return None
+
+
 def visible_gpus() -> int:
-    """Visible HIP devices, counted without initialising the GPU."""
-    import torch
-    return int(torch.cuda.device_count())
+    """Visible GPUs, counted without initialising HIP or HSA in this process (a parent that did
+    would hold the device while its ranks start, and on this pool must never exec afterwards):
+    the KFD topology in sysfs, else amdsmi, capped by ROCR_/HIP_/CUDA_VISIBLE_DEVICES. Raises
+    LaunchError when neither source answers (torch.cuda.device_count() is not used: it falls
+    back to hipGetDeviceCount when amdsmi fails)."""
+    n = _kfd_gpu_count()
+    if n is None:
+        n = _amdsmi_gpu_count()
+    if n is None:
+        raise LaunchError("cannot count GPUs: no KFD topology under /sys/class/kfd and no working amdsmi")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
 
 
 def rank_env(rank: int, world: int, port: int, base=None) -> dict:

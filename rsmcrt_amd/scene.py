@@ -217,6 +217,61 @@ def model(children, op=abi.OP_UNION, k=0.0) -> Model:
     return Model(list(children), op, float(k))
 
 
+@dataclass
+class Modifier:
+    """A modifier of sdfModifiers.f90 wrapping one SDF (primitive, model or modifier). Like the
+    reference's *_init functions it takes the layer and optics of what it wraps; its own
+    transform is the identity and is never applied."""
+    kind: int
+    child: object
+    param: List[float]
+
+    @property
+    def opt(self) -> Mono:
+        return self.child.opt
+
+    @property
+    def layer(self) -> int:
+        return self.child.layer
+
+
+def revolution(prim, o, center=(0.0, 0.0, 0.0)) -> Modifier:
+    """revolution_init(prim, o, center) sdfModifiers.f90:232-259."""
+    return Modifier(abi.SDF_REVOLUTION, prim, [float(o), *map(float, center)])
+
+
+def extrude(prim, h) -> Modifier:
+    """extrude_init(prim, h) :143-159."""
+    return Modifier(abi.SDF_EXTRUDE, prim, [float(h)])
+
+
+def onion(prim, thickness) -> Modifier:
+    """onion_init(prim, thickness) :261-277."""
+    return Modifier(abi.SDF_ONION, prim, [float(thickness)])
+
+
+def twist(prim, k) -> Modifier:
+    """twist_init(prim, k) :126-141. Its k is a default (single precision) real, so the stored
+    k is the float32 rounding of the value, widened."""
+    return Modifier(abi.SDF_TWIST, prim, [float(np.float32(k))])
+
+
+def bend(prim, k) -> Modifier:
+    """bend_init(prim, k) :196-212."""
+    return Modifier(abi.SDF_BEND, prim, [float(k)])
+
+
+def elongate(prim, size: Vec) -> Modifier:
+    """elongate_init(prim, size) :161-176."""
+    return Modifier(abi.SDF_ELONGATE, prim, [float(v) for v in size])
+
+
+def displacement_sine(prim, amplitude, freq: Vec) -> Modifier:
+    """displacement_init(prim, func) :178-194 with the built-in f(p) = a sin(fx x) sin(fy y)
+    sin(fz z) (smcrt.h SMCRT_DISP_SINE): the reference takes any procedure(primitive)."""
+    return Modifier(abi.SDF_DISPLACEMENT, prim, [float(abi.DISP_SINE), float(amplitude), *map(float, freq)])
+
+
 class Scene:
     """An ordered sdfs_array (reference index i+1 == tauint2 layer) flattened to nodes."""
 
@@ -231,7 +286,22 @@ class Scene:
         pending = list(zip(top, self.sdfs))
         while pending:
             idx, s = pending.pop(0)
-            if isinstance(s, Model):
+            if isinstance(s, Modifier):
+                nd = abi.SdfNode()
+                nd.kind = int(s.kind)
+                nd.layer = int(s.layer)
+                for i, v in enumerate(_colmajor(identity())):
+                    nd.transform[i] = v
+                for i, v in enumerate(s.param):
+                    nd.param[i] = float(v)
+                o = s.opt
+                nd.mus, nd.mua, nd.hgg, nd.n = o.mus, o.mua, o.hgg, o.n
+                nd.first_child = len(nodes)
+                nd.n_children = 1
+                nodes.append(None)
+                pending.append((nd.first_child, s.child))
+                nodes[idx] = nd
+            elif isinstance(s, Model):
                 nd = abi.SdfNode()
                 nd.kind = abi.SDF_MODEL
                 nd.layer = int(s.layer)

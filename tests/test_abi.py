@@ -33,6 +33,14 @@ def test_exports(lib_path):
         assert fn in exported, fn
 
 
+def test_abi_version_matches_header():
+    """The header, the ctypes mirror and the Fortran module agree on the version; version 4 is
+    the 56-byte smcrt_kernel_times (lean_hazards)."""
+    txt = open(HEADER).read()
+    assert int(re.search(r"#define SMCRT_ABI_VERSION (\d+)", txt).group(1)) == abi.SMCRT_ABI_VERSION == 4
+    assert C.sizeof(abi.KernelTimes) == 56
+
+
 def test_load_and_version(lib_path):
     from rsmcrt_amd import engine
     L = engine.load_library(lib_path)
@@ -62,7 +70,8 @@ STRUCTS = {
     "smcrt_photon_record": (abi.PhotonRecord, ["pos", "weight", "cell", "draws", "status"]),
     "smcrt_tallies": (abi.Tallies, ["jmean", "jmean_f64", "det_bins", "counters", "records"]),
     "smcrt_device_tallies": (abi.DeviceTallies, ["jmean", "det_bins", "records"]),
-    "smcrt_kernel_times": (abi.KernelTimes, ["transport_ms", "deposit_ms", "launches"]),
+    "smcrt_kernel_times": (abi.KernelTimes, ["transport_ms", "deposit_ms", "launches", "lean_launches", "far_steps",
+                                             "fold_cu_ms", "lean_hazards"]),
     "smcrt_pack_layout": (abi.PackLayout, ["n_voxels", "n_det_bins", "fields"]),
     "smcrt_escape_config": (abi.EscapeConfig, ["symmetry", "n", "max", "pos", "dir", "rotation"]),
     "smcrt_inverse_config": (abi.InverseConfig, ["layer", "flags", "max_steps", "max_step_size", "accuracy", "seed"]),

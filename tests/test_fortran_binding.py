@@ -112,7 +112,7 @@ def test_example_multi_gpu_matches_single(lib_path, tmp_path):
 
 
 # ---- the conversion glue (bindings/fortran/smcrt_glue.f90) ----------
-GLUE_SCENES = ("scat_test", "aptran", "validation1", "omg", "test_dects")
+GLUE_SCENES = ("scat_test", "aptran", "validation1", "omg", "test_dects", "egg_test")
 SRC_FIELDS = ("pos", "dir", "p1", "p2", "p3", "radius", "beam_size", "focal_length", "rlo", "rhi", "sigma", "rotation")
 
 

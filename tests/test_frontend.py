@@ -104,8 +104,21 @@ def test_sphere_scene_build_defined_list():
     assert Job(res("sphere.toml")).nodes[7].param[0] == j.nodes[7].param[0]  # deterministic
 
 
+def test_egg_revolution_modifiers():
+    """egg_test.toml: setup_egg (setupGeometry.f90:149-248), two Moss eggs revolved about the
+    y axis (the revolution modifier, sdfModifiers.f90:286-303), a yolk sphere and a bounding
+    box; numOptProp = 3 with the default mus = 1, mua = 0, hgg = 0, n = 1 of each layer."""
+    j = Job(res("egg_test.toml"))
+    assert j.experiment == "egg" and j.desc.n_top == 4
+    same_scene(j, builders.setup_egg([1.0] * 3, [0.0] * 3, [0.0] * 3, [1.0] * 3, (0.0, 0.0, 0.0), (5.0, 5.0, 5.0),
+                                     2.0, 1.5, 1.4, 0.02, 1.0))
+    assert [j.nodes[i].kind for i in range(6)] == [abi.SDF_SPHERE, abi.SDF_REVOLUTION, abi.SDF_REVOLUTION, abi.SDF_BOX,
+                                                   abi.SDF_EGG, abi.SDF_EGG]
+    meta = dict(l.split(" = ", 1) for l in j.metadata().strip().splitlines())
+    assert meta["BottomSphereRadius"] == "2.0" and meta["ShellThickness"] == "0.02" and meta["YolkRadius"] == "1.0"
+
+
 @pytest.mark.parametrize("name,code,why", [
-    ("egg_test.toml", abi.ERR_UNSUPPORTED, "revolution"),
     ("logo.toml", abi.ERR_UNSUPPORTED, "svg"),
     ("vessels.toml", abi.ERR_UNSUPPORTED, "edges.dat"),
     # resdir//"test/parse/test.png" does not exist under res/ (parse_spectrum.f90:87-92)

@@ -829,3 +829,75 @@ def test_lean_kernel_paths(monkeypatch, case):
         assert cpu.counter("absorbed") > n // 2
     if case == "test-kernel":
         np.testing.assert_allclose(runs["1"].moments, cpu.moments, rtol=1e-12)
+
+
+@pytest.mark.parametrize("knob", ["0", "all"])
+def test_lean_hazards_counted_as_faults(monkeypatch, knob):
+    """A deferred lean-kernel walk (lean.h) must never end in tflag or an error stop; if one
+    did, its photon would already have gone on as if the walk stayed inside the grid. Every
+    such "hazard" is counted in SMCRT_CTR_FAULTS and returned in kernel_times.lean_hazards
+    (INTEGRATION.md §6). The debug knob SMCRT_DEBUG_LEAN_MARGIN provokes them on the
+    boundary-source scene: "0" drops the walk's margin from the grid faces, "all" defers every
+    segment that starts in the grid, so walks that leave the grid become hazards. Without the
+    knob the same run has no hazard and equals the oracle; with it, the faults counter equals
+    the oracle's plus the hazards."""
+    sc = builders.setup_sphere(5.0, 0.5, 0.8, 1.0, 1.0)
+    src = scene.uniform_source((-1.0, -1.0, 0.999), (2.0, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    g = scene.grid(48, 48, 48, 1, 1, 1)
+    n = 30000
+    monkeypatch.setenv("SMCRT_LEAN", "1")
+    with Engine(sc, g) as eng:
+        eng.kernel_times()
+        clean = eng.run(src, n, seed=SEED, records=True)
+        kt_clean = eng.kernel_times()
+    monkeypatch.setenv("SMCRT_DEBUG_LEAN_MARGIN", knob)
+    with Engine(sc, g) as eng:
+        eng.kernel_times()
+        haz = eng.run(src, n, seed=SEED, records=True)
+        kt = eng.kernel_times()
+    cpu = O.run(sc, g, src, n, seed=SEED, records=True)
+    assert kt_clean["lean_launches"] > 0 and kt_clean["lean_hazards"] == 0, kt_clean
+    compare(clean, cpu)
+    assert kt["lean_launches"] > 0, kt
+    if knob == "all":
+        assert kt["lean_hazards"] > 0, kt
+    assert haz.counter("faults") == cpu.counter("faults") + kt["lean_hazards"], (haz.counter("faults"), kt)
+
+
+def test_egg_scene_revolution():
+    """res/egg_test.toml's scene (setup_egg, setupGeometry.f90:149-248: two Moss eggs revolved
+    about y by the revolution modifier, a yolk, a bounding box) at 64^3, through the general
+    instantiation's composite evaluator (geometry.h node_value), bit-exact against the oracle.
+    Distinct optical properties per layer so that every layer matters."""
+    sc = builders.setup_egg([8.0, 3.0, 15.0], [0.2, 0.05, 1.0], [0.8, 0.6, 0.9], [1.0, 1.0, 1.0],
+                            (0.0, 0.0, 0.0), (5.0, 5.0, 5.0))
+    gpu, cpu = both(sc, scene.grid(64, 64, 64, 2.5, 2.5, 2.5), scene.point_source(), 3000,
+                    flags=abi.FLAG_PATHLENGTH | abi.FLAG_RENDER_SOURCE)
+    compare(gpu, cpu)
+    assert cpu.counter("absorbed") > 0 and cpu.counter("faults") == 0
+
+
+def test_modifier_scenes():
+    """Every modifier of sdfModifiers.f90 in one Fresnel scene (refractive indices differ, so
+    calcNormal and reflect_refract evaluate them too): extrude, onion, twist, bend, elongate,
+    displacement, and a revolved CSG model, with a pencil and a point source; bit-exact
+    against the oracle."""
+    from rsmcrt_amd.scene import box as bx, model, mono as mo, sphere as sp, torus as to, translate, invert
+    o1, o2, o3 = mo(5.0, 0.5, 0.7, 1.2), mo(2.0, 0.1, 0.3, 1.0), mo(9.0, 0.2, 0.9, 1.4)
+    tops = [
+        scene.onion(sp(0.25, o1, 1, transform=invert(translate((0.5, 0.5, 0.0)))), 0.05),
+        scene.twist(bx((0.3, 0.2, 0.6), o2, 2, transform=invert(translate((-0.5, 0.5, 0.0)))), 2.5),
+        scene.bend(bx((0.5, 0.1, 0.2), o3, 3, transform=invert(translate((0.0, -0.5, 0.3)))), 1.5),
+        scene.elongate(to(0.12, 0.04, o1, 4, transform=invert(translate((0.5, -0.5, -0.4)))), (0.1, 0.0, 0.05)),
+        scene.displacement_sine(sp(0.2, o2, 5, transform=invert(translate((-0.5, -0.5, -0.3)))), 0.02, (9.0, 7.0, 5.0)),
+        scene.extrude(sp(0.2, o3, 6, transform=invert(translate((0.0, 0.0, 0.5)))), 0.1),
+        scene.revolution(model([sp(0.1, o1, 7), bx((0.1, 0.3, 0.1), o1, 7)], abi.OP_SMOOTH_UNION, 0.05), 0.3,
+                         center=(0.0, 0.1, -0.5)),
+        bx((2.0, 2.0, 2.0), mo(0.5, 0.01, 0.0, 1.0), 8),
+    ]
+    sc = scene.Scene(tops)
+    g = scene.grid(48, 48, 48, 1, 1, 1)
+    for src, n in ((scene.point_source(), 3000), (scene.pencil_source((0.0, 0.0, 0.99), (0.0, 0.0, -1.0)), 3000)):
+        gpu, cpu = both(sc, g, src, n)
+        compare(gpu, cpu)
+        assert cpu.counter("fresnel") > 0

@@ -21,6 +21,8 @@ for p in $PASSES; do
     fetch) run pmc_fetch --pmc FETCH_SIZE ;;
     write) run pmc_write --pmc WRITE_SIZE ;;
     tcc) run pmc_tcc --pmc TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum ;;
+    stall1) run pmc_stall1 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_VMEM ;;
+    stall2) run pmc_stall2 --pmc SQ_IFETCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_LDS_IDX_ACTIVE SQ_INSTS_SENDMSG ;;
     valu) run pmc_valu --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_LDS SQ_INSTS_SMEM ;;
   esac
 done
