@@ -337,6 +337,7 @@ def reference_pinned(device):
         out[f"{which}_absorb_depth_vs_fit"] = {"photons": d.n_photons, "rel_rms": rep["rel_rms"],
                                                "integral_ratio": rep["integral_ratio"], "bins": rep["bins"],
                                                "model_term": refval.model_term(which),
+                                               "model_term_note": refval.MODEL_TERM_NOTE,
                                                "bins_outside_4sigma_plus_model": len(rep["failed"]), "pass": ok}
     j = Job(os.path.join(ROOT, "tests", "golden", "res", "validateFibreDect.toml"))
     d = j.desc

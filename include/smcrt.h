@@ -554,6 +554,10 @@ int smcrt_reduce_device_tallies(smcrt_scene* scene, smcrt_comm* comm, smcrt_devi
  * every device's accumulators onto the first device with ONE packed RCCL reduce, adds them
  * into `io` as smcrt_run does and zeroes the accumulators. A job split into batches therefore
  * pays one collective when it collects (per checkpoint, or once), not one per batch.
+ * If a launch fails inside smcrt_multi_accumulate, everything accumulated since the last
+ * collect is discarded (the devices are fenced, the accumulators zeroed) and the error is
+ * returned, so a later collect never sums partial tallies; smcrt_multi_device_photons tells
+ * how many photons the accumulators hold.
  * smcrt_multi_run = accumulate + collect. Results do not depend on the number of devices or
  * on which device ran which chunk (up to the fp64 summation order of jmean); counters and
  * integer tallies are exact. Photon records are refused (use smcrt_run). */

@@ -980,7 +980,11 @@ static int job_run_impl(smcrt_job* J0, int32_t device, const std::vector<int32_t
   // reference's checkpoint layout (writer.f90:426-457). Without checkpoints the whole job is
   // one batch. With several GPUs the batches accumulate on the devices and are reduced (one
   // RCCL collective) only when a checkpoint is written and at the end.
-  constexpr int64_t MIN_BATCH = 4 << 20;
+  // SMCRT_JOB_MIN_BATCH (photons per GPU) overrides the minimum: 1 writes a checkpoint at
+  // every multiple of checkpoint_every_n, exactly the reference's cadence, at the cost of one
+  // launch (and with several GPUs one collective) per checkpoint
+  int64_t MIN_BATCH = 4 << 20;
+  if (const char* mb = std::getenv("SMCRT_JOB_MIN_BATCH")) MIN_BATCH = std::max<int64_t>(1, std::strtoll(mb, nullptr, 10));
   const int64_t every = J->ckptfreq > 0 ? J->ckptfreq : std::max<int64_t>(1, J->nphotons);
   const int64_t want = MIN_BATCH * (int64_t)std::max<size_t>(1, devices.size());
   const int64_t batch = J->ckptfreq > 0 ? every * ((want + every - 1) / every) : every;

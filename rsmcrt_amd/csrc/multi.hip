@@ -430,6 +430,19 @@ static smcrt_device_tallies device_tallies(const smcrt_multi* m, size_t g) {
   return dt;
 }
 
+// Throw away everything accumulated since the last collect (after a failed launch): wait for
+// every device, zero its accumulators and photon count, so that a later collect never adds
+// partial tallies whose photons no caller counted.
+static void discard_locked(smcrt_multi* m) {
+  for (size_t g = 0; g < m->devices.size(); ++g) {
+    if (hipSetDevice(m->devices[g]) != hipSuccess) continue;
+    (void)hipDeviceSynchronize();
+    if (m->d_buf[g]) (void)hipMemset(m->d_buf[g], 0, sizeof(double) * (size_t)m->o.total);
+    if (m->d_ctr[g]) (void)hipMemset(m->d_ctr[g], 0, sizeof(unsigned long long) * SMCRT_NCOUNTERS);
+    m->photons[g] = 0;
+  }
+}
+
 // Photons [first, first + n) in chunks handed to whichever device has a free launch slot
 // (guided: a chunk is half of what is left per device, at least `min_chunk`), each an
 // overlapped smcrt_run_device into that device's accumulators. A chunk's results do not
@@ -458,7 +471,11 @@ static int accumulate_locked(smcrt_multi* m, const smcrt_source* src, const smcr
       c.first_photon = cfg->first_photon + issued;
       smcrt_device_tallies dt = device_tallies(m, g);
       const int rs = smcrt_run_device(s, src, &c, &dt, smcrt::scene_stream(s));
-      if (rs) return rs;
+      if (rs) {  // (the chunks already launched would leave partial tallies behind)
+        const std::string msg = g_last_error;
+        discard_locked(m);
+        return fail(rs, msg + " (smcrt_multi_accumulate: the photons accumulated since the last collect were discarded)");
+      }
       m->photons[g] += k;
       issued += k;
       launched = true;

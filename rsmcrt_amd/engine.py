@@ -375,7 +375,11 @@ class MultiEngine:
     def accumulate(self, source, n_photons, seed=123456789, flags=abi.FLAG_PATHLENGTH, first_photon=0):
         """Launch photons [first_photon, +n_photons) over the devices; nothing is waited for."""
         cfg = Engine.config(n_photons, seed, flags, first_photon)
-        _check(load_library().smcrt_multi_accumulate(self._h, C.byref(source), C.byref(cfg)))
+        try:
+            _check(load_library().smcrt_multi_accumulate(self._h, C.byref(source), C.byref(cfg)))
+        except SmcrtError:
+            self._pending = 0  # (the library discarded everything since the last collect)
+            raise
         self._pending += int(n_photons)
 
     def device_photons(self):
@@ -387,7 +391,9 @@ class MultiEngine:
     def collect(self, result: Result | None = None) -> Result:
         """One packed RCCL reduce of everything accumulated since the last collect."""
         res = result if result is not None else Result(self.grid, self.dets, 0)
-        res.n_photons += self._pending
+        held = sum(self.device_photons())  # the library's own count of what the accumulators hold
+        assert held == self._pending, (held, self._pending)
+        res.n_photons += held
         self._pending = 0
         t = res.tallies()
         _check(load_library().smcrt_multi_collect(self._h, C.byref(t)))

@@ -46,16 +46,29 @@ def to_reference_units(sums, n_photons, dz):
     return sums / REF_XY * (REF_DZ / dz) * (REF_N / n_photons)
 
 
+# An independent ceiling on the model term: the blanket 5 % of round 2, chosen before any
+# calibration on the restatement. The measured per-target terms must stay below it.
+MODEL_CEILING = 0.05
+# The per-target term is calibrated on the CPU restatement itself, so a systematic bias of the
+# restatement would be built into it: agreement within it is "parity unpinned", evidence only
+# that the GPU equals the restatement and that neither drifted past the ceiling.
+MODEL_TERM_NOTE = ("parity unpinned: the model term is calibrated on the CPU restatement "
+                   "(tests/golden/ri_model_residual.json), capped by an independent 5 % ceiling")
+
+
 def model_term(which: str) -> float:
     """The fit's own inaccuracy for target `which`, measured (not chosen): the largest
     |mean transport profile - fit| / fit over the tested bins, plus 3 standard errors, from 8
     seeds x 1e6 photons of the CPU restatement (tests/golden/make_ri_model_residual.py ->
-    tests/golden/ri_model_residual.json): validation2 3.5 %, validation3 2.0 %."""
+    tests/golden/ri_model_residual.json): validation2 3.5 %, validation3 2.0 %. Never more
+    than MODEL_CEILING (an AssertionError if the calibration ever claims more)."""
     import json
     import os
     p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ri_model_residual.json")
     with open(p) as f:
-        return float(json.load(f)[which]["model_term"])
+        m = float(json.load(f)[which]["model_term"])
+    assert 0.0 <= m <= MODEL_CEILING, (which, m)
+    return m
 
 
 def compare_profile(sim, fit, depths, sigma, rel_model, k_sigma=4.0, rebin=5, floor=0.01):
