@@ -275,9 +275,11 @@ def fp64_roofline(sc, sdf_evals_per_launch, kern_ms):
             "frac": ach / FP64_PEAK_TFLOPS, "sdf_flop_per_launch": flop, "flop_per_array_eval": flop_per_eval(sc)}
 
 
-# Issue cycles per wave64 VALU instruction on one SIMD-32 (profiles/r01_valu_rates.txt for
-# fp64, MI355X_MICROARCH.md for 32-bit: 2 cycles with >= 2 waves per SIMD)
-VALU_CYCLES = {"f64_addmulfma": 5.0, "f64_trans": 17.0, "int64": 8.0, "other_32bit": 2.0}
+# Issue cycles per wave64 VALU instruction on one SIMD, measured on MI355X with 3 waves per
+# SIMD and 8 independent chains (tools/microbench/valu_rates.hip, profiles/r04_s1/valu_rates.txt:
+# v_add_u32 / v_xor_b32 / v_mul_f32 3.2, fp64 add/mul/fma 5.1, v_rcp_f64 16.8, v_mad_u64_u32 7.7;
+# round 3 assumed 2 cycles for 32-bit ops, which under-stated the utilisation)
+VALU_CYCLES = {"f64_addmulfma": 5.1, "f64_trans": 16.8, "int64": 7.7, "other_32bit": 3.2}
 SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 

@@ -613,8 +613,9 @@ int smcrt_write_checkpoint(const char* filename, const char* toml_filename, int6
  * smcrt_job_load reads a res/<name>.toml file with the reference's keys, defaults and error
  * messages. It builds the scene the way setup_simulation does and keeps the output and
  * simulation settings.
- *   Geometries: sphere, box, test_box, scat_test, scat_test2, aptran, sphere_scene, exp, omg.
- *     vessels (needs data files the reference does not ship), egg and logo return
+ *   Geometries: sphere, box, test_box, scat_test, scat_test2, aptran, sphere_scene, exp, omg,
+ *     egg (ABI 4: revolution modifiers). vessels (needs data files the reference does not ship)
+ *     and logo (the reference stops on it, setupGeometry.f90:326-328) return
  *     SMCRT_ERR_UNSUPPORTED.
  *   Sources: point, uniform, pencil; a constant spectrum.
  *   Detectors: circle, annulus, camera, grouped by type as parse_detectors does.

@@ -56,15 +56,10 @@ __host__ __device__ __forceinline__ double csg(int32_t op, double d1, double d2,
 // sdf_prim_s reads the primitive's kind, transform t[0..11] and parameters P[0..7] with a
 // stride of S doubles (S = 1: a node; S = 64: the cooperative EVAL's LDS table, one column
 // per lane, transport.h); sdf_prim is it applied to a node.
+// sdf_shape_s is the primitive's formula at its local point p; sdf_prim_s forms p first.
 template <int S>
-__host__ __device__ __forceinline__ double sdf_prim_s(int32_t kind, const double* __restrict__ t,
-                                                      const double* __restrict__ P_, V3 pos, bool translate_only) {
+__host__ __device__ __forceinline__ double sdf_shape_s(int32_t kind, const double* __restrict__ P_, const V3 p) {
 #define P(i) P_[(i) * S]
-#define T(i) t[(i) * S]
-  const V3 p = translate_only ? v3(pos.x + T(3), pos.y + T(7), pos.z + T(11))
-                              : v3(T(0) * pos.x + T(1) * pos.y + T(2) * pos.z + T(3),
-                                   T(4) * pos.x + T(5) * pos.y + T(6) * pos.z + T(7),
-                                   T(8) * pos.x + T(9) * pos.y + T(10) * pos.z + T(11));  // dotmat
   switch (kind) {
     case SMCRT_SDF_SPHERE:  // :494-508
       return sqrt(p.x * p.x + p.y * p.y + p.z * p.z) - P(0);
@@ -150,7 +145,18 @@ __host__ __device__ __forceinline__ double sdf_prim_s(int32_t kind, const double
       return __builtin_nan("");
   }
 #undef P
+}
+
+template <int S>
+__host__ __device__ __forceinline__ double sdf_prim_s(int32_t kind, const double* __restrict__ t,
+                                                      const double* __restrict__ P_, V3 pos, bool translate_only) {
+#define T(i) t[(i) * S]
+  const V3 p = translate_only ? v3(pos.x + T(3), pos.y + T(7), pos.z + T(11))
+                              : v3(T(0) * pos.x + T(1) * pos.y + T(2) * pos.z + T(3),
+                                   T(4) * pos.x + T(5) * pos.y + T(6) * pos.z + T(7),
+                                   T(8) * pos.x + T(9) * pos.y + T(10) * pos.z + T(11));  // dotmat
 #undef T
+  return sdf_shape_s<S>(kind, P_, p);
 }
 
 __host__ __device__ __forceinline__ double sdf_prim(const smcrt_sdf_node* __restrict__ nd, V3 pos, bool translate_only) {

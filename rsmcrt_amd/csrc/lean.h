@@ -86,8 +86,33 @@ namespace smcrt {
 #define SMCRT_LEAN_EVENT_LANES 20
 #endif
 constexpr uint32_t ST_ABSORB = 40;  // absorbed; recordWeight waits for the photon's cells
+// The block's event pool (see "Event pool" below; off by default): interactions of every wave
+// of the block are queued in LDS and run by whichever wave has SMCRT_LEAN_POOL_MIN of them (or
+// nothing else to do), so the event code runs on fuller waves than one wave's own events fill.
+// Measured on M1 (same box, round 4, profiles/r04_s2/ab_pool.txt): 196-204 M photons/s
+// against 207-213 M without it (bit-exact either way): the pooled events' extra LDS traffic,
+// the two segment slots its LDS forces and the separate runs of the remaining local events
+// cost more than the fuller event waves save.
+#ifndef SMCRT_LEAN_POOL
+#define SMCRT_LEAN_POOL 0
+#endif
+#ifndef SMCRT_LEAN_POOL_MIN
+#define SMCRT_LEAN_POOL_MIN 48
+#endif
+// With the pool, the events a wave still runs itself (completion, emission, the tauint2 entry
+// after an emission, interactions that end the photon) are one or two per photon, and a
+// finished photon's lane takes no new photon until they have run: run them once this many
+// wait (the interactions' batch size, SMCRT_LEAN_EVENT_LANES, would leave lanes empty;
+// 4 measured best of 1 and 4).
+#ifndef SMCRT_LEAN_LOCAL_EVENT_LANES
+#define SMCRT_LEAN_LOCAL_EVENT_LANES 4
+#endif
 #ifndef SMCRT_LEAN_SLOTS
+#if SMCRT_LEAN_POOL
+#define SMCRT_LEAN_SLOTS 2  // (the pool's LDS: two slots keep three blocks per CU)
+#else
 #define SMCRT_LEAN_SLOTS 3
+#endif
 #endif
 constexpr uint32_t LEAN_SLOTS = SMCRT_LEAN_SLOTS;  // segments a photon may have in flight (<= 4)
 // Ring entries per wave. Idle walkers refill from the ring at the end of every walk phase, so
@@ -114,6 +139,17 @@ struct LeanShared {
   uint32_t busy[256];                         // bit s: slot s holds a segment in flight
   uint32_t lu[3][256];                        // interactions, nscatt, status of the photon (LL_*)
   uint32_t wctr[4][LC_N];                     // per-wave counters
+#if SMCRT_LEAN_POOL
+  // the event pool: per photon (thread) an in/out slot, and a ring of queued owners
+  double ev_dir[3][256];     // in: direction; out: the scattered direction
+  double ev_cached[256];     // in/out: the RNG's cached half block
+  double ev_tau[256];        // out: the new optical depth
+  uint32_t ev_pid[2][256];   // in: photon index words
+  uint32_t ev_draws[256];    // in/out: draws taken
+  uint32_t ev_code[256];     // in: layer; out: EV_DONE | result bits (written last)
+  uint32_t eq[256];          // ticket << 8 | owner thread, written after the owner's slot
+  uint32_t eq_head, eq_tail; // tickets: claimed by processors / reserved by producers
+#endif
 };
 
 __device__ __forceinline__ unsigned long long lean_pack(int32_t x, int32_t y, int32_t z) {
@@ -145,7 +181,9 @@ enum : uint32_t {
   LF_WAIT = 16u,   // waiting for a synchronous segment
   LF_CELLS = 32u,  // xcell/ycell/zcell are the photon's cells
   LF_MOVE_FWD = 64u, LF_MOVE_BACK = 128u,  // the move after the request
+  LF_EVQ = 256u,   // the photon's interaction is queued in the block's event pool
 };
+enum : uint32_t { EV_DONE = 1u << 31, EV_ABSORB = 1u, EV_RUNAWAY = 2u };  // LeanShared::ev_code results
 struct LeanPhoton {
   V3 pos, dir;
   Rng rng;
@@ -173,7 +211,7 @@ __device__ __forceinline__ void lean_count(LeanShared* sh, int c) {
 // g_diag[0..15] at the end of each wave (the host prints them per launch), and the s_memtime
 // share of each phase in g_diag_t[1..8].
 enum : int { LD_TRIPS = 0, LD_WSTEPS, LD_WLANES, LD_PUSH, LD_SYNC, LD_BLOCKED, LD_EVALS, LD_ELANES, LD_P7,
-             LD_REVERT, LD_WAITING, LD_IDLE, LD_RING, LD_EVWAIT, LD_BUSY, LD_N };
+             LD_REVERT, LD_WAITING, LD_IDLE, LD_RING, LD_EVWAIT, LD_BUSY, LD_POOL, LD_POOLN, LD_P7LANES, LD_N };
 #define LDIAG(i, v) (ld[(i)] += (uint64_t)(v))
 #define LDIAG_T(i)                                                  \
   do {                                                              \
@@ -231,6 +269,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   for (int c = lane_id; c < LC_N; c += 64) sh->wctr[wv][c] = 0;
   for (int f = 0; f < 3; ++f) sh->lu[f][threadIdx.x] = 0;
   sh->busy[threadIdx.x] = 0;
+#if SMCRT_LEAN_POOL
+  sh->eq[threadIdx.x] = ((threadIdx.x - 256u) & 0xFFFFFFu) << 8;  // (no ticket matches before it is written)
+  if (threadIdx.x == 0) sh->eq_head = sh->eq_tail = 0;
+#endif
   __syncthreads();
 
   // lean_margin (see the header comment), per axis, corner coordinates. The debug knob
@@ -273,6 +315,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
   unsigned long long lt[9] = {};
   unsigned long long lt_last = __builtin_amdgcn_s_memtime();
 #endif
+#if SMCRT_LEAN_POOL
+  // a pooled interaction's results (written by whichever wave ran it), see "Event pool"
+  auto pickup = [&]() {
+    if (P.has(LF_EVQ)) {
+      const uint32_t code = __hip_atomic_load(&sh->ev_code[threadIdx.x], __ATOMIC_ACQUIRE,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (code & EV_DONE) {
+        P.clr(LF_EVQ);
+        P.rng.draws = sh->ev_draws[threadIdx.x];
+        P.rng.cached = sh->ev_cached[threadIdx.x];
+        if (code & EV_ABSORB) {  // absorbed: recordWeight once the cells are in
+          P.set(LF_TFLAG);
+          P.st = ST_ABSORB;
+        } else {  // scattered, then the next tauint2 entry
+          if (code & EV_RUNAWAY) P.set(LF_FAULT | LF_TFLAG);
+          P.dir = v3(sh->ev_dir[0][threadIdx.x], sh->ev_dir[1][threadIdx.x], sh->ev_dir[2][threadIdx.x]);
+          P.tau = sh->ev_tau[threadIdx.x];
+          P.taurun = 0.0;
+          P.hop = 0;
+          P.st = ST_H0;
+        }
+      }
+    }
+  };
+#endif
+  // P8: arrive at the hop-loop head, inttau2.f90:61
+  auto p8 = [&]() {
+    if (!(P.f & (LF_REQ | LF_WAIT | LF_PEND)) && P.st == ST_H0) {
+      if (!(P.taurun <= P.tau)) P.st = ST_T2END;
+      else if (++P.hop > (uint32_t)MAX_HOP_ITERS) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; }
+      else P.set(LF_PEND);
+    }
+  };
   for (;; ++w_iters) {
     LDIAG_T(8);
     LDIAG(LD_TRIPS, 1);
@@ -307,6 +382,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       if (__ballot(P.st != ST_IDLE || W.seg) == 0 && head == tail) break;
     }
 
+#if SMCRT_LEAN_POOL
+    // results other waves wrote since this wave's last P7: the photon evaluates this trip
+    if (__ballot(P.has(LF_EVQ))) {
+      pickup();
+      p8();
+    }
+#endif
     LDIAG(LD_WAITING, __popcll(__ballot(P.has(LF_WAIT))));
     LDIAG(LD_IDLE, __popcll(__ballot(P.st == ST_IDLE)));
     LDIAG(LD_BUSY, __popcll(__ballot(P.st != ST_IDLE)));
@@ -581,14 +663,121 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
       P.st = ST_DONE;
     }
     // ---- P7: photon events, batched as in transport_kernel ---------------------------------
+#if SMCRT_LEAN_POOL
+    // Event pool. An interaction that will draw (albedo roulette, then scatter and the next
+    // tauint2 entry, kernelsMod.f90:1958-1975 + inttau2.f90:48-60) is not run by its own wave:
+    // the photon writes its direction, RNG state and layer to its slot in LDS and queues its
+    // thread index in the block's ring; any wave of the block that finds SMCRT_LEAN_POOL_MIN
+    // queued (or has nothing else to do) claims up to 64 of them and runs them on its lanes,
+    // writing the results back to the owners' slots, which the owners pick up. A photon's draws
+    // come from its own Philox stream, so which lane runs its event changes no bit.
+    // Ordering: LDS operations of one wave complete in order; slot data precede the release
+    // store of the ring entry (or of the result code), which the reader acquires.
     {
-      const bool ev = free_ && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
+      pickup();
+      // queue this wave's interactions that draw (test_kernel runs its events locally: moments)
+      const bool qev = free_ && !test_kernel && P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT | LF_EVQ)) &&
+                       LLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS;
+      const uint64_t qm = __ballot(qev);
+      if (qm) {
+        const int first = __builtin_ctzll(qm);
+        uint32_t base = 0;
+        if (lane_id == first) base = atomicAdd(&sh->eq_tail, (uint32_t)__popcll(qm));
+        base = __builtin_amdgcn_readlane(base, first);
+        if (qev) {
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+          sh->ev_dir[0][threadIdx.x] = P.dir.x; sh->ev_dir[1][threadIdx.x] = P.dir.y; sh->ev_dir[2][threadIdx.x] = P.dir.z;
+          sh->ev_cached[threadIdx.x] = P.rng.cached;
+          sh->ev_pid[0][threadIdx.x] = P.rng.pid_lo; sh->ev_pid[1][threadIdx.x] = P.rng.pid_hi;
+          sh->ev_draws[threadIdx.x] = P.rng.draws;
+          sh->ev_code[threadIdx.x] = (uint32_t)P.layer;
+          const uint32_t t = base + rank;
+          __hip_atomic_store(&sh->eq[t & 255u], ((t & 0xFFFFFFu) << 8) | threadIdx.x, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+          P.set(LF_EVQ);
+        }
+      }
+      // run queued events: SMCRT_LEAN_POOL_MIN of them, or any when every busy lane of this wave
+      // waits for one (the wave has nothing else to do; this also drains the pool at the end)
+      const uint64_t qbusy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
+      const uint64_t qwait = __ballot(P.has(LF_EVQ));
+      uint32_t claim_h = 0, claim_n = 0;
+      if (lane_id == 0) {
+        const uint32_t want = (qbusy != 0 && qwait == qbusy) ? 1u : (uint32_t)SMCRT_LEAN_POOL_MIN;
+        for (;;) {
+          const uint32_t h = __hip_atomic_load(&sh->eq_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t tl = __hip_atomic_load(&sh->eq_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const uint32_t av = tl - h;
+          if (av < want) break;
+          const uint32_t n = av < 64u ? av : 64u;
+          uint32_t exp = h;
+          if (__hip_atomic_compare_exchange_strong(&sh->eq_head, &exp, h + n, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            claim_h = h; claim_n = n;
+            break;
+          }
+        }
+      }
+      claim_n = __builtin_amdgcn_readfirstlane(claim_n);
+      claim_h = __builtin_amdgcn_readfirstlane(claim_h);
+      LDIAG(LD_POOL, claim_n ? 1 : 0);
+      LDIAG(LD_POOLN, claim_n);
+      if (claim_n) {
+        if ((uint32_t)lane_id < claim_n) {
+          const uint32_t t = claim_h + (uint32_t)lane_id;
+          uint32_t e;
+          // the producer reserved the ticket before writing its entry: wait for it (a few cycles)
+          while (((e = __hip_atomic_load(&sh->eq[t & 255u], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 8) !=
+                 (t & 0xFFFFFFu))
+            __builtin_amdgcn_s_sleep(1);
+          const uint32_t o = e & 255u;
+          Rng rg;
+          rg.pid_lo = sh->ev_pid[0][o]; rg.pid_hi = sh->ev_pid[1][o];
+          rg.draws = sh->ev_draws[o]; rg.cached = sh->ev_cached[o];
+          const int32_t layer = (int32_t)sh->ev_code[o];
+          const TopProps pr = props[layer - 1];
+          // kernelsMod.f90:1958-1975 (the local path below, for another photon)
+          const double ran = rg.next(K.key0, K.key1);
+          ++sh->lu[LL_INTER][o];
+          uint32_t res = 0;
+          if (!(ran < pr.albedo)) {
+            sh->lu[LL_STATUS][o] = 1;
+            lean_count(sh, LC_ABSORBED);
+            res = EV_ABSORB;
+          } else {
+            Lane L;
+            L.dir = v3(sh->ev_dir[0][o], sh->ev_dir[1][o], sh->ev_dir[2][o]);
+            L.rng = rg; L.fault = false; L.tflag = false;
+            scatter(K, L, pr.hgg);  // photon.f90:1045-1103
+            rg = L.rng;
+            if (L.fault) res = EV_RUNAWAY;
+            ++sh->lu[LL_NSCATT][o];
+            lean_count(sh, LC_SCATTERS);
+            lean_count(sh, LC_TAU);  // tauint2 entry, inttau2.f90:48-60
+            sh->ev_tau[o] = -det_log(rg.next(K.key0, K.key1));
+            sh->ev_dir[0][o] = L.dir.x; sh->ev_dir[1][o] = L.dir.y; sh->ev_dir[2][o] = L.dir.z;
+          }
+          sh->ev_draws[o] = rg.draws;
+          sh->ev_cached[o] = rg.cached;
+          __hip_atomic_store(&sh->ev_code[o], res | EV_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        pickup();  // (this wave's own events among them)
+      }
+    }
+#endif
+    {
+      const bool ev = free_ && !P.has(LF_EVQ) && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
       const uint64_t evm = __ballot(ev);
-      const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
+      const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH && !P.has(LF_EVQ));
       const uint32_t nev = __popcll(evm);
+#if SMCRT_LEAN_POOL
+      const bool run_ev = nev && (nev >= SMCRT_LEAN_LOCAL_EVENT_LANES || evm == busy);
+#else
       const bool run_ev = nev && (nev >= SMCRT_LEAN_EVENT_LANES || evm == busy);
+#endif
       LDIAG(LD_P7, run_ev ? 1 : 0);
       LDIAG(LD_EVWAIT, run_ev ? 0 : nev);
+      LDIAG(LD_P7LANES, run_ev ? nev : 0);
 #ifdef SMCRT_LEAN_ABL_NO_P7  // register-pressure analysis builds only (tools/regs.sh)
       if (run_ev && __ballot(P.st == 12345)) {
 #else
@@ -700,11 +889,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMCRT_WAVES
 
     LDIAG_T(7);
     // ---- P8: arrive at the hop-loop head, :61 --------------------------------------------
-    if (!(P.f & (LF_REQ | LF_WAIT | LF_PEND)) && P.st == ST_H0) {
-      if (!(P.taurun <= P.tau)) P.st = ST_T2END;
-      else if (++P.hop > (uint32_t)MAX_HOP_ITERS) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; }
-      else P.set(LF_PEND);
-    }
+    p8();
   }
 
 #ifdef SMCRT_DIAG

@@ -139,9 +139,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
     for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
   // the cooperative EVAL's primitive table (COOP instantiations), after the wave words
   double* const ctab = sh_dyn + hist_off + dep_words / 2;
+  // the culled EVAL's primitive records (cull.h CULL_LTAB), after the cooperative table
+  double* const ltab = ctab + (K.ctab ? CTAB_DOUBLES : 0);
   if constexpr (COOP) {
     if (K.ctab)
       for (int i = threadIdx.x; i < CTAB_DOUBLES; i += blockDim.x) ctab[i] = K.ctab[i];
+    for (int i = threadIdx.x; i < (int)K.n_ltab * LTAB_DOUBLES; i += blockDim.x) ltab[i] = K.ltab[i];
   }
 #pragma unroll
   for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           EvalOut S;
           double dl = 0.0;  // this lane's ds(lane + 1) (LDS-table EVAL)
           if (K.ctab) S = eval_coop_tab(ctab, K.n_top, q, false, 0, 0, &dl);
-          else if (K.cull) S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0);
+          else if (K.cull) S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, ltab);
           else S = eval_sdfs(nodes, prog, K.n_prog, q, false, 0, 0);
           w_sdf += (uint32_t)K.n_top;  // ST_M1's ds array is counted (packet%cnts)
           // far-field certificate of this EVAL (far.h): the nearest top k and the smallest
@@ -402,11 +405,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           const V3 ql = v3(readlane_f64(q.x, l), readlane_f64(q.y, l), readlane_f64(q.z, l));
           const EvalOut o = eval_culled_coop(nodes, prog, K.n_prog, K.cull, ql,
                                              __builtin_amdgcn_readlane((int)mask_le, l) != 0,
-                                             __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l));
+                                             __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l), ltab);
           if (lane_id == l) R = o;
         }
       } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)
-        R = eval_culled(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj);
+        R = eval_culled(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj, ltab);
       } else {
         R = eval_sdfs<XSRC>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }
@@ -906,6 +909,9 @@ struct smcrt_scene {
   // exact SDF culling (cull.h): grid + lists + the always-evaluated program, one allocation
   CullGrid* d_cull = nullptr;
   void* d_cull_data = nullptr;
+  // the culled EVAL's LDS records of identity-transform primitive tops (cull.h CULL_LTAB)
+  double* d_ltab = nullptr;
+  uint32_t n_ltab = 0;
   double cull_mean_list = 0.0;
   double inv2[3] = {0.0, 0.0, 0.0};
   int grid_mode = 0;  // transport_kernel<*, GM>: 1 = every 2*max a power of two, 2 = and every n too
@@ -1061,8 +1067,10 @@ static size_t lean_lds(const smcrt_scene* s) {
 // deposit words (4 wave tile histograms, or the block's bucket words), then the coop table.
 static size_t transport_lds(const smcrt_scene* s, uint32_t dep_words, bool xsrc) {
   const bool ctab = s->d_ctab && !xsrc && s->coop_lanes > 0;  // the COOP instantiation stages it
+  const bool coop = !xsrc && s->coop_lanes > 0;  // the COOP instantiation also stages the LDS records
   return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
-         (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0);
+         (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0) +
+         (coop ? (size_t)s->n_ltab * LTAB_DOUBLES * sizeof(double) : 0);
 }
 // 32-bit LDS words of a block's deposit state (deposit.h): a tile histogram per wave, or one
 // 64-bit bucket word per tile shared by the block.
@@ -1100,7 +1108,8 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   if (s->fstream) (void)hipStreamSynchronize(s->fstream);
   void* ptrs[] = {s->d_ctab, s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
-                  s->d_sorted, s->d_tile_count, s->d_tile_start, s->d_pieces, s->d_order, s->d_cull, s->d_cull_data};
+                  s->d_sorted, s->d_tile_count, s->d_tile_start, s->d_pieces, s->d_order, s->d_cull, s->d_cull_data,
+                  s->d_ltab};
   for (int i = 0; i < MAX_SLOTS; ++i) {
     void* per[] = {s->d_pool[i], s->d_chunk_fill[i], s->d_dep_ctl[i], s->d_bin_counts[i], s->d_bucket_tile[i]};
     for (void* p : per)
@@ -1325,6 +1334,44 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
+  // The culled EVAL's LDS records (cull.h CULL_LTAB, round 4): a listed top that is a primitive
+  // with the identity transform gets its parameters in LDS, so the per-lane list walk loads them
+  // from LDS instead of from the node table in device memory (M4: ~9 dependent loads per lane
+  // EVAL). Only while the COOP kernel's LDS, records included, keeps two blocks per CU
+  // (conservative: 16 B per tile for the deposit words). Off by default: on M4 it measured
+  // 5.98 / 6.09 M photons/s against 7.00 / 6.03 M without (same box, profiles/r04_s2/
+  // ab_m4_ltab.txt; the tail-bound workload's noise is larger than any gain). SMCRT_CULL_LTAB=1
+  // turns it on.
+  std::vector<double> ltab;
+  if (cull.enabled) {
+    const char* le = std::getenv("SMCRT_CULL_LTAB");
+    std::vector<int32_t> rec((size_t)n_top, -1);
+    for (int32_t i = 0; i < n_top; ++i) {
+      const smcrt_sdf_node& nd = nodes[top[i]];
+      bool id = !composite_kind(nd.kind);
+      for (int k = 0; id && k < 16; ++k) id = nd.transform[k] == ((k % 5) == 0 ? 1.0 : 0.0);
+      if (id) {
+        rec[(size_t)i] = (int32_t)(ltab.size() / LTAB_DOUBLES);
+        for (int k = 0; k < LTAB_DOUBLES; ++k) ltab.push_back(nd.param[k]);
+      }
+    }
+    const size_t fb = faces.size() * sizeof(double) + sizeof(TopProps) * (size_t)n_top;
+    const uint64_t nv = (uint64_t)grid->nx * grid->ny * grid->nz;
+    const size_t est = sizeof(LaneShared) + (fb <= 40960 ? fb : 0) + (n_dets ? 3 * 256 * sizeof(double) : 0) +
+                       16 * (size_t)((nv + TILE_VOXELS - 1) / TILE_VOXELS) +
+                       (!ctab.empty() ? CTAB_DOUBLES * sizeof(double) : 0) + ltab.size() * sizeof(double);
+    if (!(le && std::string(le) == "1") || ltab.empty() || est > 80 * 1024 - 1024 ||
+        ltab.size() / LTAB_DOUBLES >= (1u << 24)) {
+      ltab.clear();
+    } else {
+      for (size_t k = 0; k < cull.list.size(); k += 2) {
+        const uint32_t t = cull.list[k] & CULL_TOP_MASK;
+        if ((cull.list[k] & CULL_MODEL) || rec[t] < 0) continue;
+        cull.list[k] |= CULL_LTAB;
+        cull.list[k + 1] = ((uint32_t)nodes[top[t]].kind << 24) | (uint32_t)rec[t];
+      }
+    }
+  }
   if (cull.enabled) {  // [ProgOp always | u32 off | u32 list | double lb], each 16-B aligned
     std::vector<ProgOp> pa;
     for (int32_t t : cull.always)
@@ -1353,9 +1400,15 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (e == hipSuccess) e = hipMemcpy(s->d_cull, &G, sizeof G, hipMemcpyHostToDevice);
     if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("cull upload: ") + hipGetErrorString(e)));
     s->cull_mean_list = cull.mean_list;
+    if (!ltab.empty()) {
+      if ((st = dalloc(&s->d_ltab, ltab.size()))) return cleanup_fail(st);
+      e = hipMemcpy(s->d_ltab, ltab.data(), sizeof(double) * ltab.size(), hipMemcpyHostToDevice);
+      if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("cull upload: ") + hipGetErrorString(e)));
+      s->n_ltab = (uint32_t)(ltab.size() / LTAB_DOUBLES);
+    }
     if (std::getenv("SMCRT_CULL_LOG"))  // diagnostics
-      std::fprintf(stderr, "[cull] %d tops, %zu always, %d x %d x %d cells of %.4g, %.1f tops per cell\n", n_top,
-                   cull.always.size(), cull.n[0], cull.n[1], cull.n[2], cull.cell, cull.mean_list);
+      std::fprintf(stderr, "[cull] %d tops, %zu always, %d x %d x %d cells of %.4g, %.1f tops per cell, %u LDS records\n",
+                   n_top, cull.always.size(), cull.n[0], cull.n[1], cull.n[2], cull.cell, cull.mean_list, s->n_ltab);
   }
   {  // binned deposition state (deposit.h)
     const uint64_t nv = (uint64_t)grid->nx * grid->ny * grid->nz;
@@ -1751,9 +1804,10 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
       std::fprintf(stderr, "[diag-lean] wave trips %llu | walk steps/trip %.3f, busy walkers/step %.1f | pushes/trip %.2f"
                    " (sync %.3f), blocked req/trip %.2f | EVAL phases/trip %.3f lanes/EVAL %.1f | P7 runs/trip %.3f,"
                    " event lanes waiting/trip %.2f, reverts %llu | lanes waiting sync/trip %.2f, idle %.2f, busy %.2f |"
-                   " ring fill %.1f\n", h[0], h[1] / tr, (double)h[2] / std::max(1ull, h[1]), h[3] / tr, h[4] / tr,
-                   h[5] / tr, h[6] / tr, (double)h[7] / std::max(1ull, h[6]), h[8] / tr, h[13] / tr, h[9], h[10] / tr,
-                   h[11] / tr, h[14] / tr, h[12] / tr);
+                   " ring fill %.1f | pool runs/trip %.3f items/run %.1f | local P7 lanes/run %.1f\n", h[0], h[1] / tr,
+                   (double)h[2] / std::max(1ull, h[1]), h[3] / tr, h[4] / tr, h[5] / tr, h[6] / tr,
+                   (double)h[7] / std::max(1ull, h[6]), h[8] / tr, h[13] / tr, h[9], h[10] / tr, h[11] / tr, h[14] / tr,
+                   h[12] / tr, h[15] / tr, (double)h[16] / std::max(1ull, h[15]), (double)h[17] / std::max(1ull, h[8]));
     }
     unsigned long long lt = 0;
     for (int i = 0; i < 64; ++i) lt += h[i];
@@ -1849,6 +1903,8 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.coop_lanes = s->coop_lanes;
   K.cull = s->d_cull;
   K.ctab = s->d_ctab;
+  K.ltab = s->d_ltab;
+  K.n_ltab = s->n_ltab;
   const bool far = s->fm_err > 0.0 && (cfg->flags & SMCRT_FLAG_PATHLENGTH);
   K.fm_err = far ? s->fm_err : 0.0;
   K.fm_step = s->fm_step;
