@@ -150,23 +150,34 @@ __device__ __forceinline__ uint32_t box_stride(const KParams& K, Lane& L, int m,
   return 0;
 }
 
-// The far-field loop for near top k of kind KIND (SPHERE or BOX), run by the photon's lane
-// alone. ct: the cooperative EVAL's LDS table; m2 / neg_other: the certificate of the full
-// EVAL at p0; trav0: the distance from p0 to L.pos (the step P4 took after that EVAL).
+// The near top's transform and parameters: column k of the cooperative EVAL's LDS table
+// (stride 64) or a node's own arrays (stride 1).
+struct NearTop {
+  const double* t;  // t[r * stride], r < 12
+  const double* p;  // p[r * stride], r < 8
+  int stride;
+};
+__device__ __forceinline__ void near_load(const NearTop& nt, double* tl, double* pl) {
+#pragma unroll
+  for (int r = 0; r < 12; ++r) tl[r] = nt.t[r * nt.stride];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) pl[r] = nt.p[r * nt.stride];
+}
+
+// The far-field loop for near top nt of kind KIND (SPHERE or BOX), run by the photon's lane
+// alone. m2 / neg_other: the certificate of the full EVAL at p0; trav0: the distance from p0
+// to L.pos (the step P4 took after that EVAL).
 // On entry L is at ST_M1 with an EVAL pending and no segment. Returns the steps taken; acc
 // receives their deposits' sum for voxel *vox, nsdf the EVALs consumed.
 template <int GM, int KIND>
-__device__ __forceinline__ uint32_t far_march(const KParams& K, Lane& L, const double* ct, int k, double m2,
+__device__ __forceinline__ uint32_t far_march(const KParams& K, Lane& L, const NearTop& nt, double m2,
                                               bool neg_other, double trav0, double kap,
                                               const double* __restrict__ xf, const double* __restrict__ yf,
                                               const double* __restrict__ zf, double& acc, uint32_t& vox,
                                               uint32_t& nsdf) {
   const double eps = 1e-8;  // inttau2.f90:56
   double tl[12], pl[8];
-#pragma unroll
-  for (int r = 0; r < 12; ++r) tl[r] = ct[r * 64 + k];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) pl[r] = ct[(12 + r) * 64 + k];
+  near_load(nt, tl, pl);
   const V3 dir = L.dir;
   const bool zx = dir.x == 0.0, zy = dir.y == 0.0, zz = dir.z == 0.0;
   // (the reciprocal-based test needs operands where the division does no scaling)
@@ -251,16 +262,45 @@ __device__ __forceinline__ uint32_t far_march(const KParams& K, Lane& L, const d
   return n;
 }
 
-// Wave minimum of v (every lane active), by the cooperative EVAL's DPP row scans.
-__device__ __forceinline__ double wave_min_f64(double v) {
-  double b;
-  b = dpp_f64<0x111, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
-  b = dpp_f64<0x112, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
-  b = dpp_f64<0x114, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
-  b = dpp_f64<0x118, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
-  b = dpp_f64<0x142, 0xa>(__builtin_inf(), v); v = b < v ? b : v;
-  b = dpp_f64<0x143, 0xc>(__builtin_inf(), v); v = b < v ? b : v;
-  return readlane_f64(v, 63);
+
+// The boundary probe's glancing loop (inttau2.f90:226-237) with only the near top evaluated
+// per iteration. The loop goes on while new_layer == old_layer and minval(abs(dsNew)) < eps,
+// each iteration moving smallStepPos = pos + d_sdf*dir with d_sdf = d_sdf + eps (pos and dir
+// fixed). Under the certificate of the full EVAL at p0 = the current smallStepPos (header:
+// every other computed |ds_j| stays above |ds_k| while |ds_k(p)| + travel < m2 - 2 fm_err),
+// minval(abs(dsNew)) = |ds_k| exactly, and while ds_k < 0 maxloc(dsNew, mask dsNew < 0) is k
+// (every other negative value is below -|ds_k|). So an iteration with ds_k < 0, top k ==
+// old_layer and |ds_k| < eps is one the full EVAL would continue too, with the same values.
+// The travel from p0 needs no sum: every smallStepPos is formed afresh from pos, so it is
+// (d_sdf - d0)|dir| plus the rounding of the two positions (2 fm_step).
+// On entry L is at ST_G0 with the EVAL at L.ssp pending (that EVAL produced the certificate),
+// top_k is the near top's 1-based index. The loop stops BEFORE an iteration it cannot decide,
+// and before the glancing guard's last iteration, with L at ST_G0, d and ssp of that iteration
+// and its EVAL pending, as the main loop's P3 would have left it. Returns the iterations taken
+// (each one a full EVAL of the reference, counted in packet%cnts).
+template <int KIND>
+__device__ __forceinline__ uint32_t far_glance(const KParams& K, Lane& L, const NearTop& nt, int32_t top_k, double m2) {
+  const double eps = 1e-8;  // inttau2.f90:56
+  if (top_k != L.old_layer) return 0;
+  double tl[12], pl[8];
+  near_load(nt, tl, pl);
+  const V3 dir = L.dir;
+  const double dn = sqrt(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z) * (1.0 + 0x1.0p-48);
+  const double lim = m2 - 2.0 * K.fm_err;
+  const double d0 = L.d;
+  uint32_t n = 0;
+  for (;;) {
+    const double v = sdf_prim_s<1>(KIND, tl, pl, L.ssp, true);
+    const double trav = (L.d - d0) * (1.0 + 0x1.0p-48) * dn + 2.0 * K.fm_step;
+    if (!(fabs(v) + trav < lim)) break;                  // the certificate no longer covers ssp (or NaN)
+    if (!(v < 0.0) || !(-v < eps)) break;                // the loop may end here: the full EVAL decides
+    if (L.loopc + 1u > (uint32_t)MAX_GLANCE_ITERS) break; // the guard's iteration (a fault): main loop
+    ++L.loopc;                                           // P3, ST_G0 (:232-237)
+    L.d = L.d + eps;
+    L.ssp = L.pos + smul(L.d, L.dir);
+    ++n;
+  }
+  return n;
 }
 
 }  // namespace smcrt

@@ -231,6 +231,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
     }
 
 #ifdef SMCRT_DIAG_STATES
+#ifdef SMCRT_DIAG_TAIL  // only the trips of waves with at most 4 photons left (the launch's tail)
+    if (__popcll(__ballot(L.st != ST_IDLE)) <= 4)
+#endif
     {
       const uint32_t cls = (L.seg ? 32u : 0u) + (L.st & 31u);
       for (uint32_t c = 0; c < 64; ++c) {  // wave-uniform loop: count lanes per class
@@ -259,23 +262,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
       const bool ev_wait = (L.st == ST_INTERACT || L.st == ST_T2 || L.st == ST_EMIT || L.st == ST_DONE);
       const uint64_t act = __ballot(L.st != ST_IDLE && !ev_wait);
       const uint64_t cand = __ballot(L.st == ST_M1 && L.pend && !L.seg);
-      if (cand && __popcll(act) <= SOLO_LANES) {  // (a few photons: one after the other)
-        const int ow = __builtin_ctzll(cand);
-        bool run = true;
-        while (run) {
-          const V3 q = v3(readlane_f64(L.pos.x, ow), readlane_f64(L.pos.y, ow), readlane_f64(L.pos.z, ow));
-          EvalOut S;
-          double dl = 0.0;  // this lane's ds(lane + 1) (LDS-table EVAL)
-          if (K.ctab) S = eval_coop_tab(ctab, K.n_top, q, false, 0, 0, &dl);
-          else if (K.cull) S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, ltab);
-          else S = eval_sdfs(nodes, prog, K.n_prog, q, false, 0, 0);
-          w_sdf += (uint32_t)K.n_top;  // ST_M1's ds array is counted (packet%cnts)
-          // far-field certificate of this EVAL (far.h): the nearest top k and the smallest
-          // |ds| of the others, for a march that has run a while
-          int fk = -1;
-          double fm2 = 0.0;
-          bool fneg = false;
-          if (K.fm_err > 0.0 && K.ctab && __builtin_amdgcn_readlane((int)L.loopc, ow) >= SMCRT_FAR_MIN_LOOP) {
+      // a glancing loop (ST_G0, inttau2.f90:226-237) that has run a while: tried at its 8th
+      // iteration and every 64 after (a try whose certificate fails costs one extra EVAL)
+      const uint64_t gcand =
+          K.fm_err > 0.0 ? __ballot(L.st == ST_G0 && L.pend && L.loopc >= SMCRT_FAR_MIN_LOOP &&
+                                    ((L.loopc - SMCRT_FAR_MIN_LOOP) & 63u) == 0)
+                         : 0ull;
+      // the full EVAL at q (every lane), and with `want` its far-field certificate (far.h): the
+      // near top's kind (SPHERE or BOX; -1: none), where its data are, its 1-based index, a
+      // lower bound on every other top's |ds| and whether another top is negative
+      int fkind = -1;
+      NearTop fnt{nullptr, nullptr, 1};
+      int32_t ftop = 0;
+      double fm2 = 0.0;
+      bool fneg = false;
+      auto certified_eval = [&](V3 q, bool want) -> EvalOut {
+        EvalOut S;
+        double dl = 0.0;  // this lane's ds(lane + 1) (LDS-table EVAL)
+        fkind = -1;
+        if (K.ctab) {
+          S = eval_coop_tab(ctab, K.n_top, q, false, 0, 0, &dl);
+          if (want) {
             const bool mine = lane_id < K.n_top;
             const double ad = mine ? fabs(dl) : __builtin_inf();
             const uint64_t km = __ballot(mine && ad == S.minabs);
@@ -286,10 +293,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
               if (kind == SMCRT_SDF_SPHERE || kind == SMCRT_SDF_BOX) {
                 fm2 = wave_min_f64(lane_id == k ? __builtin_inf() : ad);
                 fneg = __ballot(mine && lane_id != k && dl < 0.0) != 0;
-                fk = k;
+                fnt = NearTop{ctab + k, ctab + 12 * 64 + k, 64};
+                ftop = k + 1;
+                fkind = kind;
               }
             }
           }
+        } else if (K.cull) {
+          FarCert fc;
+          S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, ltab, want ? &fc : nullptr);
+          if (want && fc.node >= 0) {
+            const int32_t node = __builtin_amdgcn_readfirstlane(fc.node);
+            const int kind = nodes[node].kind;
+            if (kind == SMCRT_SDF_SPHERE || kind == SMCRT_SDF_BOX) {
+              fm2 = fc.m2;
+              fneg = fc.neg_other;
+              fnt = NearTop{nodes[node].transform, nodes[node].param, 1};
+              ftop = fc.top;
+              fkind = kind;
+            }
+          }
+        } else {
+          S = eval_sdfs(nodes, prog, K.n_prog, q, false, 0, 0);
+        }
+        return S;
+      };
+      if (cand && __popcll(act) <= SOLO_LANES) {  // (a few photons: one after the other)
+        const int ow = __builtin_ctzll(cand);
+        bool run = true;
+        while (run) {
+          const V3 q = v3(readlane_f64(L.pos.x, ow), readlane_f64(L.pos.y, ow), readlane_f64(L.pos.z, ow));
+          // the far-field certificate of this EVAL, for a march that has run a while
+          const bool want = K.fm_err > 0.0 && __builtin_amdgcn_readlane((int)L.loopc, ow) >= SMCRT_FAR_MIN_LOOP;
+          const EvalOut S = certified_eval(q, want);
+          w_sdf += (uint32_t)K.n_top;  // ST_M1's ds array is counted (packet%cnts)
           if (lane_id == ow) {
             L.pend = false;  // P3, ST_M1: :177-191
             L.minabs = S.minabs;
@@ -335,17 +372,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
             }
           }
           run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
-          if (run && fk >= 0) {  // the far-field march from the certificate (far.h)
+          if (run && fkind >= 0) {  // the far-field march from the certificate (far.h)
             uint32_t n = 0, nsdf = 0;
             if (lane_id == ow) {
               double acc = 0.0;
               uint32_t vox = 0;
               const double kap = props[L.layer - 1].kappa;
-              const int kind = (int)ctab[20 * 64 + fk] & 15;
-              n = kind == SMCRT_SDF_BOX
-                      ? far_march<GM, SMCRT_SDF_BOX>(K, L, ctab, fk, fm2, fneg, S.minabs, kap, xf, yf, zf, acc, vox, nsdf)
-                      : far_march<GM, SMCRT_SDF_SPHERE>(K, L, ctab, fk, fm2, fneg, S.minabs, kap, xf, yf, zf, acc, vox,
-                                                        nsdf);
+              n = fkind == SMCRT_SDF_BOX
+                      ? far_march<GM, SMCRT_SDF_BOX>(K, L, fnt, fm2, fneg, S.minabs, kap, xf, yf, zf, acc, vox, nsdf)
+                      : far_march<GM, SMCRT_SDF_SPHERE>(K, L, fnt, fm2, fneg, S.minabs, kap, xf, yf, zf, acc, vox, nsdf);
               if (n) {
                 LCTR(LC_UPD) += n;
                 double* const jm = C->jmean;
@@ -359,6 +394,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
             w_dep += n;
             run = __builtin_amdgcn_readlane((int)(L.st == ST_M1 && L.pend && !L.seg), ow) != 0;
           }
+        }
+      } else if (gcand && __popcll(act) <= SOLO_LANES) {
+        // the glancing loop with the near top only (far.h far_glance); this EVAL is not
+        // consumed here: the loop's first iteration re-evaluates the near top at the same point
+        const int ow = __builtin_ctzll(gcand);
+        const V3 q = v3(readlane_f64(L.ssp.x, ow), readlane_f64(L.ssp.y, ow), readlane_f64(L.ssp.z, ow));
+        certified_eval(q, true);
+        if (fkind >= 0) {
+          uint32_t n = 0;
+          if (lane_id == ow)
+            n = fkind == SMCRT_SDF_BOX ? far_glance<SMCRT_SDF_BOX>(K, L, fnt, ftop, fm2)
+                                       : far_glance<SMCRT_SDF_SPHERE>(K, L, fnt, ftop, fm2);
+          n = (uint32_t)__builtin_amdgcn_readlane((int)n, ow);
+          w_sdf += n * (uint32_t)K.n_top;  // each iteration consumed a (counted) G0 EVAL
+          if (n && lane_id == ow && C->far_steps) atomicAdd(C->far_steps, (unsigned long long)n);
         }
       }
     }
@@ -1267,29 +1317,6 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
         for (int r = 0; r < 8; ++r) ctab[(12 + r) * 64 + i] = nd.param[r];
         ctab[20 * 64 + i] = (double)nd.kind + (translate_only(top[i]) ? 16.0 : 0.0);
       }
-      // The far-field march needs every top 1-Lipschitz (exact-distance primitives under
-      // translation-only transforms) and a bound on the computed values' error: a few ulps
-      // of the largest operand, taken here as 2^-44 of the scene's extent (far.h).
-      // SMCRT_FAR_MARCH=0 turns it off.
-      const char* fe = std::getenv("SMCRT_FAR_MARCH");
-      bool fm = !(fe && std::string(fe) == "0");
-      double ext = grid->xmax + grid->ymax + grid->zmax + 1.0;
-      double scale = 0.0;
-      for (int32_t i = 0; fm && i < n_top; ++i) {
-        const smcrt_sdf_node& nd = nodes[top[i]];
-        const int32_t kd = nd.kind;
-        fm = translate_only(top[i]) && (kd == SMCRT_SDF_SPHERE || kd == SMCRT_SDF_BOX || kd == SMCRT_SDF_TORUS ||
-                                        kd == SMCRT_SDF_SEGMENT || kd == SMCRT_SDF_CAPSULE);
-        double m = std::fabs(nd.transform[3]) + std::fabs(nd.transform[7]) + std::fabs(nd.transform[11]);
-        for (int r = 0; r < 8; ++r) m += std::fabs(nd.param[r]);
-        fm = fm && std::isfinite(m);
-        scale = std::max(scale, m);
-      }
-      fm = fm && std::isfinite(ext);
-      if (fm) {
-        s->fm_err = std::ldexp(scale + ext, -44);
-        s->fm_step = std::ldexp(scale + ext, -48);
-      }
     }
   }
   // exact culling of the SDF array for many-top scenes (cull.h); SMCRT_CULL=0 turns it off
@@ -1298,6 +1325,32 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     const char* ce = std::getenv("SMCRT_CULL");
     const double gh[3] = {grid->xmax, grid->ymax, grid->zmax};
     if (s->coop_lanes > 0 && !(ce && std::string(ce) == "0")) cull = build_cull(nodes, n_nodes, top, n_top, gh);
+  }
+  // The far-field march and glance (far.h) need every top 1-Lipschitz (exact-distance
+  // primitives under translation-only transforms), a full EVAL that yields a certificate (the
+  // cooperative LDS table or the culled EVAL) and a bound on the computed values' error: a few
+  // ulps of the largest operand, taken here as 2^-44 of the scene's extent. SMCRT_FAR_MARCH=0
+  // turns them off.
+  if (!ctab.empty() || cull.enabled) {
+    const char* fe = std::getenv("SMCRT_FAR_MARCH");
+    bool fm = !(fe && std::string(fe) == "0");
+    double ext = grid->xmax + grid->ymax + grid->zmax + 1.0;
+    double scale = 0.0;
+    for (int32_t i = 0; fm && i < n_top; ++i) {
+      const smcrt_sdf_node& nd = nodes[top[i]];
+      const int32_t kd = nd.kind;
+      fm = translate_only(top[i]) && (kd == SMCRT_SDF_SPHERE || kd == SMCRT_SDF_BOX || kd == SMCRT_SDF_TORUS ||
+                                      kd == SMCRT_SDF_SEGMENT || kd == SMCRT_SDF_CAPSULE);
+      double m = std::fabs(nd.transform[3]) + std::fabs(nd.transform[7]) + std::fabs(nd.transform[11]);
+      for (int r = 0; r < 8; ++r) m += std::fabs(nd.param[r]);
+      fm = fm && std::isfinite(m);
+      scale = std::max(scale, m);
+    }
+    fm = fm && std::isfinite(ext);
+    if (fm) {
+      s->fm_err = std::ldexp(scale + ext, -44);
+      s->fm_step = std::ldexp(scale + ext, -48);
+    }
   }
   // n*p/(2*max) may be computed as n*p*inv exactly when 2*max is a power of two
   const double maxes[3] = {grid->xmax, grid->ymax, grid->zmax};

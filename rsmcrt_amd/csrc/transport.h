@@ -1038,6 +1038,18 @@ __device__ __forceinline__ void coop_step(CoopAcc& a) {
   b.loc = dpp_i32<CTRL, ROWS>(0, a.loc);
   coop_fold(a, b);
 }
+// Wave minimum of v (every lane active), by the cooperative EVAL's DPP row scans.
+__device__ __forceinline__ double wave_min_f64(double v) {
+  double b;
+  b = dpp_f64<0x111, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
+  b = dpp_f64<0x112, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
+  b = dpp_f64<0x114, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
+  b = dpp_f64<0x118, 0xf>(__builtin_inf(), v); v = b < v ? b : v;
+  b = dpp_f64<0x142, 0xa>(__builtin_inf(), v); v = b < v ? b : v;
+  b = dpp_f64<0x143, 0xc>(__builtin_inf(), v); v = b < v ? b : v;
+  return readlane_f64(v, 63);
+}
+
 // The whole wave evaluates the SDF array at the wave-uniform point q (all lanes active).
 // (lane_d, if given, receives the lane's own ds(lane + 1), 0 past n_top)
 __device__ __forceinline__ EvalOut eval_coop_tab(const double* ct, int32_t n_top, V3 q, bool mask_le, int32_t capi,
@@ -1072,6 +1084,15 @@ __device__ __forceinline__ EvalOut eval_coop_tab(const double* ct, int32_t n_top
   if (lane_d) *lane_d = d;
   return r;
 }
+
+// The far-field certificate of a full EVAL at p0 (far.h): the nearest top is the primitive
+// `node`, every other top has a computed |ds| >= m2 at p0, and neg_other says whether one of
+// them is negative there. node < 0: no certificate.
+struct FarCert {
+  int32_t node, top;  // top: its 1-based index
+  double m2;
+  bool neg_other;
+};
 
 // Culled EVAL (cull.h): the always-evaluated tops wave-uniformly, then each lane walks its
 // cell's list of tops with per-lane loads; a lane whose bound test fails (or that needs the
@@ -1201,8 +1222,14 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
 __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __restrict__ nodes,
                                                     const ProgOp* __restrict__ prog, int32_t n_prog,
                                                     const CullGrid* __restrict__ G, V3 q, bool mask_le,
-                                                    int32_t capi, int32_t capj, const double* ltab) {
+                                                    int32_t capi, int32_t capj, const double* ltab,
+                                                    FarCert* fc = nullptr) {
   const int lane = (int)(threadIdx.x & 63);
+  // (certificate only) the always-evaluated tops' smallest |ds|, whether one is negative, and
+  // whether any value is NaN or infinite (no certificate then)
+  double a_min = __builtin_inf();
+  bool a_neg = false, a_bad = false;
+  if (fc) fc->node = -1;
   EvalOut r;
   r.minabs = __builtin_inf();
   r.minv = __builtin_inf();
@@ -1226,6 +1253,11 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
         if (d < r.minv) r.minv = d;
         const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
         if (neg && (r.maxloc == 0 || d > best)) { best = d; r.maxloc = op.top; }
+        if (fc) {
+          if (a < a_min) a_min = a;
+          a_neg = a_neg || d < 0.0;
+          a_bad = a_bad || !(a <= 0x1.fffffffffffffp+1023);
+        }
       }
     }
   }
@@ -1242,6 +1274,12 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
     const uint2* __restrict__ ent = (const uint2*)G->list;
     CoopAcc a;
     a.minabs = r.minabs; a.minv = r.minv; a.best = best; a.loc = r.maxloc;  // (every lane: the uniform part)
+    // (certificate only) this lane's entries: smallest and second smallest |ds|, the node of
+    // the smallest (-1: a model or an LDS record), negatives, and NaN or infinite values
+    double l1 = __builtin_inf(), l2 = __builtin_inf();
+    int32_t n1 = -1, t1 = 0;
+    uint32_t nneg = 0;
+    bool neg1 = false, lbad = false;
     for (uint32_t k0 = b; k0 < e; k0 += 64) {
       const uint32_t k = k0 + (uint32_t)lane;
       if (k < e) {
@@ -1270,6 +1308,19 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
         o.best = neg ? d : -__builtin_inf();
         o.loc = neg ? i + 1 : 0;
         coop_fold(a, o);
+        if (fc) {
+          const double ad = o.minabs;
+          if (ad < l1) {
+            l2 = l1; l1 = ad;
+            n1 = (en.x & (CULL_MODEL | CULL_LTAB)) ? -1 : (int32_t)en.y;
+            t1 = i + 1;
+            neg1 = d < 0.0;
+          } else if (ad < l2) {
+            l2 = ad;
+          }
+          nneg += d < 0.0 ? 1u : 0u;
+          lbad = lbad || !(ad <= 0x1.fffffffffffffp+1023);
+        }
       }
     }
     coop_step<0x111, 0xf>(a);
@@ -1288,7 +1339,26 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
                     dmin(q.z - cz, cz + G->cell - q.z));
     h = dmax(h, 0.0);
     const double T = dmax(h, G->lb[c]) * (1.0 - 1e-12);
-    if (!(r.minabs < T)) full = true;
+    if (!(r.minabs < T)) {
+      full = true;
+    } else if (fc) {
+      // The far-field certificate (far.h): one listed primitive attains min|ds| (no always-
+      // evaluated top does); every other listed or always-evaluated top has |ds| >= m2, and
+      // every unlisted one ds >= T > 0, so m2 also takes T.
+      const uint64_t km = __ballot(l1 == r.minabs);
+      const bool bad = a_bad || __ballot(lbad) != 0;
+      if (__popcll(km) == 1 && !bad && !(a_min <= r.minabs)) {
+        const int kl = __builtin_ctzll(km);
+        const int32_t node = __builtin_amdgcn_readlane(n1, kl);
+        double m2 = wave_min_f64(lane == kl ? l2 : l1);
+        m2 = dmin(dmin(m2, a_min), T);
+        const bool neg = a_neg || __ballot(nneg > ((lane == kl && neg1) ? 1u : 0u)) != 0;
+        fc->node = node;
+        fc->top = __builtin_amdgcn_readlane(t1, kl);
+        fc->m2 = m2;
+        fc->neg_other = neg;
+      }
+    }
   }
   if (full) r = eval_sdfs(nodes, prog, n_prog, q, mask_le, capi, capj);
   return r;

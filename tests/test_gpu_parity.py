@@ -7,6 +7,8 @@ bins) must be bit-exact; each photon's final position/direction must be bit-iden
 built from many atomic adds (jmean, survival-bias absorb, moments) differ only by summation
 order: |gpu - cpu| <= 1e-12 * |cpu| + 1e-300 per voxel.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -99,7 +101,7 @@ def test_tail_machinery_wall_photons(variant, monkeypatch):
     assert cpu.counter("sdf_evals") > 300 * 41 * 500  # (long marches: the tail machinery ran)
 
 
-@pytest.mark.parametrize("case", ["gm2", "gm1", "gm0", "survival", "off"])
+@pytest.mark.parametrize("case", ["gm2", "gm1", "gm0", "survival", "culled", "off"])
 def test_far_field_march(case, monkeypatch):
     """The far-field march (far.h): a lone photon's long march re-evaluates only its nearest
     SDF while a certificate from the last full EVAL bounds every other one. Photons within
@@ -107,9 +109,12 @@ def test_far_field_march(case, monkeypatch):
     loop. Counters (SDF evaluations, deposits, grid updates), photon records and jmean must
     equal the oracle's exactly as without it ("off": SMCRT_FAR_MARCH=0), on every grid kind
     (GM 2: power-of-two cells, 1: power-of-two extent, 0: neither) and with the unbinned
-    (survival-bias) deposit path."""
+    (survival-bias) deposit path. "culled": the certificate comes from the culled EVAL
+    (SMCRT_COOP_TAB=0) instead of the LDS table."""
     if case == "off":
         monkeypatch.setenv("SMCRT_FAR_MARCH", "0")
+    if case == "culled":
+        monkeypatch.setenv("SMCRT_COOP_TAB", "0")
     flags = abi.FLAG_PATHLENGTH | (abi.FLAG_SURVIVAL_BIAS if case == "survival" else 0)
     g = {"gm1": scene.grid(50, 50, 50, 1, 1, 1), "gm0": scene.grid(40, 36, 44, 1.25, 1.25, 1.25)}.get(
         case, scene.grid(32, 32, 32, 1, 1, 1))
@@ -128,6 +133,45 @@ def test_far_field_march(case, monkeypatch):
         assert kt["far_steps"] == 0, kt
     else:
         assert kt["far_steps"] > steps // 2, (kt, steps)  # most steps ran in the far-field loop
+
+
+@pytest.mark.parametrize("geom", ["parallel", "oblique"])
+@pytest.mark.parametrize("variant", ["table", "culled", "off"])
+def test_far_glance_wall_photons(variant, geom, monkeypatch):
+    """The boundary probe's glancing loop (inttau2.f90:226-237) with the near top only
+    (far.h far_glance). Photons launched within 5e-9 (< eps) of a side wall: moving parallel
+    to it ("parallel") the loop never ends in the reference and stops here at the glancing
+    guard (MAX_GLANCE_ITERS) with a fault; moving away from it at 1e-3 rad ("oblique") it ends
+    after ~1000 iterations. The certificate comes from the LDS table (sphere_scene, 41 tops)
+    or the culled EVAL (an 81-top capsule net); "off": SMCRT_FAR_MARCH=0. Counters (faults,
+    SDF evaluations), photon records and jmean must equal the oracle's bit for bit."""
+    if variant == "off":
+        monkeypatch.setenv("SMCRT_FAR_MARCH", "0")
+    if variant == "table" or variant == "off":
+        sc = builders.setup_sphere_scene(builders.random_sphere_list(40))
+        g = scene.grid(32, 32, 32, 1, 1, 1)
+        p1, p3 = (-1.0, -1.0, 0.9999999), (0.0, 2.0, 0.0)
+    else:
+        sc = builders.synthetic_vessels(80)
+        g = scene.grid(64, 64, 64, 0.16, 0.09, 0.13)
+        p1, p3 = (-0.16, -0.09, 0.1299), (0.0, 0.18, 0.0)
+    d = (0.0, 0.0, -1.0) if geom == "parallel" else (math.sin(1e-3), 0.0, -math.cos(1e-3))
+    src = scene.uniform_source(p1, (5e-9, 0.0, 0.0), p3, d)
+    n = 4
+    with Engine(sc, g) as eng:
+        eng.kernel_times()
+        gpu = eng.run(src, n, seed=SEED, records=True)
+        kt = eng.kernel_times()
+    cpu = O.run(sc, g, src, n, seed=SEED, records=True)
+    compare(gpu, cpu)
+    if geom == "parallel":
+        assert cpu.counter("faults") == n  # (every photon reached the glancing guard)
+    if variant == "off":
+        assert kt["far_steps"] == 0, kt
+    elif geom == "parallel":
+        assert kt["far_steps"] > n * 50000, kt  # most iterations ran in far_glance
+    else:
+        assert kt["far_steps"] > 0, kt
 
 
 def test_detectors_validation1():
