@@ -1,7 +1,7 @@
 """Build the HIP engine library in-tree: rsmcrt_amd/libsmcrt.so (gfx950).
 
-Plain hipcc, one translation unit, no torch extension machinery: the library is a C-ABI
-shared object (include/smcrt.h) that Fortran/C/Python can bind.
+Plain hipcc, no torch extension machinery: every source compiles to an object in parallel and
+one link makes the C-ABI shared object (include/smcrt.h) that Fortran/C/Python can bind.
 """
 from __future__ import annotations
 
@@ -10,6 +10,8 @@ import shutil
 import glob
 import subprocess
 import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
@@ -19,7 +21,7 @@ DEPS = SOURCES + sorted(glob.glob(os.path.join(PKG, "csrc", "*.h"))) + [os.path.
 ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no fused multiply-add, so fp64 trajectories are bit-identical to the
 # CPU restatement (oracle/), which is compiled the same way.
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          f"--offload-arch={ARCH}", "-Wall"]
 
 
@@ -40,10 +42,22 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
-    cmd = [hipcc(), *FLAGS, "-o", LIB + ".tmp", *SOURCES, "-lz", "-ldl"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    with tempfile.TemporaryDirectory(prefix="smcrt_build_") as tmp:
+        objs = [os.path.join(tmp, os.path.basename(src) + ".o") for src in SOURCES]
+
+        def compile_one(i: int) -> None:
+            cmd = [hipcc(), *FLAGS, "-c", "-o", objs[i], SOURCES[i]]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            subprocess.run(cmd, check=True)
+
+        jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1)))
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(compile_one, range(len(SOURCES))))
+        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp", *objs, "-lz", "-ldl"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
     return LIB
 

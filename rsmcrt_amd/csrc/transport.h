@@ -1225,10 +1225,14 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
                                                     int32_t capi, int32_t capj, const double* ltab,
                                                     FarCert* fc = nullptr) {
   const int lane = (int)(threadIdx.x & 63);
-  // (certificate only) the always-evaluated tops' smallest |ds|, whether one is negative, and
-  // whether any value is NaN or infinite (no certificate then)
-  double a_min = __builtin_inf();
-  bool a_neg = false, a_bad = false;
+  // (certificate only) the always-evaluated tops' smallest and second smallest |ds|, the node
+  // and 1-based index of the smallest when it is a lone primitive (-1: a model), how many are
+  // negative and whether the smallest is, and whether any value is NaN or infinite (no
+  // certificate then)
+  double a_min = __builtin_inf(), a_min2 = __builtin_inf();
+  int32_t a_node = -1, a_top = 0;
+  uint32_t a_nneg = 0;
+  bool a_neg1 = false, a_bad = false;
   if (fc) fc->node = -1;
   EvalOut r;
   r.minabs = __builtin_inf();
@@ -1254,8 +1258,15 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
         const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
         if (neg && (r.maxloc == 0 || d > best)) { best = d; r.maxloc = op.top; }
         if (fc) {
-          if (a < a_min) a_min = a;
-          a_neg = a_neg || d < 0.0;
+          if (a < a_min) {
+            a_min2 = a_min; a_min = a;
+            a_node = op.action == PROG_TOP ? node : -1;
+            a_top = op.top;
+            a_neg1 = d < 0.0;
+          } else if (a < a_min2) {
+            a_min2 = a;
+          }
+          a_nneg += d < 0.0 ? 1u : 0u;
           a_bad = a_bad || !(a <= 0x1.fffffffffffffp+1023);
         }
       }
@@ -1342,9 +1353,10 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
     if (!(r.minabs < T)) {
       full = true;
     } else if (fc) {
-      // The far-field certificate (far.h): one listed primitive attains min|ds| (no always-
-      // evaluated top does); every other listed or always-evaluated top has |ds| >= m2, and
-      // every unlisted one ds >= T > 0, so m2 also takes T.
+      // The far-field certificate (far.h): one top attains min|ds|, either a listed primitive
+      // (no always-evaluated top does) or an always-evaluated lone primitive (no listed top
+      // does, e.g. a bounding box's wall); every other listed or always-evaluated top has
+      // |ds| >= m2, and every unlisted one ds >= T > 0, so m2 also takes T.
       const uint64_t km = __ballot(l1 == r.minabs);
       const bool bad = a_bad || __ballot(lbad) != 0;
       if (__popcll(km) == 1 && !bad && !(a_min <= r.minabs)) {
@@ -1352,11 +1364,17 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
         const int32_t node = __builtin_amdgcn_readlane(n1, kl);
         double m2 = wave_min_f64(lane == kl ? l2 : l1);
         m2 = dmin(dmin(m2, a_min), T);
-        const bool neg = a_neg || __ballot(nneg > ((lane == kl && neg1) ? 1u : 0u)) != 0;
+        const bool neg = a_nneg > 0 || __ballot(nneg > ((lane == kl && neg1) ? 1u : 0u)) != 0;
         fc->node = node;
         fc->top = __builtin_amdgcn_readlane(t1, kl);
         fc->m2 = m2;
         fc->neg_other = neg;
+      } else if (km == 0 && !bad && a_min == r.minabs && a_min2 > a_min && a_node >= 0) {
+        const double m2 = dmin(dmin(wave_min_f64(l1), a_min2), T);
+        fc->node = __builtin_amdgcn_readfirstlane(a_node);
+        fc->top = __builtin_amdgcn_readfirstlane(a_top);
+        fc->m2 = m2;
+        fc->neg_other = a_nneg > (a_neg1 ? 1u : 0u) || __ballot(nneg > 0) != 0;
       }
     }
   }
