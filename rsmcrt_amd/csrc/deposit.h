@@ -488,7 +488,9 @@ __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __r
     const uint32_t b = pos < BUCKET_RECORDS ? bw_cur(w) : bw_next(w);
     const bool slot = todo && pos < 2 * BUCKET_RECORDS;
     const bool ok = slot && b < K.n_buckets;
+#ifndef SMCRT_ABL_NO_RECSTORE  // timing ablation only: slots are claimed, records not written
     if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
+#endif
     const bool claim = todo && pos == BUCKET_RECORDS;
     const bool spill = slot && !ok;
     const bool wait = todo && !slot;  // both buckets full: a claim is pending in another wave
@@ -629,6 +631,83 @@ __device__ __forceinline__ unsigned long long red_load(const unsigned long long*
   return *p;
 #endif
 }
+#ifndef SMCRT_RED_WAVE
+#define SMCRT_RED_WAVE 1
+#endif
+#ifndef SMCRT_RED_GROUP
+#define SMCRT_RED_GROUP 4
+#endif
+#ifndef SMCRT_RED_THREADS
+#define SMCRT_RED_THREADS 1024
+#endif
+constexpr uint32_t RED_THREADS = SMCRT_RED_THREADS;  // bk_reduce's block size
+#if SMCRT_RED_WAVE
+// One wave per bucket (round 4): wave w of the block takes buckets w, w + 16, w + 32, ... of the
+// piece, RED_GROUP at a time; a bucket's id and fill are scalar loads and its 256 records four
+// coalesced 512-B loads per wave. The next group's records are loaded before this group's LDS
+// adds are issued (software pipeline), so each wave keeps 2 * RED_GROUP * 4 records per lane
+// in flight and its memory latency overlaps its own LDS atomics; no ids/fills staging in LDS
+// and no block barrier inside a piece. Sums are the same fp64 LDS adds in a different order.
+constexpr int RED_GROUP = SMCRT_RED_GROUP;
+__global__ __launch_bounds__(RED_THREADS) void bk_reduce(const unsigned long long* __restrict__ pool,
+                                                  const uint32_t* __restrict__ order,
+                                                  const uint32_t* __restrict__ bucket_fill,
+                                                  const Piece* __restrict__ pieces,
+                                                  const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
+                                                  double* __restrict__ jmean, unsigned long long* __restrict__ busy) {
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  __shared__ double acc[TILE_VOXELS];
+  const uint32_t n_pieces = dep_ctl[2];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  constexpr uint32_t NW = RED_THREADS / 64;  // waves per block
+  constexpr int NR = RED_GROUP * 4;        // records per lane per group
+  for (uint32_t pi = blockIdx.x; pi < n_pieces; pi += gridDim.x) {
+    const Piece p = pieces[pi];
+    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) acc[i] = 0.0;
+    __syncthreads();
+    // group g of this wave: buckets w + NW * (RED_GROUP * g + u), u < RED_GROUP
+    auto fetch = [&](uint32_t g, unsigned long long* x) {
+#pragma unroll
+      for (int u = 0; u < RED_GROUP; ++u) {
+        const uint32_t b = w + NW * (RED_GROUP * g + (uint32_t)u);
+        uint32_t f = 0, id = 0;
+        if (b < p.count) {
+          id = uniform(order[p.start + b]);
+          f = uniform(bucket_fill[id]);
+        }
+        const unsigned long long* __restrict__ base = pool + ((uint64_t)id << BUCKET_SHIFT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t slot = lane + 64u * (uint32_t)r;
+          x[4 * u + r] = slot < f ? red_load(base + slot) : ~0ull;
+        }
+      }
+    };
+    const uint32_t ng = (p.count + NW * RED_GROUP - 1) / (NW * RED_GROUP);  // groups of the piece (wave 0's count)
+    unsigned long long cur[NR];
+    fetch(0, cur);
+    for (uint32_t g = 0; g < ng; ++g) {
+      unsigned long long nxt[NR];
+      if (g + 1 < ng) fetch(g + 1, nxt);
+#pragma unroll
+      for (int k = 0; k < NR; ++k)
+        if (cur[k] != ~0ull) atomicAdd(&acc[(uint32_t)(cur[k] >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)cur[k]));
+      if (g + 1 < ng) {
+#pragma unroll
+        for (int k = 0; k < NR; ++k) cur[k] = nxt[k];
+      }
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)p.tile << TILE_SHIFT;
+    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) {
+      const double a = acc[i];
+      if (a != 0.0 && base + i < n_voxels) atomic_add_nr(jmean + base + i, a);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && busy) atomicAdd(busy, __builtin_amdgcn_s_memrealtime() - t_start);
+}
+#else
 __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __restrict__ pool,
                                                   const uint32_t* __restrict__ order,
                                                   const uint32_t* __restrict__ bucket_fill,
@@ -693,6 +772,7 @@ __global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __re
   }
   if (threadIdx.x == 0 && busy) atomicAdd(busy, __builtin_amdgcn_s_memrealtime() - t_start);
 }
+#endif
 
 // ---- bin_reduce: one tile piece per block, fp64 LDS sums added into jmean ----------------
 // (blockDim.x must be 1024)

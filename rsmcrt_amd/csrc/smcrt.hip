@@ -1706,7 +1706,7 @@ static bool ensure_pool(smcrt_scene* s, uint64_t records) {
   // SMCRT_SLOTS=2 / =4 overrides.
   {
     const char* ns = std::getenv("SMCRT_SLOTS");
-    const int want = ns ? (std::atoi(ns) < MAX_SLOTS ? 2 : MAX_SLOTS) : (s->lean_ok || s->fm_err > 0.0 ? 2 : MAX_SLOTS);
+    const int want = ns ? std::max(2, std::min(MAX_SLOTS, std::atoi(ns))) : (s->lean_ok || s->fm_err > 0.0 ? 2 : MAX_SLOTS);
     uint64_t deep = DEEP_SLOT_BYTES;
     size_t mfree = 0, mtotal = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess)
@@ -1817,8 +1817,10 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
                          s->d_tile_count, s->d_pieces, s->d_dep_ctl[sl]);
       hipLaunchKernelGGL(bk_place, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_bucket_tile[sl], s->d_dep_ctl[sl],
                          K.n_buckets, s->n_tiles, s->d_tile_count, s->d_order);
-      hipLaunchKernelGGL(bk_reduce, dim3(1024), dim3(1024), 0, fs, s->d_pool[sl], s->d_order, s->d_chunk_fill[sl],
+#ifndef SMCRT_ABL_NO_FOLD  // timing ablation only: records are never summed (not exact)
+      hipLaunchKernelGGL(bk_reduce, dim3(1024), dim3(RED_THREADS), 0, fs, s->d_pool[sl], s->d_order, s->d_chunk_fill[sl],
                          s->d_pieces, s->d_dep_ctl[sl], nv, Ch.jmean, s->d_queue + MAX_SLOTS + 2);
+#endif
     } else {
     if (!K.hist_tiles)  // else the transport kernel built the counts
       hipLaunchKernelGGL(bin_hist, dim3(BIN_BLOCKS), dim3(BIN_THREADS), 0, fs, s->d_pool[sl], s->d_chunk_fill[sl],
