@@ -252,7 +252,7 @@ contains
         real(c_double), optional, intent(in) :: k
         type(smcrt_sdf) :: s
         if (size(array) < 1) error stop "smcrt_model: a model needs at least one SDF"
-        ! (a child may be a model again, as in the reference; smcrt_scene_create accepts three
+        ! (a child may be a model again, as in the reference; smcrt_scene_create accepts 32
         ! levels of models)
         s%node%kind = SMCRT_SDF_MODEL
         s%node%op = op

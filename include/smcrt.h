@@ -66,7 +66,7 @@ typedef enum smcrt_sdf_kind {
      (first_child, n_children = 1), which may be a primitive, a model or another modifier; it
      takes the layer and optical properties of that node (the *_init functions copy
      prim%optProps and prim%layer) and ignores its own transform (the reference sets it to the
-     identity and never applies it). Models and modifiers nest at most three levels deep. */
+     identity and never applies it). Models and modifiers nest at most 32 levels deep. */
   SMCRT_SDF_REVOLUTION = 12, /* param[0]=o, param[1..3]=center: q = (|(p-c).xz| - o, (p-c).y, 0)   :286-303 */
   SMCRT_SDF_EXTRUDE = 13,    /* param[0]=h: w = (d(p), |p.z| - h); min(max(w),0) + |max(w,0)|    :268-284 */
   SMCRT_SDF_ONION = 14,      /* param[0]=thickness: |d(p)| - thickness                          :305-315 */

@@ -290,6 +290,9 @@ typedef struct {
 } scene_t;
 
 static double sdf_eval_node(const scene_t* S, int32_t idx, vec3 pos, int depth);
+/* composites (models, modifiers) nest at most this many levels below a top, as the engine
+ * accepts (geometry.h PROG_MAX_DEPTH); the reference's recursion has no limit */
+#define ORACLE_MAX_NEST 32
 
 static double csg(int32_t op, double d1, double d2, double k) {
   switch (op) {
@@ -314,14 +317,14 @@ static double sdf_eval_node(const scene_t* S, int32_t idx, vec3 pos, int depth) 
   const smcrt_sdf_node* nd = &S->nodes[idx];
   const double* P = nd->param;
   if (nd->kind == SMCRT_SDF_MODEL) {                                     /* eval_model sdf_base.f90:146-161 */
-    if (depth > 8 || nd->n_children < 1) return NAN;
+    if (depth >= ORACLE_MAX_NEST || nd->n_children < 1) return NAN;
     double res = sdf_eval_node(S, nd->first_child, pos, depth + 1);
     for (int32_t i = 1; i < nd->n_children; ++i)
       res = csg(nd->op, res, sdf_eval_node(S, nd->first_child + i, pos, depth + 1), nd->k);
     return res;
   }
   if (nd->kind > SMCRT_SDF_MODEL) {  /* the modifiers of sdfModifiers.f90: one wrapped node, own transform unused */
-    if (depth > 8 || nd->n_children != 1) return NAN;
+    if (depth >= ORACLE_MAX_NEST || nd->n_children != 1) return NAN;
     const int32_t ch = nd->first_child;
     switch (nd->kind) {
       case SMCRT_SDF_REVOLUTION: {                                       /* eval_revolution :286-303 */

@@ -126,7 +126,7 @@ Bound top_bound(const smcrt_sdf_node* nodes, int32_t n_nodes, int32_t idx) {
 // ds of a top-level SDF at q (host; the fold of sdf_base.f90:146-161). Only used to choose
 // list lengths, never for a result.
 double top_value(const smcrt_sdf_node* nodes, int32_t idx, V3 q) {
-  return node_value<PROG_MAX_DEPTH>(nodes, idx, q);  // (models and modifiers, geometry.h)
+  return node_value(nodes, idx, q);  // (models and modifiers, geometry.h)
 }
 
 double box_dist(const double* clo, const double* chi, const Bound& b) {

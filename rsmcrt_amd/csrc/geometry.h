@@ -176,10 +176,10 @@ enum : int32_t {
 // array(i)%value%evaluate, sdf_base.f90:146-161; or a modifier of sdfModifiers.f90, which
 // wraps one node). A top-level model's children are ops of the program; a child that is
 // itself a composite, or a top-level modifier, is one op with PROG_SUB whose value node_value
-// computes. Three levels of composites are supported; deeper trees are rejected at scene
-// creation.
+// computes. Composites may nest PROG_MAX_DEPTH levels below a top (the reference's recursion
+// has no limit; scene creation rejects deeper trees and trees that contain themselves).
 enum : int32_t { PROG_SUB = 8 };
-constexpr int PROG_MAX_DEPTH = 3;
+constexpr int PROG_MAX_DEPTH = 32;
 
 struct ProgOp {
   int32_t node;   // primitive node index
@@ -247,27 +247,46 @@ __host__ __device__ __forceinline__ double modifier_value(const smcrt_sdf_node* 
 
 // The value of node `idx` at pos: a primitive (its own transform), a model (eval_model's left
 // fold over its children, sdf_base.f90:146-161; the model's transform is not applied) or a
-// modifier (its wrapped node at modifier_point, then modifier_value). D is how many composite
-// levels remain (scene creation rejects deeper trees; a composite at D = 0 is NaN). One loop
-// with one recursive site serves models and modifiers alike, so each level inlines one
-// primitive. Children are evaluated with their transforms in full (dotmat), which equals
-// sdf_prim's translate-only shortcut bit for bit (see sdf_prim_s).
-template <int D>
+// modifier (its wrapped node at modifier_point, then modifier_value). Composites are walked
+// without recursion: a stack of frames (node, next child, accumulator, query point), one per
+// open composite, so the depth costs stack slots (private memory), not inlined code, and
+// every level runs the same single primitive site. The operations and their order are those
+// of the recursive definition, so the value is the same bit for bit. Children are evaluated
+// with their transforms in full (dotmat), which equals sdf_prim's translate-only shortcut bit
+// for bit (see sdf_prim_s). A tree deeper than PROG_MAX_DEPTH (rejected at scene creation)
+// yields NaN.
+struct NodeFrame {
+  int32_t idx, c;  // the composite, its next child
+  double acc;      // the fold of its children so far
+  V3 pos;          // the point it is evaluated at
+};
 __host__ __device__ __forceinline__ double node_value(const smcrt_sdf_node* __restrict__ nodes, int32_t idx, V3 pos) {
-  const smcrt_sdf_node* __restrict__ nd = nodes + idx;
-  if (!composite_kind(nd->kind)) return sdf_prim(nd, pos, false);
-  if constexpr (D == 0) {
-    return __builtin_nan("");
-  } else {
-    const bool model = nd->kind == SMCRT_SDF_MODEL;
-    const int32_t n = model ? nd->n_children : 1;
-    const V3 q = model ? pos : modifier_point(nd, pos);
-    double acc = 0.0;
-    for (int32_t c = 0; c < n; ++c) {
-      const double v = node_value<D - 1>(nodes, nd->first_child + c, q);
-      acc = (c == 0 || !model) ? v : csg(nd->op, acc, v, nd->k);
+  if (!composite_kind(nodes[idx].kind)) return sdf_prim(nodes + idx, pos, false);
+  NodeFrame st[PROG_MAX_DEPTH];
+  int sp = 0;
+  st[0].idx = idx; st[0].c = 0; st[0].acc = 0.0; st[0].pos = pos;
+  for (;;) {
+    const smcrt_sdf_node* __restrict__ M = nodes + st[sp].idx;
+    const bool model = M->kind == SMCRT_SDF_MODEL;
+    double v;
+    if (st[sp].c < (model ? M->n_children : 1)) {
+      const int32_t ci = M->first_child + st[sp].c;
+      const V3 q = model ? st[sp].pos : modifier_point(M, st[sp].pos);
+      if (composite_kind(nodes[ci].kind)) {  // open the child composite
+        if (sp + 1 >= PROG_MAX_DEPTH) return __builtin_nan("");
+        ++sp;
+        st[sp].idx = ci; st[sp].c = 0; st[sp].acc = 0.0; st[sp].pos = q;
+        continue;
+      }
+      v = sdf_prim(nodes + ci, q, false);  // a primitive child: folded into this frame
+    } else {  // every child folded: the composite's value goes to its parent frame
+      v = model ? st[sp].acc : modifier_value(M, st[sp].acc, st[sp].pos);
+      if (sp == 0) return v;
+      --sp;
     }
-    return model ? acc : modifier_value(nd, acc, pos);
+    const smcrt_sdf_node* __restrict__ P = nodes + st[sp].idx;
+    st[sp].acc = (st[sp].c == 0 || P->kind != SMCRT_SDF_MODEL) ? v : csg(P->op, st[sp].acc, v, P->k);
+    ++st[sp].c;
   }
 }
 
@@ -280,7 +299,7 @@ __host__ __device__ __forceinline__ double prog_value(const smcrt_sdf_node* __re
                                                       int32_t action, bool translate_only, V3 q) {
   if constexpr (!NEST) return sdf_prim(nodes + node, q, translate_only);
   if (!(action & PROG_SUB)) return sdf_prim(nodes + node, q, translate_only);
-  return node_value<PROG_MAX_DEPTH>(nodes, node, q);
+  return node_value(nodes, node, q);
 }
 
 }  // namespace smcrt

@@ -118,13 +118,14 @@ def _nested(levels):
 
 
 def test_nested_model_depth_checked_before_the_device(lib_path):
-    """Nested models (eval_model's recursion, sdf_base.f90:146-161) are accepted up to three
-    levels (geometry.h PROG_NEST); a fourth level is rejected with UNSUPPORTED before any
-    device call, so both are checkable without a GPU."""
+    """Nested models (eval_model's recursion, sdf_base.f90:146-161) are accepted up to 32
+    levels (geometry.h PROG_MAX_DEPTH, node_value's explicit stack); a 33rd level is rejected
+    with UNSUPPORTED before any device call, so both are checkable without a GPU."""
     from rsmcrt_amd import engine, scene
     L = engine.load_library(lib_path)
     g = scene.grid(8, 8, 8, 1, 1, 1)
-    for levels, want in ((3, (abi.OK, abi.ERR_NO_DEVICE)), (4, (abi.ERR_UNSUPPORTED,))):
+    for levels, want in ((3, (abi.OK, abi.ERR_NO_DEVICE)), (32, (abi.OK, abi.ERR_NO_DEVICE)),
+                         (33, (abi.ERR_UNSUPPORTED,))):
         sc = _nested(levels)
         h = C.c_void_p()
         st = L.smcrt_scene_create(sc.node_array(), len(sc.nodes), sc.top_array(), sc.n_top, C.byref(g), None, 0, 0,
@@ -132,5 +133,5 @@ def test_nested_model_depth_checked_before_the_device(lib_path):
         assert st in want, (levels, st, L.smcrt_last_error())
         if st == abi.OK:
             L.smcrt_scene_destroy(h)
-        if levels == 4:
+        if levels == 33:
             assert b"nested" in L.smcrt_last_error()

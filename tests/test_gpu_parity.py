@@ -637,13 +637,32 @@ def _nested_models(lay, opt_m):
                                  sphere(0.09, opt_m, lay(), transform=t((-0.22, -0.3, -0.2)))], abi.OP_SUBTRACTION),
                           torus(0.1, 0.02, opt_m, lay(), transform=t((-0.3, -0.3, -0.1)))], abi.OP_SMOOTH_UNION, 0.03),
                    cylinder((-0.3, -0.45, -0.2), (-0.3, -0.15, -0.2), 0.03, opt_m, lay())], abi.OP_UNION)
-    return [two, three]
+    return [two, three, _deep_chain(lay, opt_m)]
+
+
+def _deep_chain(lay, opt_m, levels=16):
+    """A top whose composites nest `levels` deep (geometry.h node_value's explicit stack; the
+    reference's eval_model recursion has no depth limit): models (smooth union with a box) and
+    modifiers (elongate, revolution) alternate down to a sphere."""
+    from rsmcrt_amd.scene import box, elongate, invert, model, revolution, sphere, translate
+    t = lambda c: invert(translate(c))  # noqa: E731
+    node = sphere(0.05, opt_m, lay(), transform=t((0.3, -0.3, 0.0)))
+    for i in range(levels - 1):
+        if i % 3 == 0:
+            node = model([node, box((0.03, 0.03, 0.03), opt_m, lay(), transform=t((0.33, -0.3, 0.02 * (i % 5))))],
+                         abi.OP_SMOOTH_UNION, 0.01)
+        elif i % 3 == 1:
+            node = elongate(node, (0.002, 0.0, 0.001))
+        else:
+            node = revolution(node, 0.0, center=(0.0, 0.0, 0.0)) if i == 2 else model([node], abi.OP_UNION)
+    return node
 
 
 @pytest.mark.parametrize("path", ["serial", "coop", "culled"])
 def test_nested_models(path):
     """Models inside models (geometry.h PROG_SUB: a child model is one op whose value folds
-    its own children, a grandchild model first) in scenes of 3, 11 and ~55 tops that would
+    its own children, a grandchild model first), two, three and 16 levels deep, in scenes of
+    4, 12 and ~56 tops that would
     otherwise take the serial, cooperative and culled EVALs: a scene with nested models always
     runs the general instantiation with the serial EVAL (smcrt.hip), so these check that
     routing too. Fresnel at every nested surface (n differs). Photon records, counters and
