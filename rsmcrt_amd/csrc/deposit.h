@@ -379,6 +379,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 // Sharing the words per block (round 2: per wave before) keeps 4x fewer buckets open, so
 // their partly written cache lines fit in L2 and leave it whole.
 // The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
+#ifndef SMCRT_REC_NT
+#define SMCRT_REC_NT 0
+#endif
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
 #ifndef SMCRT_BUCKET_BATCH
@@ -489,7 +492,17 @@ __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __r
     const bool slot = todo && pos < 2 * BUCKET_RECORDS;
     const bool ok = slot && b < K.n_buckets;
 #ifndef SMCRT_ABL_NO_RECSTORE  // timing ablation only: slots are claimed, records not written
-    if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
+    if (ok) {
+      unsigned long long* const at = K.rec_pool + ((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1));
+#if SMCRT_REC_NT == 2  // experiment: every record store non-temporal
+      __builtin_nontemporal_store(pack_record(vox, val), at);
+#elif SMCRT_REC_NT == 1  // experiment: the store that completes a 128-B line non-temporal
+      if ((pos & 15u) == 15u) __builtin_nontemporal_store(pack_record(vox, val), at);
+      else *at = pack_record(vox, val);
+#else
+      *at = pack_record(vox, val);
+#endif
+    }
 #endif
     const bool claim = todo && pos == BUCKET_RECORDS;
     const bool spill = slot && !ok;
