@@ -25,9 +25,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# eight hardware queues for the scene's streams, set before torch starts the HIP runtime
-# (rsmcrt_amd/__init__.py explains; a caller's own setting wins)
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# at least eight hardware queues for the scene's streams, set before torch starts the HIP
+# runtime (rsmcrt_amd/__init__.py explains; the boxes export HIP's default of 4)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 WORKLOADS = ("m0", "m1", "m2", "m3", "m4", "m5", "escape")
 

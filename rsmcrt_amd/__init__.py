@@ -9,11 +9,25 @@ import os
 # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (default 4), read once
 # when the HIP runtime starts. A scene uses up to four launch streams, its own stream and a
 # fold stream, and torch has its own: with four queues, overlapped launches that share a queue
-# run one after the other. Eight measured +16-19 % on the tail-bound scenes (M4, M5) and no
-# change on M1 (profiles/r03_s3/hwq_ab.txt). setdefault: a caller's own setting wins, and it
-# only takes effect if nothing has started the HIP runtime yet (C/Fortran callers export it
+# run one after the other (a kernel trace shows two launch streams on one queue). Eight
+# measured +16-19 % on the tail-bound scenes (M5, profiles/r03_s3/hwq_ab.txt and
+# profiles/r04_s3/hwq_ab.txt) and no change on M1. The GPU boxes export the HIP default (4)
+# explicitly, so a value below 8 is raised to 8 (a caller's setting of 8 or more wins); it only
+# takes effect if nothing has started the HIP runtime yet (C/Fortran callers export it
 # themselves).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+MIN_HW_QUEUES = 8
+
+
+def _raise_hw_queues(env=os.environ, want=MIN_HW_QUEUES):
+    try:
+        cur = int(env.get("GPU_MAX_HW_QUEUES", "0"))
+    except ValueError:
+        cur = 0
+    if cur < want:
+        env["GPU_MAX_HW_QUEUES"] = str(want)
+
+
+_raise_hw_queues()
 
 from . import abi, builders, scene  # noqa: E402,F401
 
