@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           }
         } else if (K.cull) {
           FarCert fc;
-          S = eval_culled_coop(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, ltab, want ? &fc : nullptr);
+          S = eval_culled_coop<XSRC>(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, ltab, want ? &fc : nullptr);
           if (want && fc.node >= 0) {
             const int32_t node = __builtin_amdgcn_readfirstlane(fc.node);
             const int kind = nodes[node].kind;
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
             }
           }
         } else {
-          S = eval_sdfs(nodes, prog, K.n_prog, q, false, 0, 0);
+          S = eval_sdfs<XSRC>(nodes, prog, K.n_prog, q, false, 0, 0);
         }
         return S;
       };
@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           const int l = __builtin_ctzll(m);
           m &= m - 1;
           const V3 ql = v3(__shfl(q.x, l, 64), __shfl(q.y, l, 64), __shfl(q.z, l, 64));
-          const EvalOut o = eval_sdfs_coop(nodes, prog, K.n_prog, K.n_top, ql, __shfl((int)mask_le, l, 64) != 0,
+          const EvalOut o = eval_sdfs_coop<XSRC>(nodes, prog, K.n_prog, K.n_top, ql, __shfl((int)mask_le, l, 64) != 0,
                                            __shfl(capi, l, 64), __shfl(capj, l, 64));
           if (lane_id == l) R = o;
         }
@@ -453,13 +453,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           const int l = __builtin_ctzll(m);
           m &= m - 1;
           const V3 ql = v3(readlane_f64(q.x, l), readlane_f64(q.y, l), readlane_f64(q.z, l));
-          const EvalOut o = eval_culled_coop(nodes, prog, K.n_prog, K.cull, ql,
+          const EvalOut o = eval_culled_coop<XSRC>(nodes, prog, K.n_prog, K.cull, ql,
                                              __builtin_amdgcn_readlane((int)mask_le, l) != 0,
                                              __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l), ltab);
           if (lane_id == l) R = o;
         }
       } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)
-        R = eval_culled(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj, ltab);
+        R = eval_culled<XSRC>(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj, ltab);
       } else {
         R = eval_sdfs<XSRC>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }
@@ -950,7 +950,8 @@ struct smcrt_scene {
   unsigned long long far_reported = 0;
   // a top model has a model or modifier among its children, or a top is a modifier: only the
   // general instantiation evaluates composites below the top level (geometry.h node_value), so
-  // such scenes always run it, with the serial EVAL (no cooperative, culled or lean paths)
+  // such scenes always run it: with many tops its COOP variant (cooperative and culled EVALs,
+  // round 4), else the serial EVAL; never the lean kernel
   bool nested = false;
   // the fold's workgroup run time: d_queue[MAX_SLOTS + 2] running total (s_memrealtime ticks at
   // wall_khz), reported per CU (one bk_reduce workgroup fills a CU)
@@ -1089,16 +1090,18 @@ static hipError_t harvest_times(smcrt_scene* s) {
 }
 
 // The transport kernel instantiation for this scene (LDS faces? power-of-two grid?).
-// Scenes with many tops (coop_lanes > 0) and a plain source get the instantiation with the
-// cooperative tail EVAL; it costs registers (scratch spills), so small scenes never pay for it.
+// Scenes with many tops (coop_lanes > 0) get an instantiation with the cooperative tail EVAL
+// and culling; it costs registers (scratch spills), so small scenes never pay for it. With the
+// general emitter (XSRC: other sources, batched origins, composites below the top level) that
+// is transport_kernel<.., true, true> (round 4; before, such scenes ran the serial EVAL).
 static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
 #define TK(F, G)                                                                                         \
   {(const void*)transport_kernel<F, G, false, false>, (const void*)transport_kernel<F, G, true, false>, \
-   (const void*)transport_kernel<F, G, false, true>}
-  static const void* const fns[2][3][3] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
+   (const void*)transport_kernel<F, G, false, true>, (const void*)transport_kernel<F, G, true, true>}
+  static const void* const fns[2][3][4] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
                                            {TK(true, 0), TK(true, 1), TK(true, 2)}};
 #undef TK
-  return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : (s->coop_lanes > 0 ? 2 : 0)];
+  return fns[s->lds_faces ? 1 : 0][s->grid_mode][(xsrc ? 1 : 0) + (s->coop_lanes > 0 ? 2 : 0)];
 }
 
 // lean_kernel (lean.h) of this scene's face staging and grid mode
@@ -1116,8 +1119,9 @@ static size_t lean_lds(const smcrt_scene* s) {
 // Dynamic LDS of the transport kernel: staged props + faces, detector start points, then the
 // deposit words (4 wave tile histograms, or the block's bucket words), then the coop table.
 static size_t transport_lds(const smcrt_scene* s, uint32_t dep_words, bool xsrc) {
-  const bool ctab = s->d_ctab && !xsrc && s->coop_lanes > 0;  // the COOP instantiation stages it
-  const bool coop = !xsrc && s->coop_lanes > 0;  // the COOP instantiation also stages the LDS records
+  (void)xsrc;
+  const bool ctab = s->d_ctab && s->coop_lanes > 0;  // the COOP instantiations stage it
+  const bool coop = s->coop_lanes > 0;  // the COOP instantiations also stage the LDS records
   return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
          (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0) +
          (coop ? (size_t)s->n_ltab * LTAB_DOUBLES * sizeof(double) : 0);
@@ -1301,7 +1305,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   // A sparse wave evaluates its lanes' SDF arrays one lane at a time across the wave when
   // that is cheaper than the serial per-lane chain over all n_top tops (transport.h).
   for (const ProgOp& op : prog) s->nested = s->nested || (op.action & PROG_SUB) != 0;
-  s->coop_lanes = n_top >= 8 && !s->nested ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
+  s->coop_lanes = n_top >= 8 ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
   // The cooperative EVAL's LDS table: at most 64 tops, none of them a model (transport.h).
   // SMCRT_COOP_TAB=0 keeps the global-memory cooperative EVAL.
   std::vector<double> ctab;

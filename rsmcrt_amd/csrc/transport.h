@@ -942,6 +942,7 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
 // cycles). Results equal eval_sdfs': min/abs-min are exact, maxloc ties go to the lowest top
 // index as eval_sdfs' strict compares do, and the captured values come from the owning lane.
 // (minv may differ from eval_sdfs' in the sign of a zero; it is only ever tested with > 0.)
+template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restrict__ nodes,
                                                            const ProgOp* __restrict__ prog, int32_t n_prog,
                                                            int32_t n_top, V3 q, bool mask_le, int32_t capi,
@@ -956,7 +957,7 @@ __device__ __forceinline__ EvalOut eval_sdfs_coop(const smcrt_sdf_node* __restri
     double acc = 0.0;
     for (int32_t ip = b; ip < e; ++ip) {
       const ProgOp op = prog[ip];
-      const double v = prog_value<false>(nodes, op.node, op.action, op.translate_only != 0, q);
+      const double v = prog_value<NEST>(nodes, op.node, op.action, op.translate_only != 0, q);
       if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
       else acc = csg(op.op, acc, v, op.k);
     }
@@ -1108,6 +1109,7 @@ __device__ unsigned long long g_cull_diag[6];
 #ifndef SMCRT_CULL_PREFETCH
 #define SMCRT_CULL_PREFETCH 1
 #endif
+template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict__ nodes,
                                                const ProgOp* __restrict__ prog, int32_t n_prog,
                                                const CullGrid* __restrict__ G, V3 q, bool have, bool mask_le,
@@ -1125,7 +1127,7 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     for (int32_t ip = 0; ip < na; ++ip) {
       const ProgOp op = pa[ip];
       const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-      const double v = prog_value<false>(nodes, node, op.action, op.translate_only != 0, q);
+      const double v = prog_value<NEST>(nodes, node, op.action, op.translate_only != 0, q);
       if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
       else acc = csg(op.op, acc, v, op.k);
       if (op.top > 0) {
@@ -1168,7 +1170,7 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
         double acc = 0.0;
         for (int32_t ip = o0; ip < o1; ++ip) {
           const ProgOp op = prog[ip];
-          const double v = prog_value<false>(nodes, op.node, op.action, op.translate_only != 0, q);
+          const double v = prog_value<NEST>(nodes, op.node, op.action, op.translate_only != 0, q);
           if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
           else acc = csg(op.op, acc, v, op.k);
         }
@@ -1207,7 +1209,7 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
   if ((threadIdx.x & 63) == 0 && __ballot(have && full)) atomicAdd(&g_cull_diag[5], 1ull);
 #endif
   if (__ballot(have && full)) {
-    const EvalOut f = eval_sdfs(nodes, prog, n_prog, q, mask_le, capi, capj);
+    const EvalOut f = eval_sdfs<NEST>(nodes, prog, n_prog, q, mask_le, capi, capj);
     if (full) r = f;
   }
   return r;
@@ -1219,6 +1221,7 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
 // memory latencies per list instead of one per entry and lane. Results equal eval_culled's
 // (and so eval_sdfs'): min and abs-min are order free, maxloc ties go to the lowest index.
 // Call with all lanes active; q, mask_le, capi and capj must be wave-uniform.
+template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __restrict__ nodes,
                                                     const ProgOp* __restrict__ prog, int32_t n_prog,
                                                     const CullGrid* __restrict__ G, V3 q, bool mask_le,
@@ -1247,7 +1250,7 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
     for (int32_t ip = 0; ip < na; ++ip) {
       const ProgOp op = pa[ip];
       const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
-      const double v = prog_value<false>(nodes, node, op.action, op.translate_only != 0, q);
+      const double v = prog_value<NEST>(nodes, node, op.action, op.translate_only != 0, q);
       if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
       else acc = csg(op.op, acc, v, op.k);
       if (op.top > 0) {
@@ -1302,7 +1305,7 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
           double acc = 0.0;
           for (int32_t ip = o0; ip < o1; ++ip) {
             const ProgOp op = prog[ip];
-            const double v = prog_value<false>(nodes, op.node, op.action, op.translate_only != 0, q);
+            const double v = prog_value<NEST>(nodes, op.node, op.action, op.translate_only != 0, q);
             if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
             else acc = csg(op.op, acc, v, op.k);
           }
@@ -1378,7 +1381,7 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
       }
     }
   }
-  if (full) r = eval_sdfs(nodes, prog, n_prog, q, mask_le, capi, capj);
+  if (full) r = eval_sdfs<NEST>(nodes, prog, n_prog, q, mask_le, capi, capj);
   return r;
 }
 

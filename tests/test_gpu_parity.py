@@ -662,11 +662,12 @@ def _deep_chain(lay, opt_m, levels=16):
 def test_nested_models(path):
     """Models inside models (geometry.h PROG_SUB: a child model is one op whose value folds
     its own children, a grandchild model first), two, three and 16 levels deep, in scenes of
-    4, 12 and ~56 tops that would
-    otherwise take the serial, cooperative and culled EVALs: a scene with nested models always
-    runs the general instantiation with the serial EVAL (smcrt.hip), so these check that
-    routing too. Fresnel at every nested surface (n differs). Photon records, counters and
-    grids bit-exact against the oracle, whose eval_model recursion is the reference's."""
+    4, 12 and ~56 tops that take the serial, cooperative and culled EVALs: a scene with
+    composites below the top level runs the general instantiation (smcrt.hip), and since
+    round 4 its COOP variant when it has many tops (cooperative and culled EVALs with the
+    composite evaluator), so these check that routing too. Fresnel at every nested surface
+    (n differs). Photon records, counters and grids bit-exact against the oracle, whose
+    eval_model recursion is the reference's."""
     from rsmcrt_amd.scene import Scene, box, invert, mono, sphere, translate
     sdfs = []
     lay = lambda: len(sdfs) + 1  # noqa: E731
