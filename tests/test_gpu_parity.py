@@ -689,6 +689,22 @@ def test_nested_models(path):
     assert cpu.counter("fresnel") > 0
 
 
+@pytest.mark.parametrize("kind", ["table", "culled"])
+def test_general_emitter_many_tops(kind):
+    """A source of the general emitter (circular, photon.f90) in a many-top scene runs
+    transport_kernel<.., XSRC, COOP> (round 4; before, such scenes took the serial EVAL): the
+    40-sphere scene (cooperative LDS table, far-field march) and the ~56-top culling scene
+    (culled EVAL). Counters, photon records and grids bit-exact against the oracle."""
+    if kind == "table":
+        sc = builders.setup_sphere_scene(builders.random_sphere_list(40))
+    else:
+        sc = _culling_scene()
+    src = scene.circular_source((0.0, 0.0, 0.9999), (0.0, 0.0, -1.0), 0.995)
+    gpu, cpu = both(sc, scene.grid(32, 32, 32, 1, 1, 1), src, 3000)
+    compare(gpu, cpu)
+    assert cpu.counter("photons") == 3000 and cpu.counter("sdf_evals") > 0
+
+
 def _culling_scene(seed=7):
     """~60 tops for the culled EVAL (cull.h): random capsules, rotated and translated
     spheres, tori and capped cylinders, smooth-union / intersection / subtraction models, a
