@@ -1340,14 +1340,36 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     bool fm = !(fe && std::string(fe) == "0");
     double ext = grid->xmax + grid->ymax + grid->zmax + 1.0;
     double scale = 0.0;
-    for (int32_t i = 0; fm && i < n_top; ++i) {
-      const smcrt_sdf_node& nd = nodes[top[i]];
+    // A top qualifies if it is such a primitive, or (round 4) a model of qualifying children
+    // folded with union, intersection, subtraction or smooth union (min/max of 1-Lipschitz
+    // values is 1-Lipschitz, and so is the polynomial smooth minimum: its partials are 1 - h^2/2
+    // and h^2/2), at most 4 model levels deep so the fold's few roundings per level stay far
+    // below the bound. The near top of a certificate is still a lone sphere or box (far.h).
+    // m accumulates the operand magnitudes the error bound scales with.
+    std::function<bool(int32_t, int, double&)> far_ok = [&](int32_t idx, int lvl, double& m) -> bool {
+      const smcrt_sdf_node& nd = nodes[idx];
+      if (nd.kind == SMCRT_SDF_MODEL) {
+        const bool op_ok = nd.op == SMCRT_OP_UNION || nd.op == SMCRT_OP_INTERSECTION || nd.op == SMCRT_OP_SUBTRACTION ||
+                           (nd.op == SMCRT_OP_SMOOTH_UNION && nd.k > 0.0 && std::isfinite(nd.k));
+        if (lvl >= 4 || !op_ok || nd.n_children < 1) return false;
+        if (nd.op == SMCRT_OP_SMOOTH_UNION) m = std::max(m, nd.k);
+        for (int32_t c = 0; c < nd.n_children; ++c)
+          if (!far_ok(nd.first_child + c, lvl + 1, m)) return false;
+        return true;
+      }
       const int32_t kd = nd.kind;
-      fm = translate_only(top[i]) && (kd == SMCRT_SDF_SPHERE || kd == SMCRT_SDF_BOX || kd == SMCRT_SDF_TORUS ||
-                                      kd == SMCRT_SDF_SEGMENT || kd == SMCRT_SDF_CAPSULE);
-      double m = std::fabs(nd.transform[3]) + std::fabs(nd.transform[7]) + std::fabs(nd.transform[11]);
-      for (int r = 0; r < 8; ++r) m += std::fabs(nd.param[r]);
-      fm = fm && std::isfinite(m);
+      if (!translate_only(idx) || !(kd == SMCRT_SDF_SPHERE || kd == SMCRT_SDF_BOX || kd == SMCRT_SDF_TORUS ||
+                                    kd == SMCRT_SDF_SEGMENT || kd == SMCRT_SDF_CAPSULE))
+        return false;
+      double mm = std::fabs(nd.transform[3]) + std::fabs(nd.transform[7]) + std::fabs(nd.transform[11]);
+      for (int r = 0; r < 8; ++r) mm += std::fabs(nd.param[r]);
+      if (!std::isfinite(mm)) return false;
+      m = std::max(m, mm);
+      return true;
+    };
+    for (int32_t i = 0; fm && i < n_top; ++i) {
+      double m = 0.0;
+      fm = far_ok(top[i], 0, m);
       scale = std::max(scale, m);
     }
     fm = fm && std::isfinite(ext);

@@ -31,15 +31,21 @@ decimal.getcontext().prec = 60
 FAR_KINDS = (abi.SDF_SPHERE, abi.SDF_BOX, abi.SDF_TORUS, abi.SDF_SEGMENT, abi.SDF_CAPSULE)
 
 
+def node_scale(sc, i):
+    """The operand magnitude a top contributes to the bound (smcrt.hip far_ok): a primitive's
+    translation and parameters; a model's largest child, and its smooth-union k."""
+    nd = sc.nodes[i]
+    if nd.kind == abi.SDF_MODEL:
+        m = nd.k if nd.op == abi.OP_SMOOTH_UNION else 0.0
+        return max([m] + [node_scale(sc, nd.first_child + c) for c in range(nd.n_children)])
+    m = abs(nd.transform[3]) + abs(nd.transform[7]) + abs(nd.transform[11])
+    return m + sum(abs(nd.param[r]) for r in range(8))
+
+
 def fm_bounds(sc, g):
     """fm_err, fm_step as the host computes them (smcrt.hip, far-field block)."""
     ext = g.xmax + g.ymax + g.zmax + 1.0
-    scale = 0.0
-    for i in sc.top:
-        nd = sc.nodes[i]
-        m = abs(nd.transform[3]) + abs(nd.transform[7]) + abs(nd.transform[11])
-        m += sum(abs(nd.param[r]) for r in range(8))
-        scale = max(scale, m)
+    scale = max(node_scale(sc, i) for i in sc.top)
     return np.ldexp(scale + ext, -44), np.ldexp(scale + ext, -48)
 
 
@@ -156,4 +162,69 @@ def test_far_field_error_bound(workload):
     # the grid's extent plus the scale
     assert np.spacing(g.xmax + g.ymax + g.zmax + scale) <= fm_step / 2
     # the bound's actual slack (measured: the worst error is ~1e-3 of fm_err at both scales)
+    assert worst <= fm_err / 64, (worst, fm_err)
+
+
+def exact_node(sc, i, p):
+    """A far-eligible top in decimal arithmetic: a primitive (exact_sdf) or a model folded left
+    to right with union / smooth union / subtraction / intersection (sdfModifiers.f90:428-491)."""
+    nd = sc.nodes[i]
+    if nd.kind != abi.SDF_MODEL:
+        return exact_sdf(nd, p)
+    acc = None
+    k = D(nd.k)
+    for c in range(nd.n_children):
+        v = exact_node(sc, nd.first_child + c, p)
+        if acc is None:
+            acc = v
+        elif nd.op == abi.OP_UNION:
+            acc = min(acc, v)
+        elif nd.op == abi.OP_SMOOTH_UNION:
+            h = max(k - abs(acc - v), D(0)) / k
+            acc = min(acc, v) - h * h * h * k * (D(1) / D(6))
+        elif nd.op == abi.OP_SUBTRACTION:
+            acc = max(-acc, v)
+        else:
+            acc = max(acc, v)
+    return acc
+
+
+@pytest.mark.parametrize("scale_of", ["m2", "m4"])
+def test_far_field_error_bound_models(scale_of):
+    """Round 4: a model of far-eligible primitives folded with union, smooth union,
+    subtraction or intersection (two levels deep too) qualifies for the far-field march as a
+    non-near top (smcrt.hip far_ok). Its computed value must be within the same bound:
+    evaluated by the restatement at adversarial points of every child, against the fold in
+    60-digit decimal arithmetic."""
+    from rsmcrt_amd.scene import box, capsule, model, sphere, torus
+    _, g, _, _, _, _ = bench.workload(scale_of, 32)
+    s = max(g.xmax, g.ymax, g.zmax)
+    o = mono(1.0, 0.1, 0.9, 1.0)
+    t = lambda c: invert(translate(tuple(v * s for v in c)))  # noqa: E731
+    kids = lambda: [sphere(0.2 * s, o, 1, transform=t((0.1, 0.0, 0.05))),  # noqa: E731
+                    box((0.15 * s, 0.1 * s, 0.2 * s), o, 1, transform=t((0.2, -0.05, 0.0))),
+                    capsule((0.0, -0.1 * s, 0.0), (0.2 * s, 0.1 * s, 0.1 * s), 0.05 * s, o, 1,
+                            transform=t((-0.1, 0.1, 0.0)))]
+    tops = [model(kids(), abi.OP_UNION), model(kids(), abi.OP_SMOOTH_UNION, 0.05 * s),
+            model(kids(), abi.OP_SUBTRACTION), model(kids(), abi.OP_INTERSECTION),
+            model([model(kids()[:2], abi.OP_SMOOTH_UNION, 0.03 * s),
+                   torus(0.2 * s, 0.05 * s, o, 1, transform=t((0.0, 0.2, -0.1)))], abi.OP_UNION)]
+    full = Scene(tops)
+    fm_err, _ = fm_bounds(full, g)
+    rng = np.random.Generator(np.random.Philox(11))
+    worst = 0.0
+
+    def prims(i):
+        nd = full.nodes[i]
+        if nd.kind != abi.SDF_MODEL:
+            return [nd]
+        return [q for c in range(nd.n_children) for q in prims(nd.first_child + c)]
+
+    for which, i in enumerate(full.top):
+        pts = np.concatenate([adversarial_points(nd, g, rng, n=27) for nd in prims(i)])
+        got = O.sdf_eval(full, pts, which)
+        for p, v in zip(pts, got):
+            err = abs(D(float(v)) - exact_node(full, i, p))
+            worst = max(worst, float(err))
+            assert err <= D(fm_err) / 2, (scale_of, which, p.tolist(), float(err), fm_err)
     assert worst <= fm_err / 64, (worst, fm_err)

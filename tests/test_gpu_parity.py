@@ -135,6 +135,49 @@ def test_far_field_march(case, monkeypatch):
         assert kt["far_steps"] > steps // 2, (kt, steps)  # most steps ran in the far-field loop
 
 
+@pytest.mark.parametrize("variant", ["models", "off"])
+def test_far_field_march_with_models(variant, monkeypatch):
+    """Round 4: tops that are models of far-eligible primitives (union, smooth union,
+    subtraction, intersection, nested) no longer switch the far-field march off (smcrt.hip
+    far_ok; their error bound: test_far_bound.py). 30 spheres, 6 models and a medium box take
+    the culled EVAL, whose certificate bounds the models as non-near tops; wall photons march
+    1e-3 from a side wall. Bit-exact against the oracle and against SMCRT_FAR_MARCH=0."""
+    from rsmcrt_amd.scene import Scene, box, capsule, invert, model, mono, sphere, translate
+    if variant == "off":
+        monkeypatch.setenv("SMCRT_FAR_MARCH", "0")
+    sc0 = builders.setup_sphere_scene(builders.random_sphere_list(30))
+    sdfs = list(sc0.sdfs[:-1])
+    lay = lambda: len(sdfs) + 1  # noqa: E731
+    om = mono(4.0, 0.2, 0.6, 1.3)
+    t = lambda c: invert(translate(c))  # noqa: E731
+    for j in range(6):
+        x = -0.6 + 0.24 * j
+        kids = [sphere(0.08, om, lay(), transform=t((x, 0.5, 0.2))),
+                box((0.06, 0.05, 0.07), om, lay(), transform=t((x + 0.05, 0.52, 0.2))),
+                capsule((x, 0.4, 0.0), (x + 0.1, 0.45, 0.1), 0.03, om, lay())]
+        op = (abi.OP_UNION, abi.OP_SMOOTH_UNION, abi.OP_SUBTRACTION, abi.OP_INTERSECTION)[j % 4]
+        m = model(kids, op, 0.04)
+        if j == 5:
+            m = model([model(kids[:2], abi.OP_SMOOTH_UNION, 0.03), kids[2]], abi.OP_UNION)
+        sdfs.append(m)
+    sdfs.append(sc0.sdfs[-1])
+    sc = Scene(sdfs)
+    g = scene.grid(32, 32, 32, 1, 1, 1)
+    src = scene.uniform_source((-1.0, -1.0, 0.9999999), (1e-3, 0.0, 0.0), (0.0, 2.0, 0.0), (0.0, 0.0, -1.0))
+    n = 200
+    with Engine(sc, g) as eng:
+        eng.kernel_times()
+        gpu = eng.run(src, n, seed=SEED, records=True)
+        kt = eng.kernel_times()
+    cpu = O.run(sc, g, src, n, seed=SEED, records=True)
+    compare(gpu, cpu)
+    assert cpu.counter("grid_updates") > n * 2000  # (long marches)
+    if variant == "off":
+        assert kt["far_steps"] == 0, kt
+    else:
+        assert kt["far_steps"] > cpu.counter("grid_updates") // 2, kt
+
+
 @pytest.mark.parametrize("geom", ["parallel", "oblique"])
 @pytest.mark.parametrize("variant", ["table", "culled", "off"])
 def test_far_glance_wall_photons(variant, geom, monkeypatch):
