@@ -1097,11 +1097,18 @@ static hipError_t harvest_times(smcrt_scene* s) {
 static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
 #define TK(F, G)                                                                                         \
   {(const void*)transport_kernel<F, G, false, false>, (const void*)transport_kernel<F, G, true, false>, \
-   (const void*)transport_kernel<F, G, false, true>, (const void*)transport_kernel<F, G, true, true>}
-  static const void* const fns[2][3][4] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
+   (const void*)transport_kernel<F, G, false, true>}
+  static const void* const fns[2][3][3] = {{TK(false, 0), TK(false, 1), TK(false, 2)},
                                            {TK(true, 0), TK(true, 1), TK(true, 2)}};
 #undef TK
-  return fns[s->lds_faces ? 1 : 0][s->grid_mode][(xsrc ? 1 : 0) + (s->coop_lanes > 0 ? 2 : 0)];
+  // (the general emitter with the COOP machinery is instantiated with faces in device memory
+  // only: three kernels instead of six, the library's build time, for the rare scenes that run
+  // it; transport_lds follows)
+  static const void* const xcoop[3] = {(const void*)transport_kernel<false, 0, true, true>,
+                                       (const void*)transport_kernel<false, 1, true, true>,
+                                       (const void*)transport_kernel<false, 2, true, true>};
+  if (xsrc && s->coop_lanes > 0) return xcoop[s->grid_mode];
+  return fns[s->lds_faces ? 1 : 0][s->grid_mode][xsrc ? 1 : (s->coop_lanes > 0 ? 2 : 0)];
 }
 
 // lean_kernel (lean.h) of this scene's face staging and grid mode
@@ -1119,10 +1126,10 @@ static size_t lean_lds(const smcrt_scene* s) {
 // Dynamic LDS of the transport kernel: staged props + faces, detector start points, then the
 // deposit words (4 wave tile histograms, or the block's bucket words), then the coop table.
 static size_t transport_lds(const smcrt_scene* s, uint32_t dep_words, bool xsrc) {
-  (void)xsrc;
   const bool ctab = s->d_ctab && s->coop_lanes > 0;  // the COOP instantiations stage it
   const bool coop = s->coop_lanes > 0;  // the COOP instantiations also stage the LDS records
-  return (s->lds_faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
+  const bool faces = s->lds_faces && !(xsrc && s->coop_lanes > 0);  // (transport_fn)
+  return (faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
          (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0) +
          (coop ? (size_t)s->n_ltab * LTAB_DOUBLES * sizeof(double) : 0);
 }
