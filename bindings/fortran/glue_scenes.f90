@@ -2,13 +2,14 @@
 ! parse_detectors.f90 and parse_source.f90 build them from res/<name>.toml, and writes each
 ! as the flat tables smcrt_scene_create receives. tests/test_fortran_binding.py compares them
 ! field by field with the C++ TOML front end (smcrt_job_scene) on the same files.
-! usage: glue_scenes OUTDIR  ->  OUTDIR/<name>.bin for scat_test, aptran, validation1, omg,
-! test_dects, egg_test
+! usage: glue_scenes OUTDIR [VESSELDIR]  ->  OUTDIR/<name>.bin for scat_test, aptran,
+! validation1, omg, test_dects, egg_test, and vessels (get_vessels on VESSELDIR's edges.dat,
+! nodes.dat, radii.dat; res/vessels.toml's uniform source) when VESSELDIR is given
 program glue_scenes
     use smcrt_mod
     use smcrt_glue
     implicit none
-    character(len=512) :: outdir
+    character(len=512) :: outdir, vdir
     type(smcrt_sdf), allocatable :: a(:), kids(:)
     type(smcrt_detector), allocatable :: d(:)
     type(smcrt_source) :: src
@@ -19,6 +20,8 @@ program glue_scenes
     integer :: i, ierr
 
     call get_command_argument(1, outdir)
+    vdir = ""
+    if (command_argument_count() >= 2) call get_command_argument(2, vdir)
     zero = smcrt_mono(0._c_double, 0._c_double, 0._c_double, 1._c_double)
 
     ! res/scat_test.toml: setup_scat_test (setupGeometry.f90:409-435), tau = 10; point source
@@ -122,6 +125,19 @@ program glue_scenes
                              corner1, corner2, corner3, src)
     call emit("egg_test", a, d, src, ierr)
     deallocate(a, d)
+
+    ! res/vessels.toml: get_vessels (:552-652) on the data set in VESSELDIR; uniform source on
+    ! the top face with the vector direction applied (DESIGN.md §2)
+    if (len_trim(vdir) > 0) then
+        allocate(d(0))
+        call smcrt_get_vessels(trim(vdir), a, ierr)
+        if (ierr /= SMCRT_OK) error stop "smcrt_get_vessels failed"
+        ierr = smcrt_source_from("uniform", [0._c_double, 0._c_double, 0._c_double], [0._c_double, 0._c_double, &
+                                 -1._c_double], [-0.16_c_double, -0.09_c_double, 0.129999_c_double], &
+                                 [0.32_c_double, 0._c_double, 0._c_double], [0._c_double, 0.18_c_double, 0._c_double], src)
+        call emit("vessels", a, d, src, ierr)
+        deallocate(a, d)
+    end if
 
 contains
 

@@ -27,7 +27,7 @@ module smcrt_glue
               smcrt_capsule, smcrt_cone, smcrt_egg, smcrt_plane, smcrt_model
     public :: smcrt_revolution, smcrt_extrude, smcrt_onion, smcrt_twist, smcrt_bend, smcrt_elongate, &
               smcrt_displacement_sine
-    public :: smcrt_count_nodes, smcrt_flatten
+    public :: smcrt_count_nodes, smcrt_flatten, smcrt_get_vessels
     public :: smcrt_circle_dect, smcrt_annulus_dect, smcrt_camera, smcrt_fibre_dect
     public :: smcrt_source_from
     public :: smcrt_identity, smcrt_translate, smcrt_rotate_y, smcrt_invert
@@ -284,7 +284,7 @@ contains
         s%children(1) = prim_sdf
     end function modifier
 
-    function smcrt_revolution(prim_sdf, o, center) result(s)  ! revolution_init :232-259
+    function smcrt_revolution(prim_sdf, o, center) result(s)  ! revolution_init :238-266
         type(smcrt_sdf), intent(in) :: prim_sdf
         real(c_double), intent(in) :: o
         real(c_double), optional, intent(in) :: center(3)
@@ -302,7 +302,7 @@ contains
         s = modifier(SMCRT_SDF_EXTRUDE, prim_sdf, [h])
     end function smcrt_extrude
 
-    function smcrt_onion(prim_sdf, thickness) result(s)  ! onion_init :261-277
+    function smcrt_onion(prim_sdf, thickness) result(s)  ! onion_init :268-284
         type(smcrt_sdf), intent(in) :: prim_sdf
         real(c_double), intent(in) :: thickness
         type(smcrt_sdf) :: s
@@ -338,6 +338,96 @@ contains
         type(smcrt_sdf) :: s
         s = modifier(SMCRT_SDF_DISPLACEMENT, prim_sdf, [real(SMCRT_DISP_SINE, c_double), amplitude, freq])
     end function smcrt_displacement_sine
+
+    ! ------------------------------------------------------------ scene builders ------------
+    !> get_vessels (setupGeometry.f90:552-652) for a host that builds the vessel net itself:
+    !> reads dir/edges.dat, dir/nodes.dat and dir/radii.dat with list-directed reads, counts
+    !> as the reference does (successful reads until the first failure, :585-602), reads the
+    !> nodes with the edge count as the loop bound (:615), rescales (:629-639, res = 0.001) and
+    !> returns one capsule per edge plus the dermis box. Rows of nodes that the :615 bound
+    !> leaves unread are 0 here (the reference leaves them undefined), as in the C++ front end.
+    !> status: SMCRT_OK, or SMCRT_ERR_INVALID_ARG for a missing file, no edge, an edge naming a
+    !> node outside 1..N, or an axis whose max|coordinate| is 0.
+    subroutine smcrt_get_vessels(dir, array, status)
+        character(len=*), intent(in) :: dir
+        type(smcrt_sdf), allocatable, intent(out) :: array(:)
+        integer, intent(out) :: status
+        real(c_double), allocatable :: xyz(:, :), rad(:)
+        integer, allocatable :: ends(:, :)
+        integer :: u, ios, ne, nn, i, j1, j2
+        real(c_double) :: v3(3), mx(3), scale
+        integer :: e2(2)
+        type(smcrt_optprop) :: vessel, dermis
+
+        status = SMCRT_ERR_INVALID_ARG
+        vessel = smcrt_mono(94._c_double, 231._c_double, 0.9_c_double, 1.37_c_double)
+        dermis = smcrt_mono(357._c_double, 0.458_c_double, 0.9_c_double, 1.37_c_double)
+        scale = 0.001_c_double
+
+        open(newunit=u, file=dir//"/edges.dat", status="old", action="read", iostat=ios)
+        if (ios /= 0) return
+        ne = 0
+        do
+            read(u, *, iostat=ios) e2
+            if (ios /= 0) exit
+            ne = ne + 1
+        end do
+        close(u)
+        open(newunit=u, file=dir//"/nodes.dat", status="old", action="read", iostat=ios)
+        if (ios /= 0) return
+        nn = 0
+        do
+            read(u, *, iostat=ios) v3
+            if (ios /= 0) exit
+            nn = nn + 1
+        end do
+        close(u)
+        if (ne == 0) return
+        allocate(ends(ne, 2), xyz(nn, 3), rad(nn))
+        ends = 0
+        xyz = 0._c_double
+        rad = 0._c_double
+
+        open(newunit=u, file=dir//"/edges.dat", status="old", action="read")
+        do i = 1, ne
+            read(u, *, iostat=ios) ends(i, :)
+            if (ios /= 0) exit
+        end do
+        close(u)
+        open(newunit=u, file=dir//"/nodes.dat", status="old", action="read")
+        do i = 1, min(ne, nn)        ! the reference's bound is the edge count (:615)
+            read(u, *, iostat=ios) xyz(i, :)
+            if (ios /= 0) exit
+        end do
+        close(u)
+        open(newunit=u, file=dir//"/radii.dat", status="old", action="read", iostat=ios)
+        if (ios /= 0) return
+        do i = 1, nn
+            read(u, *, iostat=ios) rad(i)
+            if (ios /= 0) exit
+        end do
+        close(u)
+
+        do i = 1, 3
+            mx(i) = maxval(abs(xyz(:, i)))
+            if (.not. (mx(i) > 0._c_double)) return
+            xyz(:, i) = xyz(:, i) / mx(i) - 0.5_c_double
+            xyz(:, i) = xyz(:, i) * mx(i) * scale
+        end do
+
+        allocate(array(ne + 1))
+        do i = 1, ne
+            j1 = ends(i, 1)
+            j2 = ends(i, 2)
+            if (j1 < 1 .or. j1 > nn .or. j2 < 1 .or. j2 > nn) then
+                deallocate(array)
+                return
+            end if
+            array(i) = smcrt_capsule(xyz(j1, :), xyz(j2, :), rad(j1) * scale, vessel, 1)
+        end do
+        array(ne + 1) = smcrt_box([.32_c_double, .18_c_double, .26_c_double], dermis, 2)
+        status = SMCRT_OK
+    end subroutine smcrt_get_vessels
 
     ! ------------------------------------------------------------ flattening ---------------
     recursive integer function smcrt_count_nodes(array) result(n)

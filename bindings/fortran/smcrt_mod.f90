@@ -9,6 +9,9 @@ module smcrt_mod
     implicit none
 
     integer(c_int), parameter :: SMCRT_OK = 0
+    ! smcrt_status (include/smcrt.h)
+    integer(c_int), parameter :: SMCRT_ERR_INVALID_ARG = -1, SMCRT_ERR_HIP = -2, SMCRT_ERR_RCCL = -3, &
+        SMCRT_ERR_DEVICE_FAULT = -4, SMCRT_ERR_NO_DEVICE = -5, SMCRT_ERR_OOM = -6, SMCRT_ERR_UNSUPPORTED = -7
     ! smcrt_sdf_kind
     integer(c_int32_t), parameter :: SMCRT_SDF_SPHERE = 1, SMCRT_SDF_BOX = 2, SMCRT_SDF_TORUS = 3, &
         SMCRT_SDF_CYLINDER = 4, SMCRT_SDF_TRIPRISM = 5, SMCRT_SDF_SEGMENT = 6, SMCRT_SDF_CAPSULE = 7, &

@@ -67,21 +67,21 @@ typedef enum smcrt_sdf_kind {
      takes the layer and optical properties of that node (the *_init functions copy
      prim%optProps and prim%layer) and ignores its own transform (the reference sets it to the
      identity and never applies it). Models and modifiers nest at most 32 levels deep. */
-  SMCRT_SDF_REVOLUTION = 12, /* param[0]=o, param[1..3]=center: q = (|(p-c).xz| - o, (p-c).y, 0)   :286-303 */
-  SMCRT_SDF_EXTRUDE = 13,    /* param[0]=h: w = (d(p), |p.z| - h); min(max(w),0) + |max(w,0)|    :268-284 */
-  SMCRT_SDF_ONION = 14,      /* param[0]=thickness: |d(p)| - thickness                          :305-315 */
-  SMCRT_SDF_TWIST = 15,      /* param[0]=k: d of p rotated by k*p.z in the xy plane              :334-352
+  SMCRT_SDF_REVOLUTION = 12, /* param[0]=o, param[1..3]=center: q = (|(p-c).xz| - o, (p-c).y, 0)   :303-321 */
+  SMCRT_SDF_EXTRUDE = 13,    /* param[0]=h: w = (d(p), |p.z| - h); min(max(w),0) + |max(w,0)|    :286-301 */
+  SMCRT_SDF_ONION = 14,      /* param[0]=thickness: |d(p)| - thickness                          :323-333 */
+  SMCRT_SDF_TWIST = 15,      /* param[0]=k: d of p rotated by k*p.z in the xy plane              :353-371
                                 (twist_init takes k as default real: pass real(k_sp, wp))      */
-  SMCRT_SDF_BEND = 16,       /* param[0]=k: d of p rotated by k*p.x in the xy plane              :354-372 */
-  SMCRT_SDF_ELONGATE = 17,   /* param[0..2]=size: q = |p| - size; d(max(q,0)) + min(max(q),0)     :317-332 */
-  SMCRT_SDF_DISPLACEMENT = 18 /* d(p) + f(p) with a built-in f (param[0] = smcrt_displacement_fn):  :374-388
+  SMCRT_SDF_BEND = 16,       /* param[0]=k: d of p rotated by k*p.x in the xy plane              :373-391 */
+  SMCRT_SDF_ELONGATE = 17,   /* param[0..2]=size: q = |p| - size; d(max(q,0)) + min(max(q),0)     :335-351 */
+  SMCRT_SDF_DISPLACEMENT = 18 /* d(p) + f(p) with a built-in f (param[0] = smcrt_displacement_fn):  :393-408
                                 the reference takes any pure function of pos and ships none    */
 } smcrt_sdf_kind;
 
 /* Built-in displacement functions f(p) of SMCRT_SDF_DISPLACEMENT (param[0]); the reference's
  * displacement_init takes an arbitrary procedure(primitive) pointer, which cannot cross to
  * device code. The `repeat` modifier is not provided: its evaluate is an `error stop "Not
- * implmented"` in the reference (sdfModifiers.f90:390-408). */
+ * implmented"` in the reference (sdfModifiers.f90:410-426). */
 typedef enum smcrt_displacement_fn {
   SMCRT_DISP_SINE = 1 /* param[1]=amplitude a, param[2..4]=frequencies (fx, fy, fz):
                          f(p) = ((a * sin(fx*p.x)) * sin(fy*p.y)) * sin(fz*p.z) */
@@ -614,9 +614,10 @@ int smcrt_write_checkpoint(const char* filename, const char* toml_filename, int6
  * messages. It builds the scene the way setup_simulation does and keeps the output and
  * simulation settings.
  *   Geometries: sphere, box, test_box, scat_test, scat_test2, aptran, sphere_scene, exp, omg,
- *     egg (ABI 4: revolution modifiers). vessels (needs data files the reference does not ship)
- *     and logo (the reference stops on it, setupGeometry.f90:326-328) return
- *     SMCRT_ERR_UNSUPPORTED.
+ *     egg (ABI 4: revolution modifiers), vessels (get_vessels, setupGeometry.f90:552-652:
+ *     edges.dat, nodes.dat and radii.dat are read from the input file's directory, the
+ *     reference's res/; a missing file is SMCRT_ERR_INVALID_ARG naming it). logo (the
+ *     reference stops on it, setupGeometry.f90:326-328) returns SMCRT_ERR_UNSUPPORTED.
  *   Sources: point, uniform, pencil; a constant spectrum.
  *   Detectors: circle, annulus, camera, grouped by type as parse_detectors does.
  * Build-defined: sphere_scene's sphere list, which the reference draws from an unseeded

@@ -327,32 +327,32 @@ static double sdf_eval_node(const scene_t* S, int32_t idx, vec3 pos, int depth) 
     if (depth >= ORACLE_MAX_NEST || nd->n_children != 1) return NAN;
     const int32_t ch = nd->first_child;
     switch (nd->kind) {
-      case SMCRT_SDF_REVOLUTION: {                                       /* eval_revolution :286-303 */
+      case SMCRT_SDF_REVOLUTION: {                                       /* eval_revolution :303-321 */
         vec3 pin = vsub(pos, v3(P[1], P[2], P[3]));
         vec3 pxz = v3(pin.x, 0.0, pin.z);
         return sdf_eval_node(S, ch, v3(vlen(pxz) - P[0], pin.y, 0.0), depth + 1);
       }
-      case SMCRT_SDF_EXTRUDE: {                                          /* eval_extrude :268-284 */
+      case SMCRT_SDF_EXTRUDE: {                                          /* eval_extrude :286-301 */
         double d = sdf_eval_node(S, ch, pos, depth + 1);
         vec3 w = v3(d, fabs(pos.z) - P[0], 0.0);
         return fmind(fmaxd(w.x, w.y), 0.0) + vlen(vmaxs(w, 0.0));
       }
-      case SMCRT_SDF_ONION:                                              /* eval_onion :305-315 */
+      case SMCRT_SDF_ONION:                                              /* eval_onion :323-333 */
         return fabs(sdf_eval_node(S, ch, pos, depth + 1)) - P[0];
-      case SMCRT_SDF_ELONGATE: {                                         /* eval_elongate :317-332 */
+      case SMCRT_SDF_ELONGATE: {                                         /* eval_elongate :335-351 */
         vec3 q = vsub(vabs(pos), v3(P[0], P[1], P[2]));
         double w = fmind(fmaxd(q.x, fmaxd(q.y, q.z)), 0.0);
         return sdf_eval_node(S, ch, vmaxs(q, 0.0), depth + 1) + w;
       }
-      case SMCRT_SDF_TWIST:                                              /* eval_twist :334-352 */
-      case SMCRT_SDF_BEND: {                                             /* eval_bend :354-372 */
+      case SMCRT_SDF_TWIST:                                              /* eval_twist :353-371 */
+      case SMCRT_SDF_BEND: {                                             /* eval_bend :373-391 */
         double s, c;
         oracle_sincos_any(P[0] * (nd->kind == SMCRT_SDF_TWIST ? pos.z : pos.x), &s, &c);
         double x2 = c * pos.x - s * pos.y;
         double y2 = s * pos.x + c * pos.y;
         return sdf_eval_node(S, ch, v3(x2, y2, pos.z), depth + 1);
       }
-      case SMCRT_SDF_DISPLACEMENT: {                                     /* eval_disp :374-388, built-in f */
+      case SMCRT_SDF_DISPLACEMENT: {                                     /* eval_disp :393-408, built-in f */
         double d1 = sdf_eval_node(S, ch, pos, depth + 1);
         double sx, sy, sz, c;
         oracle_sincos_any(P[2] * pos.x, &sx, &c);

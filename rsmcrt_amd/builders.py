@@ -126,6 +126,33 @@ def setup_omg_sdf() -> Scene:
                   box((2.0, 2.0, 2.0), opt2, 2)])
 
 
+def get_vessels(edges, nodes, radii) -> Scene:
+    """setupGeometry.f90:552-652 (geom_name='vessels') from the values its reads leave:
+    `edges` (E, 2) 1-based node indices, `nodes` (N, 3) and `radii` (N,). Rows of `nodes` the
+    reference never reads (its node loop runs to the edge count, :615) are passed as 0.0, the
+    value the C++ front end and the Fortran glue give them (the reference leaves them
+    undefined). Rescaling as :629-639 in the same operation order, res = 0.001; one capsule
+    per edge with the radius of its first node (vessel optics, layer 1), then the dermis box
+    .32 x .18 x .26 (layer 2)."""
+    import numpy as np
+    edges = np.asarray(edges, dtype=np.int64).reshape(-1, 2)
+    nodes = np.array(nodes, dtype=np.float64).reshape(-1, 3)
+    radii = np.asarray(radii, dtype=np.float64).reshape(-1)
+    res = 0.001
+    opt_v = mono(94.0, 231.0, 0.9, 1.37)
+    opt_d = mono(357.0, 0.458, 0.9, 1.37)
+    mx = np.abs(nodes).max(axis=0)
+    nodes = nodes / mx - 0.5
+    nodes = nodes * mx * res
+    sdfs = []
+    for e1, e2 in edges:
+        a = tuple(float(v) for v in nodes[e1 - 1])
+        b = tuple(float(v) for v in nodes[e2 - 1])
+        sdfs.append(capsule(a, b, float(radii[e1 - 1] * res), opt_v, 1))
+    sdfs.append(box((.32, .18, .26), opt_d, 2))
+    return Scene(sdfs)
+
+
 def synthetic_vessels(n_capsules: int = 512, seed: int = 2025, extent=(0.32, 0.18, 0.26)):
     """Build-defined stand-in for get_vessels (setupGeometry.f90:552-652), whose data files
     res/{edges,nodes,radii}.dat are not in the reference: a random tree of capsules with

@@ -205,8 +205,8 @@ __host__ __device__ __forceinline__ void det_sincos(double x, double* s, double*
   }
 }
 
-// sin and cos of any angle of the twist and bend modifiers (k * p, sdfModifiers.f90:341-342,
-// :361-362): sin(-x) = -sin(x), cos(-x) = cos(x), then det_sincos's reduction, whose
+// sin and cos of any angle of the twist and bend modifiers (k * p, sdfModifiers.f90:363-364,
+// :383-384): sin(-x) = -sin(x), cos(-x) = cos(x), then det_sincos's reduction, whose
 // fn * pio2_1 stays exact while |x| < 2^19 pi/2 (larger angles stay deterministic, with less
 // accuracy). The oracle restates it (oracle_sincos_any).
 __host__ __device__ __forceinline__ void det_sincos_any(double x, double* s, double* c) {

@@ -257,6 +257,157 @@ std::vector<double> loadtxt(const std::string& path, bool single, int64_t& rows,
   return out;
 }
 
+// Fortran list-directed input (`read(u, *, iostat=io) a, b, ...`) over one text file, enough of
+// it for get_vessels' three files. Each read statement starts at the next record (line) and
+// takes its values from as many records as it needs; the rest of its last record is skipped.
+// Values are separated by blanks or one comma; `r*c` repeats c r times; `/` ends the
+// statement (the items left keep their values). A read that hits the end of the file, or a
+// value that does not convert (e.g. "1.5" into an integer), is a failed read (iostat /= 0).
+class ListReader {
+ public:
+  explicit ListReader(const std::string& path) {
+    std::ifstream f(path);
+    ok_ = (bool)f;
+    std::string line;
+    while (std::getline(f, line)) lines_.push_back(line);
+  }
+  bool is_open() const { return ok_; }
+  // One read statement of n items; true when all n items were read (or a '/' ended it).
+  bool read_ints(int64_t* out, int n) { return read_items(n, [&](int i, const std::string& s) { return to_int(s, out[i]); }); }
+  bool read_reals(double* out, int n) { return read_items(n, [&](int i, const std::string& s) { return to_real(s, out[i]); }); }
+
+ private:
+  std::vector<std::string> lines_;
+  size_t rec_ = 0;
+  bool ok_ = false;
+
+  template <class Put>
+  bool read_items(int n, Put put) {
+    int item = 0;
+    while (item < n) {
+      if (rec_ >= lines_.size()) return false;  // end of file
+      const std::string& ln = lines_[rec_++];
+      size_t p = 0;
+      while (item < n) {
+        while (p < ln.size() && (ln[p] == ' ' || ln[p] == '\t' || ln[p] == '\r')) ++p;
+        if (p >= ln.size()) break;  // next record
+        if (ln[p] == '/') return true;
+        if (ln[p] == ',') { ++item; ++p; continue; }  // a null value: the item keeps its value
+        size_t q = p;
+        while (q < ln.size() && ln[q] != ' ' && ln[q] != '\t' && ln[q] != ',' && ln[q] != '/' && ln[q] != '\r') ++q;
+        std::string tok = ln.substr(p, q - p);
+        p = q;
+        while (p < ln.size() && (ln[p] == ' ' || ln[p] == '\t' || ln[p] == '\r')) ++p;
+        if (p < ln.size() && ln[p] == ',') ++p;  // the separator after a value
+        int64_t rep = 1;
+        const size_t star = tok.find('*');
+        if (star != std::string::npos) {
+          if (!to_int(tok.substr(0, star), rep) || rep < 1) return false;
+          tok = tok.substr(star + 1);
+        }
+        for (int64_t r = 0; r < rep && item < n; ++r, ++item)
+          if (!tok.empty() && !put(item, tok)) return false;
+      }
+    }
+    return true;
+  }
+  static bool to_int(const std::string& s, int64_t& v) {
+    if (s.empty()) return false;
+    char* end = nullptr;
+    const long long x = std::strtoll(s.c_str(), &end, 10);
+    if (*end != '\0') return false;
+    v = (int64_t)x;
+    return true;
+  }
+  static bool to_real(std::string s, double& v) {
+    for (char& c : s)
+      if (c == 'd' || c == 'D' || c == 'q' || c == 'Q') c = 'e';  // Fortran exponent letters
+    if (s.empty()) return false;
+    char* end = nullptr;
+    v = std::strtod(s.c_str(), &end);
+    return *end == '\0';
+  }
+};
+
+// get_vessels, setupGeometry.f90:552-652: a vessel net read from edges.dat (pairs of 1-based
+// node indices), nodes.dat (x y z per node) and radii.dat (one radius per node), next to the
+// input file (the reference opens res/<name>.dat). Capsules (vessel optics, layer 1) per edge,
+// then the .32 x .18 x .26 dermis box (layer 2). Kept from the reference:
+//  * the counts are the number of successful reads (:585-602); reading stops at the first
+//    failed read in each loop (:605-627);
+//  * nodes.dat is read with the EDGE count as the loop bound (:615), so with fewer edges than
+//    nodes (a tree has E = N - 1) the last rows are never read. The reference leaves them as
+//    allocate found them (undefined); here they are 0.0, which is also what the Fortran glue
+//    sets (bindings/fortran/smcrt_glue.f90 smcrt_get_vessels);
+//  * the rescaling (:629-639) in the reference's operation order, res = 0.001.
+// Refused (INVALID_ARG): a missing file, no edges, an edge index outside 1..node count (an
+// out-of-bounds access in the reference), max|x|, max|y| or max|z| = 0 (a division by zero).
+std::vector<Prim> get_vessels(const std::string& resdir) {
+  const Mono ov{94.0, 231.0, 0.9, 1.37};  // musv, muav, gv, nv (:572-575)
+  const Mono od{357.0, 0.458, 0.9, 1.37};  // musd, muad, gd, nd (:577-580)
+  auto open = [&](const char* name) {
+    ListReader r(resdir + "/" + name);
+    if (!r.is_open())
+      throw Fail(SMCRT_ERR_INVALID_ARG, std::string("vessels: cannot read ") + resdir + "/" + name +
+                                            " (get_vessels reads res/edges.dat, nodes.dat and radii.dat)");
+    return r;
+  };
+  int64_t edge_cnt = 0, node_cnt = 0;
+  {
+    ListReader r = open("edges.dat");
+    int64_t t[2];
+    while (r.read_ints(t, 2)) ++edge_cnt;
+  }
+  {
+    ListReader r = open("nodes.dat");
+    double t[3];
+    while (r.read_reals(t, 3)) ++node_cnt;
+  }
+  if (edge_cnt == 0) throw Fail(SMCRT_ERR_INVALID_ARG, "vessels: edges.dat holds no edge");
+  std::vector<int64_t> edges((size_t)(2 * edge_cnt), 0);
+  std::vector<double> nodes((size_t)(3 * node_cnt), 0.0), radii((size_t)node_cnt, 0.0);
+  {
+    ListReader r = open("edges.dat");
+    for (int64_t i = 0; i < edge_cnt; ++i)
+      if (!r.read_ints(&edges[(size_t)(2 * i)], 2)) break;
+  }
+  {
+    ListReader r = open("nodes.dat");
+    for (int64_t i = 0; i < edge_cnt && i < node_cnt; ++i)  // :615 loops to edge_cnt
+      if (!r.read_reals(&nodes[(size_t)(3 * i)], 3)) break;
+  }
+  {
+    ListReader r = open("radii.dat");
+    for (int64_t i = 0; i < node_cnt; ++i)
+      if (!r.read_reals(&radii[(size_t)i], 1)) break;
+  }
+  const double res = 0.001;
+  double mx[3] = {0.0, 0.0, 0.0};
+  for (int64_t i = 0; i < node_cnt; ++i)
+    for (int k = 0; k < 3; ++k) mx[k] = std::max(mx[k], std::fabs(nodes[(size_t)(3 * i + k)]));
+  for (int k = 0; k < 3; ++k)
+    if (!(mx[k] > 0.0)) throw Fail(SMCRT_ERR_INVALID_ARG, "vessels: nodes.dat has max|coordinate| = 0 on an axis");
+  for (int64_t i = 0; i < node_cnt; ++i)
+    for (int k = 0; k < 3; ++k) {
+      double& v = nodes[(size_t)(3 * i + k)];
+      v = (v / mx[k]) - 0.5;  // :634-636
+      v = v * mx[k] * res;    // :637-639, (v*max)*res
+    }
+  std::vector<Prim> a;
+  for (int64_t i = 0; i < edge_cnt; ++i) {
+    const int64_t e1 = edges[(size_t)(2 * i)], e2 = edges[(size_t)(2 * i + 1)];
+    if (e1 < 1 || e1 > node_cnt || e2 < 1 || e2 > node_cnt)
+      throw Fail(SMCRT_ERR_INVALID_ARG, "vessels: edge " + std::to_string(i + 1) + " names a node outside 1.." +
+                                            std::to_string(node_cnt));
+    const double* pa = &nodes[(size_t)(3 * (e1 - 1))];
+    const double* pb = &nodes[(size_t)(3 * (e2 - 1))];
+    const double radius = radii[(size_t)(e1 - 1)] * res;  // :646
+    a.push_back(prim(SMCRT_SDF_CAPSULE, {pa[0], pa[1], pa[2], pb[0], pb[1], pb[2], radius}, ov, 1));
+  }
+  a.push_back(box(.32, .18, .26, od, 2));  // :650
+  return a;
+}
+
 // parse_spectrum, parse_spectrum.f90:17-118. Files are read relative to the input file's
 // directory (the reference's res/: "res/"//sfile for 1-D, resdir//sfile for 2-D).
 void parse_spectrum(smcrt_job& J, const Table* s) {
@@ -534,11 +685,14 @@ std::vector<Prim> setup_geometry(smcrt_job& J, const Table* root) {  // parse_ge
       m.children.push_back(cylinder(seg[i], seg[i] + 3, 0.05, o1, 1, i == 0 ? invert(rotate_y(90.0)) : identity()));
     a.push_back(m);
     a.push_back(box(2.0, 2.0, 2.0, zero, 2));
-  } else if (e == "vessels") {  // :552-652 reads res/{edges,nodes,radii}.dat, absent from the reference
-    throw Fail(SMCRT_ERR_UNSUPPORTED, "vessels needs res/edges.dat, nodes.dat and radii.dat, which the reference does not ship");
+  } else if (e == "vessels") {  // get_vessels, :552-652 (data files next to the input file)
+    std::string resdir = J.toml_path;
+    const size_t slash = resdir.find_last_of('/');
+    resdir = slash == std::string::npos ? std::string(".") : resdir.substr(0, slash);
+    a = get_vessels(resdir);
   } else if (e == "egg") {  // setup_egg, setupGeometry.f90:149-248: yolk, albumen, shell, bounding box
     const double bot = egg_p[0], topr = egg_p[1], sep = egg_p[2], shell_t = egg_p[3], yolk_r = egg_p[4];
-    auto revolve = [&](Prim inner) {  // revolution(egg, 0, center = pos), sdfModifiers.f90:232-259
+    auto revolve = [&](Prim inner) {  // revolution(egg, 0, center = pos), sdfModifiers.f90:238-266 (eval :303-321)
       Prim m;
       m.kind = SMCRT_SDF_REVOLUTION;
       m.param = {0.0, pos[0], pos[1], pos[2]};

@@ -194,8 +194,8 @@ struct ProgOp {
 // Models and modifiers ("composite" nodes, every kind from SMCRT_SDF_MODEL on).
 __host__ __device__ __forceinline__ bool composite_kind(int32_t kind) { return kind >= SMCRT_SDF_MODEL; }
 
-// A modifier's query point for its wrapped node (sdfModifiers.f90). Revolution :286-303,
-// elongate :317-332 (max(q, 0)), twist :334-352, bend :354-372; the others pass pos through.
+// A modifier's query point for its wrapped node (sdfModifiers.f90). Revolution :303-321,
+// elongate :335-351 (max(q, 0)), twist :353-371, bend :373-391; the others pass pos through.
 __host__ __device__ __forceinline__ V3 modifier_point(const smcrt_sdf_node* __restrict__ M, V3 pos) {
   const double* P = M->param;
   switch (M->kind) {
@@ -219,7 +219,7 @@ __host__ __device__ __forceinline__ V3 modifier_point(const smcrt_sdf_node* __re
 }
 
 // A modifier's value from its wrapped node's value d at its own query point pos.
-// Extrude :268-284, onion :305-315, elongate :317-332 (+ w), displacement :374-388.
+// Extrude :286-301, onion :323-333, elongate :335-351 (+ w), displacement :393-408.
 __host__ __device__ __forceinline__ double modifier_value(const smcrt_sdf_node* __restrict__ M, double d, V3 pos) {
   const double* P = M->param;
   switch (M->kind) {

@@ -236,7 +236,7 @@ class Modifier:
 
 
 def revolution(prim, o, center=(0.0, 0.0, 0.0)) -> Modifier:
-    """revolution_init(prim, o, center) sdfModifiers.f90:232-259."""
+    """revolution_init(prim, o, center) sdfModifiers.f90:238-266."""
     return Modifier(abi.SDF_REVOLUTION, prim, [float(o), *map(float, center)])
 
 
@@ -246,7 +246,7 @@ def extrude(prim, h) -> Modifier:
 
 
 def onion(prim, thickness) -> Modifier:
-    """onion_init(prim, thickness) :261-277."""
+    """onion_init(prim, thickness) :268-284."""
     return Modifier(abi.SDF_ONION, prim, [float(thickness)])
 
 

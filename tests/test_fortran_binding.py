@@ -163,10 +163,16 @@ def test_glue_tables_match_the_toml_front_end(lib_path, tmp_path):
     subprocess.run([FC, "-O2", "-c", "smcrt_glue.f90"], cwd=tmp_path, check=True)
     subprocess.run([FC, "-O2", "-o", "glue_scenes", "glue_scenes.f90", "smcrt_glue.o", "smcrt_mod.o",
                     f"-L{libdir}", "-lsmcrt", f"-Wl,-rpath,{libdir}"], cwd=tmp_path, check=True)
-    subprocess.run([str(tmp_path / "glue_scenes"), str(tmp_path)], check=True)
-    for name in GLUE_SCENES:
+    # get_vessels' data (tests/golden/make_vessel_data.py): the glue reads it with the Fortran
+    # runtime's list-directed reads, the front end with its own reader
+    from tests.golden.make_vessel_data import write_vessel_data
+    vdir = tmp_path / "vessels"
+    write_vessel_data(vdir, 40, 7)
+    subprocess.run([str(tmp_path / "glue_scenes"), str(tmp_path), str(vdir)], check=True)
+    for name in GLUE_SCENES + ("vessels",):
         n_nodes, top, nodes, dets, src = _read_glue(tmp_path / f"{name}.bin")
-        j = Job(os.path.join(ROOT, "tests", "golden", "res", f"{name}.toml"))
+        j = Job(str(vdir / "vessels.toml") if name == "vessels" else
+                os.path.join(ROOT, "tests", "golden", "res", f"{name}.toml"))
         d = j.desc
         assert n_nodes == d.n_nodes and len(top) == d.n_top and len(dets) == d.n_dets, name
         assert top == list(j.top[:d.n_top]), name

@@ -118,9 +118,87 @@ def test_egg_revolution_modifiers():
     assert meta["BottomSphereRadius"] == "2.0" and meta["ShellThickness"] == "0.02" and meta["YolkRadius"] == "1.0"
 
 
+def _vessel_case(tmp_path, n_nodes, extra_edges, seed=7):
+    from tests.golden.make_vessel_data import write_vessel_data
+    edges, nodes, radii = write_vessel_data(tmp_path, n_nodes, seed, extra_edges)
+    read = np.zeros_like(nodes)
+    n_read = min(len(edges), len(nodes))  # setupGeometry.f90:615 loops to the edge count
+    read[:n_read] = nodes[:n_read]
+    return Job(str(tmp_path / "vessels.toml")), builders.get_vessels(edges, read, radii), edges, nodes
+
+
+@pytest.mark.parametrize("extra_edges", [0, 9])
+def test_vessels_get_vessels(tmp_path, extra_edges):
+    """res/vessels.toml with a data set beside it (tests/golden/make_vessel_data.py): get_vessels
+    (setupGeometry.f90:552-652) gives one capsule per edge plus the .32 x .18 x .26 dermis box,
+    node for node equal to builders.get_vessels on the values the reference's reads leave. A
+    tree (E = N - 1) leaves the last node unread (the :615 bound); with extra edges every node
+    is read. The file mixes blank and comma separators, d exponents and a record split."""
+    j, sc, edges, nodes = _vessel_case(tmp_path, 40, extra_edges)
+    same_scene(j, sc)
+    assert j.experiment == "vessels" and j.desc.n_top == len(edges) + 1
+    caps = [j.nodes[i] for i in range(len(edges))]
+    assert all(c.kind == abi.SDF_CAPSULE and c.layer == 1 and (c.mus, c.mua, c.hgg, c.n) == (94.0, 231.0, 0.9, 1.37)
+               for c in caps)
+    bx = j.nodes[len(edges)]
+    assert bx.kind == abi.SDF_BOX and bx.layer == 2 and list(bx.param[:3]) == [0.16, 0.09, 0.13]
+    assert (bx.mus, bx.mua) == (357.0, 0.458)
+    # the rescale of :629-639, checked on one capsule end by hand
+    mx = np.abs(nodes[:min(len(edges), len(nodes))]).max(axis=0)
+    e1 = int(edges[0][0]) - 1
+    want = [(nodes[e1][k] / mx[k] - 0.5) * mx[k] * 0.001 if e1 < len(edges) else -0.5 * mx[k] * 0.001
+            for k in range(3)]
+    assert list(caps[0].param[:3]) == want
+    s = j.desc.source
+    assert s.kind == abi.SRC_UNIFORM and list(s.dir) == [0.0, 0.0, -1.0] and list(s.p1) == [-0.16, -0.09, 0.129999]
+    if extra_edges == 0:  # the unread last node sits at -max/2 * res on every axis
+        last = len(nodes) - 1
+        ends = [c for c, (a, b) in zip(caps, edges) if b - 1 == last]
+        assert ends and list(ends[0].param[3:6]) == [-0.5 * mx[k] * 0.001 for k in range(3)]
+
+
+def test_vessels_missing_or_bad_data(tmp_path):
+    """Without the data files the front end names the file it could not read; a bad edge
+    index (an out-of-bounds read in the reference) is refused."""
+    with pytest.raises(SmcrtError) as e:
+        Job(res("vessels.toml"))
+    assert abi.STATUS_NAMES[abi.ERR_INVALID_ARG] in str(e.value) and "edges.dat" in str(e.value)
+    from tests.golden.make_vessel_data import write_vessel_data
+    write_vessel_data(tmp_path, 10, 3)
+    with open(tmp_path / "edges.dat", "a") as f:
+        f.write("1 11\n")
+    with pytest.raises(SmcrtError, match="outside 1..10"):
+        Job(str(tmp_path / "vessels.toml"))
+    (tmp_path / "radii.dat").unlink()
+    with pytest.raises(SmcrtError, match="radii.dat"):
+        Job(str(tmp_path / "vessels.toml"))
+
+
+@pytest.mark.gpu
+def test_vessels_job_runs_bit_exact(tmp_path):
+    """The vessels scene get_vessels builds, run through the HIP engine at 64^3 with
+    res/vessels.toml's uniform source, bit-exact against the oracle."""
+    from oracle import pyoracle as O
+    from rsmcrt_amd.engine import Engine
+    j, _, _, _ = _vessel_case(tmp_path, 40, 0)
+    d = j.desc
+    sc = scene.Scene([])
+    sc.nodes = [j.nodes[i] for i in range(d.n_nodes)]
+    sc.top = list(j.top[:d.n_top])
+    g = scene.grid(64, 64, 64, d.grid.xmax, d.grid.ymax, d.grid.zmax)
+    n = 3000
+    with Engine(sc, g) as eng:
+        gpu = eng.run(d.source, n, seed=d.seed, records=True)
+    cpu = O.run(sc, g, d.source, n, seed=d.seed, records=True)
+    assert gpu.counters_dict() == cpu.counters_dict()
+    assert np.array_equal(gpu.records, cpu.records)
+    assert np.array_equal(gpu.absorb, cpu.absorb)
+    np.testing.assert_allclose(gpu.jmean, cpu.jmean, rtol=1e-12, atol=1e-15)
+    assert cpu.counter("absorbed") > 0
+
+
 @pytest.mark.parametrize("name,code,why", [
     ("logo.toml", abi.ERR_UNSUPPORTED, "svg"),
-    ("vessels.toml", abi.ERR_UNSUPPORTED, "edges.dat"),
     # resdir//"test/parse/test.png" does not exist under res/ (parse_spectrum.f90:87-92)
     ("test_spectra_2D.toml", abi.ERR_INVALID_ARG, "Error reading file"),
     # rejected by the reference itself:

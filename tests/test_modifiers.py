@@ -83,7 +83,7 @@ def test_twist_and_bend_of_axis_symmetric_shapes(k):
 
 
 def test_twist_stores_a_single_precision_k():
-    """twist_init takes k as a default real (sdfModifiers.f90:130): 0.1 becomes float32(0.1)."""
+    """twist_init takes k as a default real (sdfModifiers.f90:131): 0.1 becomes float32(0.1)."""
     t = Scene([scene.twist(sphere(1.0, OPT, 1), 0.1)])
     assert t.nodes[0].param[0] == f32(0.1) != 0.1
 
@@ -99,7 +99,7 @@ def test_onion_extrude_elongate_closed_forms():
         want = min(max(d, wy), 0.0) + math.sqrt(max(d, 0.0) ** 2 + max(wy, 0.0) ** 2)
         assert abs(val(scene.extrude(s, 0.5), p) - want) <= 8 * EPS
         # elongate a sphere along x by 0.5: a capsule of radius 1 from x = -0.5 to 0.5 where
-        # the elongation is outside; inside, min(max(q), 0) is added (sdfModifiers.f90:327-330)
+        # the elongation is outside; inside, min(max(q), 0) is added (sdfModifiers.f90:346-349)
         q = np.abs(p) - np.array([0.5, 0.0, 0.0])
         w = min(max(q[0], max(q[1], q[2])), 0.0)
         qm = np.maximum(q, 0.0)
