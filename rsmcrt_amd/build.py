@@ -20,7 +20,10 @@ ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libsmcrt.so")
 OBJDIR = os.path.join(PKG, ".objs")
 SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp", "multi.hip", "cull.cpp")]
-DEPS = SOURCES + sorted(glob.glob(os.path.join(PKG, "csrc", "*.h"))) + [os.path.join(ROOT, "include", "smcrt.h")]
+# the transport kernel instantiations: kinst.hip once per (LDS faces, grid mode), kernel_ptrs.h
+KINST = os.path.join(PKG, "csrc", "kinst.hip")
+UNITS = [(src, ()) for src in SOURCES] + [(KINST, (f"-DKI_F={f}", f"-DKI_G={g}")) for f in (0, 1) for g in (0, 1, 2)]
+DEPS = SOURCES + [KINST] + sorted(glob.glob(os.path.join(PKG, "csrc", "*.h"))) + [os.path.join(ROOT, "include", "smcrt.h")]
 ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no fused multiply-add, so fp64 trajectories are bit-identical to the
 # CPU restatement (oracle/), which is compiled the same way.
@@ -49,8 +52,8 @@ def includes(path: str, seen=None) -> set:
     return seen
 
 
-def _obj(src: str, extra_flags=()) -> str:
-    tag = "" if not extra_flags else "." + str(abs(hash(tuple(extra_flags))) % 10**8)
+def _obj(src: str, defs=(), variant: str = "") -> str:
+    tag = "".join("." + d.lstrip("-D").replace("=", "") for d in defs) + ("." + variant if variant else "")
     return os.path.join(OBJDIR, os.path.basename(src) + tag + ".o")
 
 
@@ -68,30 +71,52 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return LIB
+def _compile_and_link(out: str, extra=(), variant: str = "", force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
-    objs = [_obj(src) for src in SOURCES]
-    todo = [i for i, src in enumerate(SOURCES) if force or _stale(objs[i], includes(src))]
+    objs = [_obj(src, defs, variant) for src, defs in UNITS]
+    todo = [i for i, (src, _) in enumerate(UNITS) if force or _stale(objs[i], includes(src))]
 
     def compile_one(i: int) -> None:
-        cmd = [hipcc(), *FLAGS, "-c", "-o", objs[i] + ".tmp", SOURCES[i]]
+        src, defs = UNITS[i]
+        cmd = [hipcc(), *FLAGS, *extra, *defs, "-c", "-o", objs[i] + ".tmp", src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         os.replace(objs[i] + ".tmp", objs[i])
 
-    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1)))
+    jobs = max(1, min(len(UNITS), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 1)))
+    # the largest units first (smcrt.hip and the transport instantiations)
+    todo.sort(key=lambda i: (UNITS[i][0] != KINST, not UNITS[i][0].endswith("smcrt.hip")))
     with ThreadPoolExecutor(jobs) as ex:
         list(ex.map(compile_one, todo))
-    cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", LIB + ".tmp", *objs, "-lz", "-ldl"]
+    cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp", *objs, "-lz", "-ldl"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(out + ".tmp", out)
+    return out
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    return _compile_and_link(LIB, force=force, verbose=verbose)
+
+
+def build_variant(name: str, flags: str, outdir: str = os.path.join(ROOT, "tools", "diag_libs"),
+                  verbose: bool = False) -> str:
+    """A compile-time variant of the library (extra -D flags) as outdir/libsmcrt_<name>.so, for
+    A/B and diagnostic runs; its objects are cached under .objs/ with the variant's name."""
+    os.makedirs(outdir, exist_ok=True)
+    return _compile_and_link(os.path.join(outdir, f"libsmcrt_{name}.so"), tuple(flags.split()), variant=name,
+                             verbose=verbose)
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python -m rsmcrt_amd.build [--force] | --variant NAME "FLAGS" [NAME2 "FLAGS2" ...]
+    if "--variant" in sys.argv:
+        a = sys.argv[sys.argv.index("--variant") + 1:]
+        for k in range(0, len(a) - 1, 2):
+            print(build_variant(a[k], a[k + 1], verbose=True))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -175,6 +175,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t* wsum, uin
   return before + x - v;
 }
 
+#ifdef SMCRT_FOLD_KERNELS  // (the fold kernels live in smcrt.hip's translation unit only)
 // ---- bin_hist: record counts per (tile, bin block) -------------------------------------
 __global__ __launch_bounds__(BIN_THREADS) void bin_hist(const unsigned long long* __restrict__ pool,
                                                         const uint32_t* __restrict__ chunk_fill,
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
     for (int k = 0; k < STAGE_PER_THREAD; ++k) v[k] = vn[k];
   }
 }
+#endif  // SMCRT_FOLD_KERNELS
 
 // =============================================================================================
 // Tile buckets: the transport kernel files each record straight into a bucket of its tile,
@@ -546,6 +548,7 @@ __device__ __forceinline__ void close_block_buckets(const KParams& K, const KCol
   }
 }
 
+#ifdef SMCRT_FOLD_KERNELS
 // ---- bk_scan: bucket offsets per tile and the reduce pieces (one block) --------------------
 // tile_nb[t] buckets of tile t -> tile_start[t] (exclusive scan), cursor[t] = tile_start[t];
 // pieces of at most `pb` buckets of one tile. dep_ctl[2] = pieces.
@@ -822,5 +825,6 @@ __global__ __launch_bounds__(1024) void bin_reduce(const unsigned long long* __r
     __syncthreads();
   }
 }
+#endif  // SMCRT_FOLD_KERNELS
 
 }  // namespace smcrt

@@ -1,0 +1,51 @@
+// kinst.hip — one (LDS faces, grid mode) slice of the transport kernel instantiations.
+// Compiled six times by build.py (-DKI_F=0/1 -DKI_G=0/1/2); see kernel_ptrs.h.
+#include "kernels.h"
+#include "kernel_ptrs.h"
+
+#if !defined(KI_F) || !defined(KI_G)
+#error "kinst.hip is compiled with -DKI_F=<0|1> -DKI_G=<0|1|2> (rsmcrt_amd/build.py)"
+#endif
+#define KI_NAME3(a, f, g) a##_##f##_##g
+#define KI_NAME2(a, f, g) KI_NAME3(a, f, g)
+#define KI_NAME(a) KI_NAME2(a, KI_F, KI_G)
+
+namespace smcrt {
+
+const void* KI_NAME(kinst_transport)(int xsrc, int coop) {
+  constexpr bool F = KI_F != 0;
+  if (xsrc && coop) {
+    if constexpr (!F) return (const void*)transport_kernel<false, KI_G, true, true>;
+    return nullptr;
+  }
+  if (xsrc) return (const void*)transport_kernel<F, KI_G, true, false>;
+  if (coop) return (const void*)transport_kernel<F, KI_G, false, true>;
+  return (const void*)transport_kernel<F, KI_G, false, false>;
+}
+
+#if KI_F == 0 && KI_G == 0
+size_t kinst_lean_shared_bytes() { return sizeof(LeanShared); }  // (one object defines it)
+#endif
+
+const void* KI_NAME(kinst_lean)() { return (const void*)lean_kernel<KI_F != 0, KI_G>; }
+
+void KI_NAME(kinst_diag)(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6) {
+#ifdef SMCRT_DIAG
+  unsigned long long h[72] = {0}, z[72] = {0};
+  if (hipDeviceSynchronize() != hipSuccess) return;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)) == hipSuccess)
+    for (int i = 0; i < 72; ++i) d72[i] += (i >= 68 && i <= 69) ? 0 : h[i];
+  for (int i = 68; i <= 69; ++i) d72[i] = h[i] > d72[i] ? h[i] : d72[i];  // the longest wave: a max
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag_t), sizeof(unsigned long long) * 9) == hipSuccess)
+    for (int i = 0; i < 9; ++i) t9[i] += h[i];
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_t), z, sizeof(unsigned long long) * 9);
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cull_diag), sizeof(unsigned long long) * 6) == hipSuccess)
+    for (int i = 0; i < 6; ++i) c6[i] += h[i];
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cull_diag), z, sizeof(unsigned long long) * 6);
+#else
+  (void)d72; (void)t9; (void)c6;
+#endif
+}
+
+}  // namespace smcrt

@@ -47,10 +47,7 @@
 #include "transport.h"
 #include "deposit.h"
 
-#ifdef SMCRT_DIAG
-extern __device__ unsigned long long g_diag[72];  // (defined in smcrt.hip)
-extern __device__ unsigned long long g_diag_t[9];
-#endif
+// (diagnostic builds: g_diag, g_diag_t are defined in kernels.h before this header)
 
 namespace smcrt {
 

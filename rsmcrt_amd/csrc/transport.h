@@ -1104,7 +1104,7 @@ struct FarCert {
 #ifdef SMCRT_DIAG
 // diagnostic builds: [0] culled lane-EVALs [1] bound-test fallbacks [2] capture/outside
 // fallbacks [3] list entries walked [4] wave-EVALs [5] wave-EVALs with a full fallback
-__device__ unsigned long long g_cull_diag[6];
+static __device__ unsigned long long g_cull_diag[6];
 #endif
 #ifndef SMCRT_CULL_PREFETCH
 #define SMCRT_CULL_PREFETCH 1
