@@ -25,10 +25,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# at least eight hardware queues for the scene's streams, set before torch starts the HIP
-# runtime (rsmcrt_amd/__init__.py explains; the boxes export HIP's default of 4)
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# at least eight (at most 32) hardware queues for the scene's streams, set before torch starts
+# the HIP runtime (rsmcrt_amd/__init__.py explains; the boxes export HIP's default of 4). The
+# package imports no torch, so this still runs first.
+from rsmcrt_amd import _raise_hw_queues  # noqa: E402
+
+_raise_hw_queues()
 
 WORKLOADS = ("m0", "m1", "m2", "m3", "m4", "m5", "escape")
 
@@ -188,6 +190,35 @@ def attach_cpu_leg(out, base, agree, rccl_ranks=None):
     out["parity"] = agree
     if rccl_ranks is not None:
         out["rccl_ranks"] = rccl_ranks
+    return out
+
+
+def rank_row(rank, photons, seconds, transport_s, reduce_ms):
+    """One rank's line of an N > 1 bench line's `ranks` breakdown: the photons it ran in the
+    timed region, its wall seconds (barrier to barrier), its transport seconds (HIP events on
+    its launch stream from the start of the timed region to the end of its last fold) and the
+    packed RCCL reduce's own time (HIP events around smcrt_reduce_device_tallies)."""
+    return {"rank": int(rank), "photons": int(photons), "seconds": float(seconds),
+            "transport_s": float(transport_s), "reduce_ms": float(reduce_ms),
+            "photons_per_s_transport": float(photons) / transport_s if transport_s > 0 else None}
+
+
+def attach_rank_breakdown(out, rows):
+    """Rank 0's summary of every rank's row (rank_row): the rows in rank order, the slowest
+    rank's transport time, the reduce's largest time and the spread of transport times, so a
+    non-linear scaling curve can be read from the line (transport imbalance vs collective
+    cost). The reference's intended reduce is mpi_reduce to rank 0 (kernelsMod.f90:2351-2357)."""
+    rows = sorted(rows, key=lambda r: r["rank"])
+    ts = [r["transport_s"] for r in rows]
+    out["ranks"] = rows
+    out["rank_summary"] = {
+        "photons_total": sum(r["photons"] for r in rows),
+        "transport_s_max": max(ts), "transport_s_min": min(ts),
+        "transport_imbalance": (max(ts) / min(ts) - 1.0) if min(ts) > 0 else None,
+        "slowest_rank": rows[ts.index(max(ts))]["rank"],
+        "reduce_ms_max": max(r["reduce_ms"] for r in rows),
+        "reduce_share_of_step_time": (max(r["reduce_ms"] for r in rows) * 1e-3 / max(r["seconds"] for r in rows)),
+    }
     return out
 
 
@@ -564,12 +595,18 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # HIP events on `stream` (torch's current stream, where the steps, the fence and the
+    # reduce are enqueued): start, end of the last fold, end of the reduce
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     t0 = time.perf_counter()
+    ev[0].record(stream)
     for s in range(args.warmup, args.warmup + args.steps):
         step(s)
     eng.fence(stream.cuda_stream)
+    ev[1].record(stream)
     if comm is not None:  # ONE packed RCCL all-reduce of every tally, inside libsmcrt
         eng.reduce_device_tallies(comm, dt_, root=-1, stream=stream.cuda_stream)
+    ev[2].record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -580,6 +617,11 @@ def main():
         dist.all_gather(per_rank, mine)
     per_rank_s = [float(x.item()) for x in per_rank]
     elapsed = max(per_rank_s)  # the max over ranks
+    rows = None
+    if world > 1:  # every rank's photons, transport time and reduce time (rank_row)
+        mine_row = rank_row(rank, args.steps * B, t1 - t0, ev[0].elapsed_time(ev[1]) * 1e-3, ev[1].elapsed_time(ev[2]))
+        rows = [None] * world
+        dist.all_gather_object(rows, mine_row)
     log(f"[bench] {args.workload}: {args.steps} timed steps in {elapsed:.2f} s")
     kt = eng.kernel_times()  # HIP events around each kernel group, on the launch stream
     eng.set_timing(False)
@@ -661,6 +703,8 @@ def main():
             "valu_roofline": valu_roofline(pmc, kern_ms),
             "cpu_baseline": None,
         }
+        if rows is not None:
+            attach_rank_breakdown(out, rows)
     if not args.no_cpu:
         threads = args.cpu_threads or cpu_threads()
         chunk = max(50, min(2000, B // 1000))
@@ -674,8 +718,9 @@ def main():
                 dist.broadcast_object_list(box, src=0)
                 return box[0]
 
-            def sharded(first, count):
-                return sharded_device_run(eng, comm, src, g, dets, run_flags, args.seed, first, count, stream, rank)
+            def sharded(first, count):  # (path-length deposition as the CPU leg, whatever the timed flags)
+                return sharded_device_run(eng, comm, src, g, dets, abi.FLAG_PATHLENGTH, args.seed, first, count,
+                                          stream, rank)
 
             base, agree = sharded_cpu_parity(
                 rank, world, lambda: cpu_run(sc, g, src, dets, args.cpu_seconds, threads, args.seed, chunk),

@@ -16,15 +16,28 @@ import os
 # takes effect if nothing has started the HIP runtime yet (C/Fortran callers export it
 # themselves).
 MIN_HW_QUEUES = 8
+MAX_HW_QUEUES = 32  # the GPU pool refuses more; HIP itself allows no more than the hardware has
 
 
-def _raise_hw_queues(env=os.environ, want=MIN_HW_QUEUES):
+def _raise_hw_queues(env=os.environ, want=MIN_HW_QUEUES, log=None):
+    """Set GPU_MAX_HW_QUEUES to at least `want` and at most MAX_HW_QUEUES. A value that does not
+    parse counts as unset; an explicit value that is changed is reported through `log` (stderr
+    by default). Returns the value left in env."""
+    raw = env.get("GPU_MAX_HW_QUEUES")
     try:
-        cur = int(env.get("GPU_MAX_HW_QUEUES", "0"))
+        cur = int(raw) if raw not in (None, "") else 0
     except ValueError:
         cur = 0
-    if cur < want:
-        env["GPU_MAX_HW_QUEUES"] = str(want)
+    new = min(max(cur, want), MAX_HW_QUEUES)
+    if raw is not None and raw != "" and str(new) != raw.strip():
+        msg = f"[rsmcrt_amd] GPU_MAX_HW_QUEUES={raw!r} -> {new} (at least {want}, at most {MAX_HW_QUEUES})"
+        if log is None:
+            import sys
+            print(msg, file=sys.stderr)
+        else:
+            log(msg)
+    env["GPU_MAX_HW_QUEUES"] = str(new)
+    return new
 
 
 _raise_hw_queues()

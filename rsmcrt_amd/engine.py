@@ -392,7 +392,9 @@ class MultiEngine:
         """One packed RCCL reduce of everything accumulated since the last collect."""
         res = result if result is not None else Result(self.grid, self.dets, 0)
         held = sum(self.device_photons())  # the library's own count of what the accumulators hold
-        assert held == self._pending, (held, self._pending)
+        if held != self._pending:  # (before any tally is reduced or normalised with it)
+            raise SmcrtError(f"multi-device photon count mismatch: the devices hold {held} photons, "
+                             f"{self._pending} were accumulated since the last collect")
         res.n_photons += held
         self._pending = 0
         t = res.tallies()

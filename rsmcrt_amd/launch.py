@@ -40,12 +40,23 @@ def free_port() -> int:
 KFD_NODES = "/sys/class/kfd/kfd/topology/nodes"
 
 
+def _can_open(path: str) -> bool:
+    try:
+        fd = os.open(path, os.O_RDWR | os.O_CLOEXEC)
+    except OSError:
+        return False
+    os.close(fd)
+    return True
+
+
 def _kfd_gpu_count():
     """GPU agents in the KFD topology (sysfs text files; nothing is opened under /dev), or
     None when the topology is not there. A node is a GPU when its simd_count is non-zero
-    (CPU nodes report 0) and this process may open its render node /dev/dri/renderD<minor>
-    (os.access only): a container sees the host's whole topology but only its own GPUs' render
-    nodes, which is the filter the HSA runtime applies too."""
+    (CPU nodes report 0) and this process can open its render node /dev/dri/renderD<minor>
+    read-write: a container sees the host's whole topology but only its own GPUs' render nodes,
+    which is the filter the HSA runtime applies too. The node is opened and closed at once
+    (os.access would check only the file mode, not the device cgroup's allow-list); opening a
+    DRM render node starts neither HSA nor HIP."""
     try:
         nodes = os.listdir(KFD_NODES)
     except OSError:
@@ -60,7 +71,7 @@ def _kfd_gpu_count():
         if int(props.get("simd_count", "0").strip() or 0) <= 0:
             continue
         minor = props.get("drm_render_minor", "").strip()
-        if minor and not os.access(f"/dev/dri/renderD{minor}", os.R_OK | os.W_OK):
+        if minor and not _can_open(f"/dev/dri/renderD{minor}"):
             continue
         n += 1
     return n

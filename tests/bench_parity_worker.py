@@ -50,8 +50,20 @@ def main():
 
         base, agree = bench.sharded_cpu_parity(
             rank, world, lambda: bench.cpu_run(sc, g, src, [], 1.0, 2, 123456789, 50), bcast, sharded)
+        # the N > 1 line's per-rank breakdown: this rank's shard timed, then the reduce timed
+        import time
+        t0 = time.perf_counter()
+        mine = O.run(sc, g, src, 200 * (rank + 1), first_photon=1000 * rank)
+        t1 = time.perf_counter()
+        tj = torch.from_numpy(mine.jmean.reshape(-1).copy())
+        dist.all_reduce(tj)
+        t2 = time.perf_counter()
+        row = bench.rank_row(rank, 200 * (rank + 1), t2 - t0, t1 - t0, (t2 - t1) * 1e3)
+        rows = [None] * world
+        dist.all_gather_object(rows, row)
         if rank == 0:
-            print(json.dumps(bench.attach_cpu_leg({"n_gpus": world}, base, agree, world)), flush=True)
+            out = bench.attach_cpu_leg({"n_gpus": world}, base, agree, world)
+            print(json.dumps(bench.attach_rank_breakdown(out, rows)), flush=True)
     finally:
         dist.destroy_process_group()
 

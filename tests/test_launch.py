@@ -76,7 +76,7 @@ def test_visible_gpus_from_kfd_topology(tmp_path, monkeypatch):
     amdsmi is an error, never a silent 0 or a HIP call."""
     from rsmcrt_amd import launch
     monkeypatch.setattr(launch, "KFD_NODES", _fake_kfd(tmp_path, [(0, 0), (1216, 128), (1216, 136), (1216, 999)]))
-    monkeypatch.setattr(launch.os, "access", lambda path, mode: not path.endswith("renderD999"))
+    monkeypatch.setattr(launch, "_can_open", lambda path: not path.endswith("renderD999"))
     for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         monkeypatch.delenv(v, raising=False)
     assert launch.visible_gpus() == 2  # (the CPU node and the inaccessible GPU are not counted)
@@ -117,9 +117,17 @@ import pytest  # noqa: E402
 
 @pytest.mark.gpu
 def test_launcher_parent_never_maps_kfd_on_gpu_box():
-    """The same check on the GPU box, where /dev/kfd exists and the count must be >= 1."""
+    """The same check on the GPU box, where /dev/kfd exists and the count must be >= 1, and the
+    launcher's count equals the GPUs this lease gives the process (HIP's count, taken in a
+    separate process after the launcher's)."""
     assert os.path.exists("/dev/kfd")
     test_launcher_parent_never_maps_kfd()
+    code = ("import sys; sys.path.insert(0, %r); from rsmcrt_amd import launch; print(launch.visible_gpus())" % ROOT)
+    n = int(subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                           check=True).stdout.split()[-1])
+    hip = int(subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                             capture_output=True, text=True, timeout=300, check=True).stdout.split()[-1])
+    assert n == hip, (n, hip)
 
 
 def test_bench_n_rank_cpu_leg_and_parity():
@@ -142,3 +150,10 @@ def test_bench_n_rank_cpu_leg_and_parity():
     assert par["counters_bit_exact_vs_cpu"] is True and par["photons_compared"] > 0
     assert par["jmean_max_rel_diff_vs_cpu"] < 1e-12 and "2 ranks" in par["gpu_side"]
     assert line["rccl_ranks"] == 2
+    # the per-rank breakdown (bench.rank_row / attach_rank_breakdown)
+    rows, summ = line["ranks"], line["rank_summary"]
+    assert [r["rank"] for r in rows] == [0, 1] and [r["photons"] for r in rows] == [200, 400]
+    assert all(r["seconds"] >= r["transport_s"] > 0 and r["reduce_ms"] >= 0 for r in rows)
+    assert summ["photons_total"] == 600 and summ["slowest_rank"] in (0, 1)
+    assert summ["transport_s_max"] >= summ["transport_s_min"] > 0 and summ["transport_imbalance"] >= 0
+    assert summ["reduce_ms_max"] == max(r["reduce_ms"] for r in rows) and 0 <= summ["reduce_share_of_step_time"] < 1

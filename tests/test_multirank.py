@@ -142,3 +142,33 @@ def test_gloo_world2_matches_single_rank(tmp_path):
     assert np.array_equal(got["absorb"], ref.absorb.reshape(-1))
     np.testing.assert_allclose(got["jmean"], ref.jmean.reshape(-1), rtol=1e-12, atol=0)
     assert got["nscatt"][0] == ref.nscatt[0]
+
+
+@pytest.mark.gpu
+def test_sharded_device_run_one_rank_comm():
+    """bench.sharded_device_run (the N > 1 bench line's GPU side of the parity check) on a
+    one-rank RCCL communicator: fresh device tallies, the rank's photons, the packed reduce onto
+    root 0 -- equal to eng.run of the same photons (counters and nscatt exact, jmean to fp64
+    fold order). The communicator reports one rank."""
+    import torch
+    import bench
+    from rsmcrt_amd import abi, builders, scene
+    from rsmcrt_amd.engine import Comm, Engine
+    torch.cuda.set_device(0)
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(32, 32, 32, 1.0, 1.0, 1.0)
+    src = scene.point_source()
+    comm = Comm(Comm.unique_id(), 1, 0, 0)
+    try:
+        assert comm.n_ranks == 1
+        with Engine(sc, g, device=0) as eng:
+            stream = torch.cuda.current_stream()
+            got = bench.sharded_device_run(eng, comm, src, g, [], abi.FLAG_PATHLENGTH, 123456789, 5000, 20000,
+                                           stream, 0)
+            want = eng.run(src, 20000, seed=123456789, first_photon=5000)
+    finally:
+        comm.close()
+    assert got.counters_dict() == want.counters_dict()
+    assert got.nscatt[0] == want.nscatt[0]
+    np.testing.assert_allclose(got.jmean, want.jmean, rtol=1e-12, atol=1e-15)
+    assert np.array_equal(got.absorb, want.absorb)
