@@ -10,10 +10,14 @@
 namespace smcrt {
 
 size_t kinst_lean_shared_bytes();  // sizeof(LeanShared), lean_kernel's static LDS
+size_t kinst_ws_shared_bytes();    // sizeof(WsShared), ws_kernel's static LDS
+int kinst_ws_threads();            // ws_kernel's block size
+int kinst_ws_photon_lanes();       // photon lanes per ws_kernel block
 
 #define SMCRT_KINST_DECL(F, G)                                                               \
   const void* kinst_transport_##F##_##G(int xsrc, int coop);                                 \
   const void* kinst_lean_##F##_##G();                                                        \
+  const void* kinst_ws_##F##_##G();                                                          \
   void kinst_diag_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6);
 SMCRT_KINST_DECL(0, 0)
 SMCRT_KINST_DECL(0, 1)
@@ -45,6 +49,16 @@ inline const void* lean_kernel_ptr(bool lds_faces, int gm) {
     case 3: return kinst_lean_1_0();
     case 4: return kinst_lean_1_1();
     default: return kinst_lean_1_2();
+  }
+}
+inline const void* ws_kernel_ptr(bool lds_faces, int gm) {
+  switch ((lds_faces ? 3 : 0) + gm) {
+    case 0: return kinst_ws_0_0();
+    case 1: return kinst_ws_0_1();
+    case 2: return kinst_ws_0_2();
+    case 3: return kinst_ws_1_0();
+    case 4: return kinst_ws_1_1();
+    default: return kinst_ws_1_2();
   }
 }
 // diagnostic builds: the kernels' tallies summed over the objects (each is cleared)

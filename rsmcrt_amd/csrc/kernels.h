@@ -36,6 +36,7 @@ static __device__ unsigned long long g_diag_t[9];
 #endif
 
 #include "lean.h"
+#include "ws.h"
 #include "far.h"
 
 // The query point of each EVAL state (the exact expressions of the reference).

@@ -25,7 +25,12 @@ const void* KI_NAME(kinst_transport)(int xsrc, int coop) {
 
 #if KI_F == 0 && KI_G == 0
 size_t kinst_lean_shared_bytes() { return sizeof(LeanShared); }  // (one object defines it)
+size_t kinst_ws_shared_bytes() { return sizeof(WsShared); }
+int kinst_ws_threads() { return WS_THREADS; }
+int kinst_ws_photon_lanes() { return (int)WS_NPL; }
 #endif
+
+const void* KI_NAME(kinst_ws)() { return (const void*)ws_kernel<KI_F != 0, KI_G>; }
 
 const void* KI_NAME(kinst_lean)() { return (const void*)lean_kernel<KI_F != 0, KI_G>; }
 

@@ -141,6 +141,9 @@ struct smcrt_scene {
   int grid_blocks = 0;
   int grid_blocks_x = 0;  // the XSRC (general emitter) instantiation
   int grid_blocks_lean = 0;  // lean_kernel (lean.h)
+  int grid_blocks_ws = 0;    // ws_kernel (ws.h): the lean path with photon and walker waves
+  // the lean path runs ws_kernel (SMCRT_LEAN_WS=0: lean_kernel) when its LDS fits
+  bool ws_ok = false;
   // lean_kernel serves this scene: equal refractive indices, no detectors, a few tops, bucketed
   // deposition, axes below 2^20 cells (SMCRT_LEAN=0 keeps transport_kernel)
   bool lean_ok = false;
@@ -703,6 +706,9 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
     s->lean_ok = ok && s->lean_mode != 0 && !s->nested;
+    const char* wsv = std::getenv("SMCRT_LEAN_WS");
+    s->ws_ok = s->lean_ok && !(wsv && std::string(wsv) == "0") &&
+               lean_lds(s) + kinst_ws_shared_bytes() <= 163840;
     const char* dm = std::getenv("SMCRT_DEBUG_LEAN_MARGIN");
     s->lean_debug = dm ? (std::string(dm) == "all" ? 2u : (std::string(dm) == "0" ? 1u : 0u)) : 0u;
   }
@@ -716,6 +722,12 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lean_fn(s), 256, lean_lds(s));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     s->grid_blocks_lean = cus * per_cu;
+  }
+  if (s->ws_ok) {
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ws_kernel_ptr(s->lds_faces, s->grid_mode),
+                                                                 kinst_ws_threads(), lean_lds(s));
+    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
+    s->grid_blocks_ws = cus * per_cu;
   }
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
@@ -952,16 +964,22 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   const bool lean = !xsrc && s->lean_ok && K.bucket_tiles && (K.flags & SMCRT_FLAG_PATHLENGTH) &&
                     !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
                     (s->lean_mode == 1 || !s->xps_measured || s->xps <= LEAN_MAX_XPS);
+  const bool ws = lean && s->ws_ok;
+  const uint64_t ws_needed = (Ch.n_photons + kinst_ws_photon_lanes() - 1) / kinst_ws_photon_lanes();
   const int blocks = (int)std::min<uint64_t>(
-      (uint64_t)(lean ? s->grid_blocks_lean : (xsrc ? s->grid_blocks_x : s->grid_blocks)),
-      std::max<uint64_t>(1, blocks_needed));
+      (uint64_t)(ws ? s->grid_blocks_ws : (lean ? s->grid_blocks_lean : (xsrc ? s->grid_blocks_x : s->grid_blocks))),
+      std::max<uint64_t>(1, ws ? ws_needed : blocks_needed));
   if (lean) {
     ++s->lean_launches;
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;
     const ProgOp* a_prog = K.prog;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(lean_fn(s), dim3(blocks), dim3(256), args, lean_lds(s), stream));
+    if (ws)
+      HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode), dim3(blocks), dim3(kinst_ws_threads()), args,
+                             lean_lds(s), stream));
+    else
+      HIPCHK(hipLaunchKernel(lean_fn(s), dim3(blocks), dim3(256), args, lean_lds(s), stream));
   } else {
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;

@@ -1,0 +1,629 @@
+// ws.h — the lean transport kernel with wave-specialised blocks (photon waves, walker waves).
+//
+// Same path, same program points and same arithmetic as lean_kernel (lean.h: noBiasPropagation
+// kernelsMod.f90:1901-1976 -> tauint2 inttau2.f90:15-364 -> update_grids :367-465), same
+// results bit for bit, for the same scenes (no Fresnel events, no detectors, no survival bias,
+// a plain source, bucketed path-length deposition).
+//
+// Why. In lean_kernel every wave is both: 64 photons and 64 walkers. Its register peak is the
+// walk (a crossing and the bucket emit) on top of the photons' live state, 167 VGPRs, so a SIMD
+// holds three waves; compiled for four it spills 36 dwords a lane. The
+// photon code alone fits four waves (128 VGPRs, 2 dwords of scratch), and a walker holds no
+// photon state at all. Here a block of WS_WAVES = 8 waves runs WS_PW photon waves and
+// 8 - WS_PW walker waves:
+//   * photon waves run fetch, EVAL, P3/P4, the segment hand-out, P5/P6, the events and P8 on
+//     their 64 photons; a segment (update_grids entry) goes into the BLOCK's ring in LDS;
+//   * walker waves take the oldest segments of the ring into idle lanes, walk them one
+//     crossing per iteration with dda_step (transport.h), file the records into the block's
+//     buckets (deposit.h) and, at a segment's end, write its final cells and flags into the
+//     owner photon's slot, exactly as lean_kernel's walkers do.
+// A segment's walk is the pure function of (start, direction, length) it is in lean_kernel
+// (the start cell is recomputed from the start with the same cell_of), the deferred/synchronous
+// rule and the hazard accounting are lean.h's, and the photon side is lean_kernel's code, so the
+// records, counters and tallies are lean_kernel's; only the order of the fp64 jmean sums differs.
+//
+// The block ring (multi-producer, multi-consumer, LDS). Ticket t uses entry t mod WS_RING, and
+// the entry's `meta` word is a sequence lock that orders its laps:
+//     written(t) -> consumed(t) -> written(t + WS_RING) -> consumed(t + WS_RING) -> ...
+//   * a photon wave reserves n tickets with one LDS add on `tail`; for each ticket t it waits
+//     until meta shows consumed(t - WS_RING) (the initial 0 for t < WS_RING), writes the entry
+//     and then meta = written(t) (owner, slot, sync flag, ticket) with a release store;
+//   * a walker wave claims up to its idle lanes' count of tickets with a compare-and-swap on
+//     `head` (never past `tail`); each lane waits until meta shows written(t), loads the entry
+//     and stores meta = consumed(t) (release);
+//   * every wait is for a strictly smaller ticket (a producer of t for the consumer of
+//     t - WS_RING, that consumer for the producer of t - WS_RING, ...), so the waits cannot form
+//     a cycle, and they end at the first lap's initial state. In practice a producer never
+//     waits: a photon has at most LEAN_SLOTS segments in flight (its busy bits), and WS_RING >=
+//     WS_NPL * LEAN_SLOTS, so ticket t - WS_RING is claimed long before t is reserved;
+//   * termination: each photon wave decrements `alive` after its last photon (its last push
+//     precedes that in its LDS order); a walker wave ends when it holds no segment, `alive` is
+//     0 and every ticket is claimed.
+// Otherwise no wave waits for another except a photon for its synchronous segment (and the
+// bucket claims of deposit.h among the walker waves, whose bound is unchanged: only walkers
+// deposit).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lean.h"
+
+namespace smcrt {
+
+#ifndef SMCRT_WS_PHOTON_WAVES
+#define SMCRT_WS_PHOTON_WAVES 5
+#endif
+constexpr int WS_WAVES = 8;
+constexpr int WS_THREADS = 64 * WS_WAVES;
+constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (the others walk)
+static_assert(WS_PW >= 1 && WS_PW < WS_WAVES, "a block needs photon and walker waves");
+constexpr uint32_t WS_NPL = 64u * WS_PW;  // photon lanes per block (<= 512: 9 owner bits)
+constexpr uint32_t ws_pow2(uint32_t v) { return v <= 1 ? 1 : 2 * ws_pow2((v + 1) / 2); }
+constexpr uint32_t WS_RING = ws_pow2(WS_NPL * LEAN_SLOTS);
+static_assert(WS_RING >= WS_NPL * LEAN_SLOTS && WS_RING < (1u << 18), "ring bound");
+// meta word: owner (9 bits) | slot << 9 (2 bits) | synchronous << 11 | consumed << 12 |
+// ((ticket + 1) mod 2^19) << 13; 0 = never written
+constexpr uint32_t WS_CONSUMED = 1u << 12;
+constexpr uint32_t WS_SEQ_MASK = 0xFFFFF000u;  // ticket and consumed bit
+__device__ __forceinline__ uint32_t ws_tick(uint32_t t) { return ((t + 1u) & 0x7FFFFu) << 13; }
+
+struct WsShared {
+  double ox[WS_RING], oy[WS_RING], oz[WS_RING];  // start, corner coordinates
+  double dx[WS_RING], dy[WS_RING], dz[WS_RING];  // direction
+  double sl[WS_RING];                            // length
+  uint32_t meta[WS_RING];                        // written last (see above)
+  unsigned long long pcell[WS_NPL][LEAN_SLOTS];  // a finished segment: cells | tflag | fault
+  uint32_t busy[WS_NPL];                         // bit s: slot s holds a segment in flight
+  uint32_t lu[3][WS_NPL];                        // interactions, nscatt, status (LL_*)
+  uint32_t wctr[WS_WAVES][LC_N];                 // per-wave counters
+  uint32_t head, tail, alive;
+};
+
+__device__ __forceinline__ void ws_count(WsShared* sh, int c) {
+  const uint64_t m = __ballot(1);
+  if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&sh->wctr[threadIdx.x >> 6][c], (uint32_t)__popcll(m));
+}
+
+// the owner's view of its busy bits (another wave's walker clears them)
+__device__ __forceinline__ uint32_t ws_busy(WsShared* sh, uint32_t pl) {
+  return __hip_atomic_load(&sh->busy[pl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ uint32_t ws_load(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <bool LDS_FACES, int GM>
+__global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ws_kernel(
+    KParams K, const smcrt_sdf_node* __restrict__ nodes, const ProgOp* __restrict__ prog,
+    const KCold* __restrict__ C) {
+  __shared__ WsShared shm;
+  WsShared* sh = &shm;
+  const double eps = 1e-8;  // inttau2.f90:56
+  const int lane_id = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+
+  extern __shared__ double sh_dyn[];  // [props | faces] | the block's bucket words
+  const TopProps* props = K.props;
+  const double* xf = K.xface;
+  const double* yf = K.yface;
+  const double* zf = K.zface;
+  int dyn_off = 0;
+  if constexpr (LDS_FACES) {
+    const int np = 4 * K.n_top;
+    const double* gp = (const double*)K.props;
+    for (int i = threadIdx.x; i < np; i += blockDim.x) sh_dyn[i] = gp[i];
+    const int nf = (K.nx + 1) + (K.ny + 1) + (K.nz + 2);
+    double* sh_faces = sh_dyn + np;
+    for (int i = threadIdx.x; i < nf; i += blockDim.x) sh_faces[i] = K.xface[i];
+    props = (const TopProps*)sh_dyn;
+    xf = sh_faces;
+    yf = sh_faces + (K.nx + 1);
+    zf = yf + (K.ny + 1);
+    dyn_off = np + nf;
+  }
+  unsigned long long* const bstate = (unsigned long long*)(sh_dyn + dyn_off);
+  init_buckets(K, C, bstate);
+  for (int c = lane_id; c < LC_N; c += 64) sh->wctr[wv][c] = 0;
+  for (uint32_t i = threadIdx.x; i < WS_NPL; i += WS_THREADS) {
+    sh->busy[i] = 0;
+    sh->lu[0][i] = sh->lu[1][i] = sh->lu[2][i] = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < WS_RING; i += WS_THREADS) sh->meta[i] = 0;
+  if (threadIdx.x == 0) {
+    sh->head = sh->tail = 0;
+    sh->alive = WS_PW;
+  }
+  __syncthreads();
+
+  uint32_t w_iters = 0;
+  if (wv < WS_PW) {
+    // =================================================================== photon waves ======
+    const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
+    const bool records_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) != 0 && C->records != nullptr;
+    const uint32_t pl = threadIdx.x;  // photon lane (the photon waves come first)
+#define WLU(f) (sh->lu[(f)][pl])
+    // lean_margin (lean.h), per axis, corner coordinates; SMCRT_DEBUG_LEAN_MARGIN (tests only)
+    const double mf = K.lean_debug ? 0.0 : 2.0 * eps;
+    const double mx = mf * (double)(K.nx + 2), my = mf * (double)(K.ny + 2), mz = mf * (double)(K.nz + 2);
+    const double ex = 2.0 * K.xmax - mx, ey = 2.0 * K.ymax - my, ez = 2.0 * K.zmax - mz;
+    const bool defer_all = K.lean_debug == 2u;
+
+    LeanPhoton P;
+    P.st = ST_FETCH; P.f = LF_CELLS;
+    P.pos = P.dir = v3(0.0, 0.0, 0.0);
+    P.tau = P.taurun = P.d = P.minabs = 0.0;
+    P.layer = P.xcell = P.ycell = P.zcell = 0;
+    P.hop = P.loopc = P.seq = 0;
+    P.rng.init(0);
+    uint32_t w_sdf = 0;
+    uint64_t chunk_base = 0;
+    uint32_t chunk_left = 0;
+    bool more = true;
+
+    // P8: arrive at the hop-loop head, inttau2.f90:61
+    auto p8 = [&]() {
+      if (!(P.f & (LF_REQ | LF_WAIT | LF_PEND)) && P.st == ST_H0) {
+        if (!(P.taurun <= P.tau)) P.st = ST_T2END;
+        else if (++P.hop > (uint32_t)MAX_HOP_ITERS) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; }
+        else P.set(LF_PEND);
+      }
+    };
+    for (;; ++w_iters) {
+      // ---- photon fetch (wave-aggregated work queue), as lean_kernel ----------------------
+      {
+        uint64_t need = __ballot(P.st == ST_FETCH);
+        while (need && more) {
+          if (chunk_left == 0) {
+            unsigned long long base = 0;
+            if (lane_id == 0) base = atomicAdd(C->queue, (unsigned long long)SMCRT_FETCH_CHUNK);
+            chunk_base = __shfl(base, 0, 64);
+            const uint64_t n_photons = C->n_photons;
+            chunk_left = (chunk_base < n_photons)
+                             ? (uint32_t)((n_photons - chunk_base) < SMCRT_FETCH_CHUNK ? (n_photons - chunk_base)
+                                                                                         : SMCRT_FETCH_CHUNK)
+                             : 0u;
+            if (chunk_left == 0) { more = false; break; }
+          }
+          const uint32_t n = __popcll(need);
+          const uint32_t take = n < chunk_left ? n : chunk_left;
+          const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
+          if (P.st == ST_FETCH && rank < take) {
+            P.rng.init(C->first_photon + chunk_base + rank);
+            P.st = ST_EMIT;
+          }
+          chunk_base += take;
+          chunk_left -= take;
+          need = __ballot(P.st == ST_FETCH);
+        }
+        if (!more && P.st == ST_FETCH) P.st = ST_IDLE;
+        if (__ballot(P.st != ST_IDLE) == 0) break;  // (walkers finish this wave's segments)
+      }
+
+      // ---- EVAL: the SDF array at the photon's query point (lean_kernel) --------------------
+      const bool have = (P.f & (LF_PEND | LF_REQ | LF_WAIT)) == LF_PEND;
+      EvalOut R;
+      R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
+      if (__ballot(have)) {
+        const bool mask_le = test_kernel && P.st == ST_LAYER;
+        const V3 q = (P.st == ST_H1 || P.st == ST_G0) ? P.pos + smul(P.d, P.dir) : P.pos;
+        R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, 0, 0);
+        const bool counted = P.st == ST_H0 || P.st == ST_H1 || P.st == ST_H3 || P.st == ST_M1 || P.st == ST_G0;
+        w_sdf += __popcll(__ballot(have && counted)) * (uint32_t)K.n_top;
+        if (have) P.clr(LF_PEND);
+      }
+
+      // ---- P3: consume the EVAL result (lean_kernel's P3) ----------------------------------
+      if (have && (P.st == ST_H0 || P.st == ST_H3 || P.st == ST_M1)) {
+        const uint32_t st0 = P.st;
+        P.minabs = R.minabs;
+        const bool small = st0 == ST_H0 && R.minabs < eps;  // on a surface: micro-step
+        const bool out = st0 != ST_H0 && R.minv > 0.0;
+        if (out) P.set(LF_TFLAG);
+        if (st0 == ST_H0) P.loopc = 0;
+        const bool done = P.taurun >= P.tau || P.has(LF_TFLAG);
+        P.d = small ? R.minabs + 2.0 * eps : R.minabs;
+        uint32_t ns = st0 == ST_M1 ? (out ? (uint32_t)ST_B0 : (uint32_t)ST_M0) : (done ? (uint32_t)ST_T2END : (uint32_t)ST_M0);
+        if (small) { ns = ST_H1; P.set(LF_PEND); }
+        P.st = ns;
+      } else if (have) {
+        switch (P.st) {
+          case ST_LAYER:  // kernelsMod.f90:1948-1952 (test_kernel: mask ds<=0, :2136)
+            P.layer = R.maxloc;
+            if (P.layer == 0) { P.set(LF_FAULT); P.st = ST_DONE; }
+            else P.st = ST_T2;
+            break;
+          case ST_H1: {  // :86-123 (the segment starts at the pre-move pos)
+            const double kap = props[P.layer - 1].kappa;
+            const double t = P.d * kap;
+            if (R.maxloc == P.layer) {
+              if (P.taurun + t < P.tau) { P.set(LF_MOVE_FWD); P.taurun = P.taurun + t; }
+              else { P.d = (P.tau - P.taurun) / kap; P.taurun = P.taurun + t; }
+            } else {
+              if (P.taurun + t < P.tau) { P.set(LF_MOVE_BACK); P.taurun = P.taurun + t; }
+              else { P.d = (P.tau - P.taurun) / kap; P.set(LF_MOVE_BACK); }
+            }
+            P.st = ST_H2;
+            P.set(LF_REQ);
+            break;
+          }
+          case ST_G0: {  // new layer and the glancing loop, :220-245; equal n: cross, :318-328
+            const int32_t new_layer = R.maxloc;
+            if (new_layer == P.layer && R.minabs < eps) {
+              if (++P.loopc > (uint32_t)MAX_GLANCE_ITERS) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; break; }
+              P.d = P.d + eps;
+              P.set(LF_PEND);
+              break;
+            }
+            if (new_layer == 0) { P.set(LF_TFLAG); P.st = ST_T2END; break; }
+            P.layer = new_layer;
+            P.st = ST_X1;
+            P.set(LF_REQ);
+            break;
+          }
+          default:
+            break;
+        }
+      }
+
+      // ---- P4: a march step, :155-176 -------------------------------------------------------
+      if (!(P.f & (LF_REQ | LF_WAIT)) && P.st == ST_M0) {
+        if (!(P.d >= eps)) {
+          P.st = ST_B0;
+        } else if (++P.loopc > (uint32_t)MAX_MARCH_ITERS) {
+          P.set(LF_FAULT | LF_TFLAG); P.st = ST_B0;
+        } else {
+          const double kap = props[P.layer - 1].kappa;
+          const double t = P.d * kap;
+          if (P.taurun + t < P.tau) {
+            P.taurun = P.taurun + t;
+            P.st = ST_M1; P.set(LF_PEND);
+          } else {
+            P.d = (P.tau - P.taurun) / kap;
+            P.taurun = P.tau;
+            P.st = ST_B0;
+          }
+          P.set(LF_REQ | LF_MOVE_FWD);  // pos += d*dir once the segment from pos is handed out
+        }
+      }
+
+      // ---- hand the new segments to the block's ring (update_grids entry, :401-415) ------------
+      if (__ballot(P.has(LF_REQ))) {
+        bool push = false, sync = false;
+        V3 old = v3(0.0, 0.0, 0.0);
+        const uint32_t slot = P.seq;
+        if (P.has(LF_REQ) && !(ws_busy(sh, pl) & (1u << slot))) {  // (else: retry next trip)
+          ws_count(sh, LC_UPD);
+          old = v3(P.pos.x + K.xmax, P.pos.y + K.ymax, P.pos.z + K.zmax);
+          const int32_t ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x, K.fex),
+                        cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y, K.fey),
+                        ck = cell_of<GM>(old.z, K.nz, K.zmax, K.inv2z, K.fez);
+          // tauint2's move after update_grids (inttau2.f90:98-122, 163-173)
+          if (P.has(LF_MOVE_FWD)) P.pos = P.pos + smul(P.d, P.dir);
+          else if (P.has(LF_MOVE_BACK)) P.pos = P.pos - smul(P.d, P.dir);
+          P.clr(LF_REQ | LF_MOVE_FWD | LF_MOVE_BACK);
+          if (ci == -1 || cj == -1 || ck == -1) {  // outside the grid: tflag, no walk
+            P.set(LF_TFLAG | LF_CELLS);
+            P.xcell = ci; P.ycell = cj; P.zcell = ck;
+          } else {
+            const double len = P.d;
+            const V3 e = v3(old.x + P.dir.x * len, old.y + P.dir.y * len, old.z + P.dir.z * len);
+            const bool inside = old.x >= mx && old.x <= ex && old.y >= my && old.y <= ey && old.z >= mz &&
+                                old.z <= ez && e.x >= mx && e.x <= ex && e.y >= my && e.y <= ey && e.z >= mz &&
+                                e.z <= ez;
+            push = true;
+            sync = !inside && !defer_all;
+          }
+        }
+        const uint64_t pm = __ballot(push);
+        if (pm) {
+          const int first = __builtin_ctzll(pm);
+          uint32_t base = 0;
+          if (lane_id == first) base = atomicAdd(&sh->tail, (uint32_t)__popcll(pm));
+          base = __builtin_amdgcn_readlane(base, first);
+          if (push) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+            const uint32_t t = base + rank;
+            const uint32_t ix = t & (WS_RING - 1);
+            // the entry's previous lap must have been consumed (see the header; no wait in practice)
+            const uint32_t prev = t < WS_RING ? 0u : (ws_tick(t - WS_RING) | WS_CONSUMED);
+            while (__hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev)
+              __builtin_amdgcn_s_sleep(1);
+            sh->ox[ix] = old.x; sh->oy[ix] = old.y; sh->oz[ix] = old.z;
+            sh->dx[ix] = P.dir.x; sh->dy[ix] = P.dir.y; sh->dz[ix] = P.dir.z;
+            sh->sl[ix] = P.d;
+            atomicOr(&sh->busy[pl], 1u << slot);
+            __hip_atomic_store(&sh->meta[ix], pl | (slot << 9) | (sync ? (1u << 11) : 0u) | ws_tick(t),
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            P.seq = P.seq + 1 == LEAN_SLOTS ? 0u : P.seq + 1;
+            P.clr(LF_CELLS);
+            if (sync) P.set(LF_WAIT);
+          }
+        }
+      }
+
+      // ---- P5: a synchronous segment finished; after a segment: next program point ---------
+      if (P.has(LF_WAIT) && !(ws_busy(sh, pl) & (1u << ((P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS)))) {
+        const unsigned long long w = sh->pcell[pl][(P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS];
+        P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
+        P.set(LF_CELLS);
+        if (w & LEAN_TFLAG) P.set(LF_TFLAG);
+        if (w & LEAN_FAULT) P.set(LF_FAULT);
+        P.clr(LF_WAIT);
+      }
+      const bool free_ = !(P.f & (LF_REQ | LF_WAIT));
+      if (free_ && (P.st == ST_H2 || P.st == ST_B0 || P.st == ST_X1)) {
+        if (P.st == ST_X1) {  // :326-335 (pos = smallStepPos)
+          P.taurun = P.taurun + P.d * props[P.layer - 1].kappa;
+          P.pos = P.pos + smul(P.d, P.dir);
+        }
+        if (P.st == ST_H2) {
+          P.st = ST_H3; P.set(LF_PEND);
+        } else if (P.st == ST_X1) {
+          P.st = P.has(LF_TFLAG) ? ST_T2END : ST_H0;
+        } else if (P.taurun >= P.tau || P.has(LF_TFLAG)) {  // B0, :204-207
+          P.st = ST_T2END;
+        } else {  // boundary probe, :213-222 (smallStepPos = pos + d*dir, formed at the EVAL)
+          P.d = P.minabs + 2.0 * eps;
+          P.loopc = 0;
+          P.st = ST_G0; P.set(LF_PEND);
+        }
+      }
+
+      // ---- P6: tauint2 write-back checks, :341-362 ------------------------------------------
+      if (free_ && P.st == ST_T2END) {
+        if (fabs(P.pos.x) > K.xmax) P.set(LF_TFLAG);
+        if (fabs(P.pos.y) > K.ymax) P.set(LF_TFLAG);
+        if (fabs(P.pos.z) > K.zmax) P.set(LF_TFLAG);
+        P.st = ST_INTERACT;
+      }
+      // the final cells of the photon's deferred segments, once they are all done
+      if (!P.has(LF_CELLS) && (P.st == ST_ABSORB || (records_on && P.st == ST_DONE)) && ws_busy(sh, pl) == 0) {
+        const unsigned long long w = sh->pcell[pl][(P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS];
+        P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
+        P.set(LF_CELLS);
+      }
+      // recordWeight of an absorbed photon (kernelsMod.f90:2202-2220) once its cells are in
+      if (P.st == ST_ABSORB && P.has(LF_CELLS)) {
+        if (P.xcell < 1 || P.xcell > K.nx || P.ycell < 1 || P.ycell > K.ny || P.zcell < 1 || P.zcell > K.nz)
+          P.set(LF_FAULT);
+        else if (C->absorb) atomic_add_nr(C->absorb + lin(K, P.xcell, P.ycell, P.zcell), 1.0);
+        P.st = ST_DONE;
+      }
+
+      // ---- P7: photon events, batched as in lean_kernel --------------------------------------
+      {
+        const bool ev = free_ && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
+        const uint64_t evm = __ballot(ev);
+        const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
+        const uint32_t nev = __popcll(evm);
+        const bool run_ev = nev && (nev >= SMCRT_LEAN_EVENT_LANES || evm == busy);
+        if (run_ev) {
+          if (ev && P.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2126-2170
+            if (P.f & (LF_TFLAG | LF_FAULT)) {
+              P.st = ST_DONE;
+            } else if (WLU(LL_INTER) + 1u > (uint32_t)MAX_INTERACTIONS) {
+              ++WLU(LL_INTER);
+              P.set(LF_FAULT); P.st = ST_DONE;
+            } else {
+              const double ran = P.rng.next(K.key0, K.key1);
+              const TopProps pr = props[P.layer - 1];
+              const bool sc = ran < pr.albedo;
+              ++WLU(LL_INTER);
+              if (!sc) {
+                P.set(LF_TFLAG); WLU(LL_STATUS) = 1; ws_count(sh, LC_ABSORBED);
+                // recordWeight(packet, 1.0) at the photon's cells once they are in (ST_ABSORB)
+                P.st = test_kernel ? ST_DONE : ST_ABSORB;
+              } else {
+                Lane L;  // scatter, photon.f90:1045-1103
+                L.dir = P.dir; L.rng = P.rng; L.fault = false; L.tflag = false;
+                scatter(K, L, pr.hgg);
+                P.dir = L.dir; P.rng = L.rng;
+                if (L.fault) P.set(LF_FAULT | LF_TFLAG);  // (renormalisation runaway)
+                const uint32_t st = ++WLU(LL_NSCATT);
+                ws_count(sh, LC_SCATTERS);
+                if (test_kernel) {
+                  if (st >= 1 && st <= 4) {
+                    double* const moments = C->moments;
+                    if (moments) {
+                      double* m = moments + 3 * (st - 1);
+                      double* m2 = moments + 12 + 3 * (st - 1);
+                      atomic_add_nr(m + 0, P.pos.x); atomic_add_nr(m + 1, P.pos.y); atomic_add_nr(m + 2, P.pos.z);
+                      atomic_add_nr(m2 + 0, P.pos.x * P.pos.x);
+                      atomic_add_nr(m2 + 1, P.pos.y * P.pos.y);
+                      atomic_add_nr(m2 + 2, P.pos.z * P.pos.z);
+                    }
+                  } else if (K.flags & SMCRT_FLAG_END_EARLY) {
+                    P.set(LF_TFLAG);
+                    WLU(LL_STATUS) = 4;
+                  }
+                }
+                P.st = ST_T2;
+              }
+            }
+          }
+          if (ev && P.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
+            ws_count(sh, LC_TAU);
+            P.tau = -det_log(P.rng.next(K.key0, K.key1));
+            P.taurun = 0.0;
+            P.hop = 0;
+            P.st = ST_H0;  // arrives in P8
+          }
+          if (ev && P.st == ST_EMIT) {  // kernelsMod.f90:1937-1945
+            P.clr(LF_FAULT); P.layer = 0;
+            WLU(LL_STATUS) = 0; WLU(LL_NSCATT) = 0; WLU(LL_INTER) = 0;
+            Lane L;
+            L.rng = P.rng; L.xcell = L.ycell = L.zcell = 0; L.layer = 0; L.tflag = false;
+            emit<GM, false>(K, C, L, 0u);
+            if (!test_kernel) {
+              int64_t tries = 0;
+              while (cell_out(K, L)) {
+                if (++tries > MAX_EMIT_TRIES) { P.set(LF_FAULT); break; }
+                ws_count(sh, LC_RETRIES);
+                emit<GM, false>(K, C, L, 0u);
+              }
+            }
+            P.pos = L.pos; P.dir = L.dir; P.rng = L.rng; P.clr(LF_TFLAG);
+            P.layer = L.layer;
+            P.xcell = L.xcell; P.ycell = L.ycell; P.zcell = L.zcell;
+            P.set(LF_CELLS);
+            if (!test_kernel && !P.has(LF_FAULT) && (K.flags & SMCRT_FLAG_RENDER_SOURCE) && C->emission)
+              atomic_add_nr(C->emission + lin(K, P.xcell, P.ycell, P.zcell), 1.0);
+            if (P.has(LF_FAULT)) P.st = ST_DONE;
+            else { P.st = ST_LAYER; P.set(LF_PEND); }
+          }
+          if (ev && P.st == ST_DONE && (P.has(LF_CELLS) || !records_on)) {  // photon finished
+            if (P.has(LF_FAULT)) { WLU(LL_STATUS) = 3; ws_count(sh, LC_FAULTS); }
+            else if (WLU(LL_STATUS) == 0) { WLU(LL_STATUS) = 2; ws_count(sh, LC_ESCAPED); }
+            ws_count(sh, LC_PHOTONS);
+            atomicAdd(&sh->wctr[wv][LC_DRAWS], P.rng.draws);
+            if (records_on) {
+              const uint64_t pid = ((uint64_t)P.rng.pid_hi << 32) | P.rng.pid_lo;
+              smcrt_photon_record* r = C->records + (pid - C->first_photon);
+              r->pos[0] = P.pos.x; r->pos[1] = P.pos.y; r->pos[2] = P.pos.z;
+              r->dir[0] = P.dir.x; r->dir[1] = P.dir.y; r->dir[2] = P.dir.z;
+              r->weight = 1.0;
+              r->cell[0] = P.xcell; r->cell[1] = P.ycell; r->cell[2] = P.zcell;
+              r->layer = P.layer;
+              r->nscatt = WLU(LL_NSCATT);
+              r->bounces = 0;
+              r->draws = P.rng.draws;
+              r->status = WLU(LL_STATUS);
+            }
+            P.clr(LF_TFLAG | LF_FAULT);
+            P.st = ST_FETCH;
+          }
+        }
+      }
+
+      // ---- P8: arrive at the hop-loop head, :61 ---------------------------------------------
+      p8();
+      // every photon of the wave waits for a walker (a synchronous segment or a free slot):
+      // yield the issue slots to the walkers
+      if (__ballot(P.st != ST_IDLE && !(P.has(LF_WAIT) || P.has(LF_REQ) ||
+                                        (P.st == ST_ABSORB && !P.has(LF_CELLS)))) == 0)
+        __builtin_amdgcn_s_sleep(1);
+    }
+#undef WLU
+    if (lane_id == 0) atomicSub(&sh->alive, 1u);  // (after this wave's last push, in its LDS order)
+    // ---- per-wave counters (photon side) ---------------------------------------------------
+    unsigned long long* const counters = C->counters;
+    if (lane_id == 0) {
+      if (C->dep_ctl && sh->wctr[wv][LC_UPD]) atomicAdd(C->dep_ctl + 6, sh->wctr[wv][LC_UPD]);  // segments
+      if (counters) {
+        const uint32_t* c = sh->wctr[wv];
+        const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
+                                             0u,            c[LC_UPD],     c[LC_TAU],      0u,             0u,
+                                             0u,            c[LC_FAULTS],  c[LC_DRAWS],    0u,             c[LC_ESCAPED],
+                                             w_iters};
+        for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
+          if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
+      }
+      double* const nscatt = C->nscatt;
+      if (nscatt && sh->wctr[wv][LC_SCATTERS]) atomic_add_nr(nscatt, (double)sh->wctr[wv][LC_SCATTERS]);
+    }
+  } else {
+    // =================================================================== walker waves ======
+    WalkSeg W;
+    W.old = v3(0.0, 0.0, 0.0);
+    W.sd = W.slen = 0.0;
+    W.xcell = W.ycell = W.zcell = 0;
+    W.dda_it = 0;
+    W.seg = W.tflag = W.fault = false;
+    V3 wdir = v3(0.0, 0.0, 0.0);
+    uint32_t wmeta = 0;
+    BucketLog WB;
+    WB.next = WB.end = 0;
+    uint32_t overflow = 0, hazards = 0, w_dep = 0;
+    for (;; ++w_iters) {
+      // idle walkers take the oldest tickets of the ring (wave-uniform)
+      const uint64_t im = __ballot(!W.seg);
+      if (im) {
+        const uint32_t ni = (uint32_t)__popcll(im);
+        uint32_t base = 0, k = 0;
+        if (lane_id == 0) {
+          for (;;) {
+            const uint32_t h = ws_load(&sh->head), t = ws_load(&sh->tail);
+            k = t - h < ni ? t - h : ni;
+            if (k == 0) break;
+            uint32_t exp = h;
+            if (__hip_atomic_compare_exchange_strong(&sh->head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
+              base = h;
+              break;
+            }
+          }
+        }
+        k = __builtin_amdgcn_readfirstlane(k);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (k) {
+          const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
+          if (!W.seg && rank < k) {
+            const uint32_t t = base + rank;
+            const uint32_t ix = t & (WS_RING - 1);
+            const uint32_t want = ws_tick(t);
+            uint32_t m;
+            // the producer reserved the ticket before writing its entry: wait for written(t)
+            while (((m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) &
+                    WS_SEQ_MASK) != want)
+              __builtin_amdgcn_s_sleep(1);
+            W.old = v3(sh->ox[ix], sh->oy[ix], sh->oz[ix]);
+            wdir = v3(sh->dx[ix], sh->dy[ix], sh->dz[ix]);
+            W.slen = sh->sl[ix];
+            wmeta = m;
+            __hip_atomic_store(&sh->meta[ix], want | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // the start cell, as the photon computed it from the same start (update_grids :401-415)
+            W.xcell = cell_of<GM>(W.old.x, K.nx, K.xmax, K.inv2x, K.fex);
+            W.ycell = cell_of<GM>(W.old.y, K.ny, K.ymax, K.inv2y, K.fey);
+            W.zcell = cell_of<GM>(W.old.z, K.nz, K.zmax, K.inv2z, K.fez);
+            W.sd = 0.0; W.dda_it = 0;
+            W.seg = true; W.tflag = false; W.fault = false;
+          }
+        }
+      }
+      const uint64_t am = __ballot(W.seg);
+      if (!am) {
+        // nothing to walk: done once every photon wave has finished and every ticket is taken
+        if (ws_load(&sh->alive) == 0 && ws_load(&sh->head) == ws_load(&sh->tail)) break;
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      // ---- one crossing of every held segment (dda_step: wall_dist, deposit, update_pos) ----
+      bool dep = false;
+      uint32_t vox = 0;
+      double val = 0.0;
+      if (W.seg) dda_step<GM>(K, W, wdir, xf, yf, zf, dep, vox, val, 1.0);
+      w_dep += __popcll(__ballot(dep));
+      emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+      // a finished segment: its cells and flags to the owner's slot, then the slot is free
+      if ((am >> lane_id & 1ull) && !W.seg) {
+        const uint32_t owner = wmeta & 511u, slot = (wmeta >> 9) & 3u;
+        const bool sync = (wmeta & (1u << 11)) != 0;
+        if (!sync && (W.tflag || W.fault)) ++hazards;  // cannot happen (lean.h); counted as a fault
+        sh->pcell[owner][slot] = lean_pack(W.xcell, W.ycell, W.zcell) | (W.tflag ? LEAN_TFLAG : 0ull) |
+                                 (W.fault ? LEAN_FAULT : 0ull);
+        // (release: the slot's cells before the bit; the owner reads the bit with acquire)
+        __hip_atomic_fetch_and(&sh->busy[owner], ~(1u << slot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    close_buckets(K, C, WB, w_dep - overflow, overflow);
+    // ---- per-wave counters (walker side) ---------------------------------------------------
+    unsigned long long* const counters = C->counters;
+    const uint32_t hz = wave_sum_u32(hazards);
+    if (lane_id == 0) {
+      if (hz) {  // reported: smcrt_kernel_times.lean_hazards, and SMCRT_CTR_FAULTS
+        atomicAdd(C->dep_ctl + 5, hz);
+        atomicAdd(C->lean_hazards, (unsigned long long)hz);
+      }
+      if (counters) {
+        if (w_dep) atomicAdd(counters + 5, (unsigned long long)w_dep);
+        if (hz) atomicAdd(counters + 11, (unsigned long long)hz);
+        atomicAdd(counters + 15, (unsigned long long)w_iters);
+      }
+    }
+  }
+  __syncthreads();  // every wave of the block is done depositing
+  close_block_buckets(K, C, bstate);
+}
+
+}  // namespace smcrt
