@@ -73,12 +73,15 @@ def up_to_date() -> bool:
 
 def _compile_and_link(out: str, extra=(), variant: str = "", force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
-    objs = [_obj(src, defs, variant) for src, defs in UNITS]
-    todo = [i for i, (src, _) in enumerate(UNITS) if force or _stale(objs[i], includes(src))]
+    # a variant's flags reach the HIP units (kernels and their host side); the host-only C++
+    # units are the base build's objects
+    var = [bool(variant) and src.endswith(".hip") for src, _ in UNITS]
+    objs = [_obj(src, defs, variant if var[i] else "") for i, (src, defs) in enumerate(UNITS)]
+    todo = [i for i, (src, _) in enumerate(UNITS) if (force and (var[i] or not variant)) or _stale(objs[i], includes(src))]
 
     def compile_one(i: int) -> None:
         src, defs = UNITS[i]
-        cmd = [hipcc(), *FLAGS, *extra, *defs, "-c", "-o", objs[i] + ".tmp", src]
+        cmd = [hipcc(), *FLAGS, *(extra if var[i] else ()), *defs, "-c", "-o", objs[i] + ".tmp", src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
@@ -108,8 +111,9 @@ def build_variant(name: str, flags: str, outdir: str = os.path.join(ROOT, "tools
     """A compile-time variant of the library (extra -D flags) as outdir/libsmcrt_<name>.so, for
     A/B and diagnostic runs; its objects are cached under .objs/ with the variant's name."""
     os.makedirs(outdir, exist_ok=True)
+    # (always recompiled: the same name may carry other flags than last time)
     return _compile_and_link(os.path.join(outdir, f"libsmcrt_{name}.so"), tuple(flags.split()), variant=name,
-                             verbose=verbose)
+                             force=True, verbose=verbose)
 
 
 if __name__ == "__main__":

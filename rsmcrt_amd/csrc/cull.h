@@ -36,11 +36,7 @@ namespace smcrt {
 // node index, so a lane reaches the primitive's parameters with one dependent load.
 constexpr uint32_t CULL_MODEL = 1u << 31;      // the top is a model: walk its program ops
 constexpr uint32_t CULL_TRANSLATE = 1u << 30;  // the node's transform is a pure translation
-// the top is a primitive with the identity transform whose parameters the kernel stages in
-// LDS (KParams::ltab): the second word is kind << 24 | its record (8 doubles, P[0..7])
-constexpr uint32_t CULL_LTAB = 1u << 29;
-constexpr uint32_t CULL_TOP_MASK = CULL_LTAB - 1;
-constexpr int LTAB_DOUBLES = 8;
+constexpr uint32_t CULL_TOP_MASK = CULL_TRANSLATE - 1;
 
 // Device view of the culling grid (one copy per scene in device memory).
 struct CullGrid {

@@ -128,12 +128,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
     for (uint32_t i = threadIdx.x; i < 4 * K.hist_tiles; i += blockDim.x) ((uint32_t*)(sh_dyn + hist_off))[i] = 0;
   // the cooperative EVAL's primitive table (COOP instantiations), after the wave words
   double* const ctab = sh_dyn + hist_off + dep_words / 2;
-  // the culled EVAL's primitive records (cull.h CULL_LTAB), after the cooperative table
-  double* const ltab = ctab + (K.ctab ? CTAB_DOUBLES : 0);
   if constexpr (COOP) {
     if (K.ctab)
       for (int i = threadIdx.x; i < CTAB_DOUBLES; i += blockDim.x) ctab[i] = K.ctab[i];
-    for (int i = threadIdx.x; i < (int)K.n_ltab * LTAB_DOUBLES; i += blockDim.x) ltab[i] = K.ltab[i];
   }
 #pragma unroll
   for (int c = 0; c < LC_N; ++c) sh->ctr[c][threadIdx.x] = 0;
@@ -290,7 +287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           }
         } else if (K.cull) {
           FarCert fc;
-          S = eval_culled_coop<XSRC>(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, ltab, want ? &fc : nullptr);
+          S = eval_culled_coop<XSRC>(nodes, prog, K.n_prog, K.cull, q, false, 0, 0, want ? &fc : nullptr);
           if (want && fc.node >= 0) {
             const int32_t node = __builtin_amdgcn_readfirstlane(fc.node);
             const int kind = nodes[node].kind;
@@ -444,11 +441,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           const V3 ql = v3(readlane_f64(q.x, l), readlane_f64(q.y, l), readlane_f64(q.z, l));
           const EvalOut o = eval_culled_coop<XSRC>(nodes, prog, K.n_prog, K.cull, ql,
                                              __builtin_amdgcn_readlane((int)mask_le, l) != 0,
-                                             __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l), ltab);
+                                             __builtin_amdgcn_readlane(capi, l), __builtin_amdgcn_readlane(capj, l));
           if (lane_id == l) R = o;
         }
       } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)
-        R = eval_culled<XSRC>(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj, ltab);
+        R = eval_culled<XSRC>(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj);
       } else {
         R = eval_sdfs<XSRC>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }

@@ -110,9 +110,6 @@ struct smcrt_scene {
   // exact SDF culling (cull.h): grid + lists + the always-evaluated program, one allocation
   CullGrid* d_cull = nullptr;
   void* d_cull_data = nullptr;
-  // the culled EVAL's LDS records of identity-transform primitive tops (cull.h CULL_LTAB)
-  double* d_ltab = nullptr;
-  uint32_t n_ltab = 0;
   double cull_mean_list = 0.0;
   double inv2[3] = {0.0, 0.0, 0.0};
   int grid_mode = 0;  // transport_kernel<*, GM>: 1 = every 2*max a power of two, 2 = and every n too
@@ -265,11 +262,9 @@ static size_t lean_lds(const smcrt_scene* s) {
 // deposit words (4 wave tile histograms, or the block's bucket words), then the coop table.
 static size_t transport_lds(const smcrt_scene* s, uint32_t dep_words, bool xsrc) {
   const bool ctab = s->d_ctab && s->coop_lanes > 0;  // the COOP instantiations stage it
-  const bool coop = s->coop_lanes > 0;  // the COOP instantiations also stage the LDS records
   const bool faces = s->lds_faces && !(xsrc && s->coop_lanes > 0);  // (transport_fn)
   return (faces ? s->face_bytes : 0) + (s->n_dets ? 3 * 256 * sizeof(double) : 0) +
-         (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0) +
-         (coop ? (size_t)s->n_ltab * LTAB_DOUBLES * sizeof(double) : 0);
+         (size_t)dep_words * sizeof(uint32_t) + (ctab ? CTAB_DOUBLES * sizeof(double) : 0);
 }
 // 32-bit LDS words of a block's deposit state (deposit.h): a tile histogram per wave, or one
 // 64-bit bucket word per tile shared by the block.
@@ -307,8 +302,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   if (s->fstream) (void)hipStreamSynchronize(s->fstream);
   void* ptrs[] = {s->d_ctab, s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
-                  s->d_sorted, s->d_tile_count, s->d_tile_start, s->d_pieces, s->d_order, s->d_cull, s->d_cull_data,
-                  s->d_ltab};
+                  s->d_sorted, s->d_tile_count, s->d_tile_start, s->d_pieces, s->d_order, s->d_cull, s->d_cull_data};
   for (int i = 0; i < MAX_SLOTS; ++i) {
     void* per[] = {s->d_pool[i], s->d_chunk_fill[i], s->d_dep_ctl[i], s->d_bin_counts[i], s->d_bucket_tile[i]};
     for (void* p : per)
@@ -558,44 +552,6 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
-  // The culled EVAL's LDS records (cull.h CULL_LTAB, round 4): a listed top that is a primitive
-  // with the identity transform gets its parameters in LDS, so the per-lane list walk loads them
-  // from LDS instead of from the node table in device memory (M4: ~9 dependent loads per lane
-  // EVAL). Only while the COOP kernel's LDS, records included, keeps two blocks per CU
-  // (conservative: 16 B per tile for the deposit words). Off by default: on M4 it measured
-  // 5.98 / 6.09 M photons/s against 7.00 / 6.03 M without (same box, profiles/r04_s2/
-  // ab_m4_ltab.txt; the tail-bound workload's noise is larger than any gain). SMCRT_CULL_LTAB=1
-  // turns it on.
-  std::vector<double> ltab;
-  if (cull.enabled) {
-    const char* le = std::getenv("SMCRT_CULL_LTAB");
-    std::vector<int32_t> rec((size_t)n_top, -1);
-    for (int32_t i = 0; i < n_top; ++i) {
-      const smcrt_sdf_node& nd = nodes[top[i]];
-      bool id = !composite_kind(nd.kind);
-      for (int k = 0; id && k < 16; ++k) id = nd.transform[k] == ((k % 5) == 0 ? 1.0 : 0.0);
-      if (id) {
-        rec[(size_t)i] = (int32_t)(ltab.size() / LTAB_DOUBLES);
-        for (int k = 0; k < LTAB_DOUBLES; ++k) ltab.push_back(nd.param[k]);
-      }
-    }
-    const size_t fb = faces.size() * sizeof(double) + sizeof(TopProps) * (size_t)n_top;
-    const uint64_t nv = (uint64_t)grid->nx * grid->ny * grid->nz;
-    const size_t est = sizeof(LaneShared) + (fb <= 40960 ? fb : 0) + (n_dets ? 3 * 256 * sizeof(double) : 0) +
-                       16 * (size_t)((nv + TILE_VOXELS - 1) / TILE_VOXELS) +
-                       (!ctab.empty() ? CTAB_DOUBLES * sizeof(double) : 0) + ltab.size() * sizeof(double);
-    if (!(le && std::string(le) == "1") || ltab.empty() || est > 80 * 1024 - 1024 ||
-        ltab.size() / LTAB_DOUBLES >= (1u << 24)) {
-      ltab.clear();
-    } else {
-      for (size_t k = 0; k < cull.list.size(); k += 2) {
-        const uint32_t t = cull.list[k] & CULL_TOP_MASK;
-        if ((cull.list[k] & CULL_MODEL) || rec[t] < 0) continue;
-        cull.list[k] |= CULL_LTAB;
-        cull.list[k + 1] = ((uint32_t)nodes[top[t]].kind << 24) | (uint32_t)rec[t];
-      }
-    }
-  }
   if (cull.enabled) {  // [ProgOp always | u32 off | u32 list | double lb], each 16-B aligned
     std::vector<ProgOp> pa;
     for (int32_t t : cull.always)
@@ -624,15 +580,9 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (e == hipSuccess) e = hipMemcpy(s->d_cull, &G, sizeof G, hipMemcpyHostToDevice);
     if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("cull upload: ") + hipGetErrorString(e)));
     s->cull_mean_list = cull.mean_list;
-    if (!ltab.empty()) {
-      if ((st = dalloc(&s->d_ltab, ltab.size()))) return cleanup_fail(st);
-      e = hipMemcpy(s->d_ltab, ltab.data(), sizeof(double) * ltab.size(), hipMemcpyHostToDevice);
-      if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("cull upload: ") + hipGetErrorString(e)));
-      s->n_ltab = (uint32_t)(ltab.size() / LTAB_DOUBLES);
-    }
     if (std::getenv("SMCRT_CULL_LOG"))  // diagnostics
-      std::fprintf(stderr, "[cull] %d tops, %zu always, %d x %d x %d cells of %.4g, %.1f tops per cell, %u LDS records\n",
-                   n_top, cull.always.size(), cull.n[0], cull.n[1], cull.n[2], cull.cell, cull.mean_list, s->n_ltab);
+      std::fprintf(stderr, "[cull] %d tops, %zu always, %d x %d x %d cells of %.4g, %.1f tops per cell\n",
+                   n_top, cull.always.size(), cull.n[0], cull.n[1], cull.n[2], cull.cell, cull.mean_list);
   }
   {  // binned deposition state (deposit.h)
     const uint64_t nv = (uint64_t)grid->nx * grid->ny * grid->nz;
@@ -729,6 +679,10 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     s->grid_blocks_ws = cus * per_cu;
   }
+  if (std::getenv("SMCRT_VERBOSE"))
+    std::fprintf(stderr, "[smcrt] scene: lean %d ws %d (blocks/CU %d, static LDS %zu + dynamic %zu B), lean grid %d, "
+                 "transport grid %d\n", (int)s->lean_ok, (int)s->ws_ok, s->grid_blocks_ws / std::max(1, cus),
+                 kinst_ws_shared_bytes(), lean_lds(s), s->grid_blocks_lean, s->grid_blocks);
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
     hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, dep_words(s), x == 1));
@@ -1040,7 +994,16 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     unsigned long long h[72], ht[9], hc[6];
     HIPCHK(hipStreamSynchronize(stream));
     kinst_diag_gather(h, ht, hc);
-    if (lean) {  // lean_kernel's tallies (lean.h LD_*)
+    if (lean && s->ws_ok) {  // ws_kernel's tallies (ws.h WD_*)
+      const double wi = (double)std::max(1ull, h[20]), pt = (double)std::max(1ull, h[24]);
+      std::fprintf(stderr, "[diag-ws] walker iters %llu: idle %.3f, busy lanes/iter %.1f, pending lanes/iter %.1f | "
+                   "photon trips %llu: sleep %.3f, idle lanes %.1f, sync-waiting %.2f, slot-blocked %.2f, EVAL lanes "
+                   "%.1f, pushes %.2f, P7 runs %.3f (lanes/run %.1f), event-waiting %.2f | producer waits %llu | event "
+                   "iters %llu, lanes/iter %.1f\n",
+                   h[20], h[21] / wi, h[22] / wi, h[23] / wi, h[24], h[25] / pt, h[30] / pt, h[27] / pt, h[26] / pt,
+                   h[31] / pt, h[32] / pt, h[28] / pt, (double)h[29] / (double)std::max(1ull, h[28]), h[36] / pt, h[33],
+                   h[34], (double)h[35] / (double)std::max(1ull, h[34]));
+    } else if (lean) {  // lean_kernel's tallies (lean.h LD_*)
       const double tr = (double)std::max(1ull, h[0]);
       std::fprintf(stderr, "[diag-lean] wave trips %llu | walk steps/trip %.3f, busy walkers/step %.1f | pushes/trip %.2f"
                    " (sync %.3f), blocked req/trip %.2f | EVAL phases/trip %.3f lanes/EVAL %.1f | P7 runs/trip %.3f,"
@@ -1136,8 +1099,6 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.coop_lanes = s->coop_lanes;
   K.cull = s->d_cull;
   K.ctab = s->d_ctab;
-  K.ltab = s->d_ltab;
-  K.n_ltab = s->n_ltab;
   const bool far = s->fm_err > 0.0 && (cfg->flags & SMCRT_FLAG_PATHLENGTH);
   K.fm_err = far ? s->fm_err : 0.0;
   K.fm_step = s->fm_step;

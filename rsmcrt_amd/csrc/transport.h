@@ -127,10 +127,6 @@ struct KParams {
   // the cooperative EVAL's table of primitives (CTAB_ROWS x 64 doubles, column = top - 1),
   // staged in LDS by the COOP instantiation; NULL when the scene does not qualify
   const double* __restrict__ ctab;
-  // culled EVAL's LDS table (cull.h CULL_LTAB): n_ltab records of LTAB_DOUBLES, staged in LDS
-  // by the COOP instantiation after the cooperative table; NULL when the scene does not qualify
-  const double* __restrict__ ltab;
-  uint32_t n_ltab;
   // far-field march (far.h), COOP instantiation with ctab: the absolute error bound of a
   // computed top-level SDF value and the per-step bound on the rounding of p + d*dir (both
   // from the scene's extent); fm_err == 0 turns it off
@@ -1113,7 +1109,7 @@ template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict__ nodes,
                                                const ProgOp* __restrict__ prog, int32_t n_prog,
                                                const CullGrid* __restrict__ G, V3 q, bool have, bool mask_le,
-                                               int32_t capi, int32_t capj, const double* ltab) {
+                                               int32_t capi, int32_t capj) {
   EvalOut r;
   r.minabs = __builtin_inf();
   r.minv = __builtin_inf();
@@ -1175,8 +1171,6 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
           else acc = csg(op.op, acc, v, op.k);
         }
         d = acc;
-      } else if (en.x & CULL_LTAB) {  // identity transform: the shape at q, parameters from LDS
-        d = sdf_shape_s<1>((int32_t)(en.y >> 24), ltab + LTAB_DOUBLES * (en.y & 0xFFFFFFu), q);
       } else {
         d = sdf_prim(nodes + en.y, q, (en.x & CULL_TRANSLATE) != 0);
       }
@@ -1225,8 +1219,7 @@ template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __restrict__ nodes,
                                                     const ProgOp* __restrict__ prog, int32_t n_prog,
                                                     const CullGrid* __restrict__ G, V3 q, bool mask_le,
-                                                    int32_t capi, int32_t capj, const double* ltab,
-                                                    FarCert* fc = nullptr) {
+                                                    int32_t capi, int32_t capj, FarCert* fc = nullptr) {
   const int lane = (int)(threadIdx.x & 63);
   // (certificate only) the always-evaluated tops' smallest and second smallest |ds|, the node
   // and 1-based index of the smallest when it is a lone primitive (-1: a model), how many are
@@ -1310,8 +1303,6 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
             else acc = csg(op.op, acc, v, op.k);
           }
           d = acc;
-        } else if (en.x & CULL_LTAB) {
-          d = sdf_shape_s<1>((int32_t)(en.y >> 24), ltab + LTAB_DOUBLES * (en.y & 0xFFFFFFu), q);
         } else {
           d = sdf_prim(nodes + en.y, q, (en.x & CULL_TRANSLATE) != 0);
         }
@@ -1326,7 +1317,7 @@ __device__ __forceinline__ EvalOut eval_culled_coop(const smcrt_sdf_node* __rest
           const double ad = o.minabs;
           if (ad < l1) {
             l2 = l1; l1 = ad;
-            n1 = (en.x & (CULL_MODEL | CULL_LTAB)) ? -1 : (int32_t)en.y;
+            n1 = (en.x & CULL_MODEL) ? -1 : (int32_t)en.y;
             t1 = i + 1;
             neg1 = d < 0.0;
           } else if (ad < l2) {

@@ -17,28 +17,38 @@
 //     crossing per iteration with dda_step (transport.h), file the records into the block's
 //     buckets (deposit.h) and, at a segment's end, write its final cells and flags into the
 //     owner photon's slot, exactly as lean_kernel's walkers do.
+//   * event waves (round 5, session 2) run the photons' interactions: the albedo roulette,
+//     scatter and the next tauint2 entry (kernelsMod.f90:1958-1975, photon.f90:1045-1103,
+//     inttau2.f90:48-60), and the tauint2 entry after an emission. A photon with such an event
+//     writes its direction, RNG state and layer into its slot, queues its lane in the block's
+//     event queue and waits; an event lane takes the queued owner, runs the event on the
+//     owner's values with the owner's own Philox stream and writes the results back. The event
+//     code so runs on full waves: in lean_kernel a wave ran its events once 20 of its lanes
+//     waited (0.52 phases a trip with 21 lanes, 22 % of the wave time). Emission, completion,
+//     the rare terminal interactions and every event of test_kernel runs (moments) stay in the
+//     photon waves, batched as in lean_kernel.
 // A segment's walk is the pure function of (start, direction, length) it is in lean_kernel
 // (the start cell is recomputed from the start with the same cell_of), the deferred/synchronous
 // rule and the hazard accounting are lean.h's, and the photon side is lean_kernel's code, so the
 // records, counters and tallies are lean_kernel's; only the order of the fp64 jmean sums differs.
 //
-// The block ring (multi-producer, multi-consumer, LDS). Ticket t uses entry t mod WS_RING, and
-// the entry's `meta` word is a sequence lock that orders its laps:
+// The block ring (multi-producer, multi-consumer, LDS). Tickets are matched one to one: photon
+// waves take them from `tail` (one reserved per segment), walker lanes from `head` (one held
+// per idle lane; head may run ahead of tail). Ticket t uses entry t mod WS_RING, whose `meta`
+// word is a sequence lock ordering the entry's laps:
 //     written(t) -> consumed(t) -> written(t + WS_RING) -> consumed(t + WS_RING) -> ...
 //   * a photon wave reserves n tickets with one LDS add on `tail`; for each ticket t it waits
 //     until meta shows consumed(t - WS_RING) (the initial 0 for t < WS_RING), writes the entry
 //     and then meta = written(t) (owner, slot, sync flag, ticket) with a release store;
-//   * a walker wave claims up to its idle lanes' count of tickets with a compare-and-swap on
-//     `head` (never past `tail`); each lane waits until meta shows written(t), loads the entry
-//     and stores meta = consumed(t) (release);
-//   * every wait is for a strictly smaller ticket (a producer of t for the consumer of
-//     t - WS_RING, that consumer for the producer of t - WS_RING, ...), so the waits cannot form
-//     a cycle, and they end at the first lap's initial state. In practice a producer never
-//     waits: a photon has at most LEAN_SLOTS segments in flight (its busy bits), and WS_RING >=
-//     WS_NPL * LEAN_SLOTS, so ticket t - WS_RING is claimed long before t is reserved;
+//   * a walker lane that holds ticket t checks its entry once per iteration (no wait); when
+//     meta shows written(t) it takes the fields, stores meta = consumed(t) (release) and walks;
+//   * every wait is a producer's, for the consumption of a strictly smaller ticket whose holder
+//     checks it every iteration, so the waits cannot form a cycle. In practice a producer never
+//     waits: a photon has at most WS_SLOTS segments in flight (its busy bits), WS_RING >=
+//     WS_NPL * WS_SLOTS, and held tickets are taken as soon as they are written;
 //   * termination: each photon wave decrements `alive` after its last photon (its last push
-//     precedes that in its LDS order); a walker wave ends when it holds no segment, `alive` is
-//     0 and every ticket is claimed.
+//     precedes that in its LDS order), which fixes the final tail; walker lanes drop tickets at
+//     or past it, and a walker wave ends when it holds no segment and no earlier ticket.
 // Otherwise no wave waits for another except a photon for its synchronous segment (and the
 // bucket claims of deposit.h among the walker waves, whose bound is unchanged: only walkers
 // deposit).
@@ -51,16 +61,26 @@
 namespace smcrt {
 
 #ifndef SMCRT_WS_PHOTON_WAVES
-#define SMCRT_WS_PHOTON_WAVES 5
+#define SMCRT_WS_PHOTON_WAVES 4
+#endif
+#ifndef SMCRT_WS_EVENT_WAVES
+#define SMCRT_WS_EVENT_WAVES 1
+#endif
+#ifndef SMCRT_WS_SLOTS
+#define SMCRT_WS_SLOTS 2
 #endif
 constexpr int WS_WAVES = 8;
 constexpr int WS_THREADS = 64 * WS_WAVES;
-constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (the others walk)
-static_assert(WS_PW >= 1 && WS_PW < WS_WAVES, "a block needs photon and walker waves");
+constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (waves 0 .. WS_PW-1)
+constexpr int WS_EW = SMCRT_WS_EVENT_WAVES;   // event waves (next), the rest walk
+static_assert(WS_PW >= 1 && WS_EW >= 1 && WS_PW + WS_EW < WS_WAVES, "a block needs all three roles");
+constexpr uint32_t WS_SLOTS = SMCRT_WS_SLOTS;  // segments a photon may have in flight (<= 4)
+static_assert(WS_SLOTS >= 1 && WS_SLOTS <= 4, "two slot bits in a meta word");
 constexpr uint32_t WS_NPL = 64u * WS_PW;  // photon lanes per block (<= 512: 9 owner bits)
 constexpr uint32_t ws_pow2(uint32_t v) { return v <= 1 ? 1 : 2 * ws_pow2((v + 1) / 2); }
-constexpr uint32_t WS_RING = ws_pow2(WS_NPL * LEAN_SLOTS);
-static_assert(WS_RING >= WS_NPL * LEAN_SLOTS && WS_RING < (1u << 18), "ring bound");
+constexpr uint32_t WS_EQ = ws_pow2(WS_NPL);  // event queue entries (a photon has at most one event queued)
+constexpr uint32_t WS_RING = ws_pow2(WS_NPL * WS_SLOTS);
+static_assert(WS_RING >= WS_NPL * WS_SLOTS && WS_RING < (1u << 18), "ring bound");
 // meta word: owner (9 bits) | slot << 9 (2 bits) | synchronous << 11 | consumed << 12 |
 // ((ticket + 1) mod 2^19) << 13; 0 = never written
 constexpr uint32_t WS_CONSUMED = 1u << 12;
@@ -72,12 +92,24 @@ struct WsShared {
   double dx[WS_RING], dy[WS_RING], dz[WS_RING];  // direction
   double sl[WS_RING];                            // length
   uint32_t meta[WS_RING];                        // written last (see above)
-  unsigned long long pcell[WS_NPL][LEAN_SLOTS];  // a finished segment: cells | tflag | fault
+  unsigned long long pcell[WS_NPL][WS_SLOTS];  // a finished segment: cells | tflag | fault
   uint32_t busy[WS_NPL];                         // bit s: slot s holds a segment in flight
   uint32_t lu[3][WS_NPL];                        // interactions, nscatt, status (LL_*)
   uint32_t wctr[WS_WAVES][LC_N];                 // per-wave counters
-  uint32_t head, tail, alive;
+  // the event queue (see "Event waves" above): per photon lane an in/out slot, and a queue of
+  // owner lanes with the ring's sequence lock
+  double ev_dir[3][WS_NPL];   // in: direction; out: the scattered direction
+  double ev_cached[WS_NPL];   // in/out: the RNG's cached half block
+  double ev_tau[WS_NPL];      // out: the new optical depth
+  uint32_t ev_pid[2][WS_NPL]; // in: photon index words
+  uint32_t ev_draws[WS_NPL];  // in/out: draws taken
+  uint32_t ev_code[WS_NPL];   // in: layer | kind << 16; out: EV_DONE | result bits (stored last)
+  uint32_t evq[WS_EQ];        // owner | consumed | ticket, as the ring's meta
+  uint32_t head, tail;        // ring tickets: handed to walker lanes / reserved by photon waves
+  uint32_t ev_head, ev_tail;  // event tickets: held by event lanes / reserved by photon waves
+  uint32_t alive;
 };
+constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u;  // event kinds (ev_code bits 16-17)
 
 __device__ __forceinline__ void ws_count(WsShared* sh, int c) {
   const uint64_t m = __ballot(1);
@@ -92,6 +124,17 @@ __device__ __forceinline__ uint32_t ws_busy(WsShared* sh, uint32_t pl) {
 __device__ __forceinline__ uint32_t ws_load(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+
+#ifdef SMCRT_DIAG
+// Diagnostic builds (-DSMCRT_DIAG): wave-uniform tallies of the schedule in g_diag[20..39]
+// (kernels.h), printed per launch by the host ([diag-ws]).
+enum : int { WD_WITERS = 20, WD_WIDLE, WD_WBUSY, WD_WPEND, WD_PTRIPS, WD_PSLEEP, WD_PBLOCKED, WD_PWAIT, WD_P7,
+             WD_P7LANES, WD_PIDLE, WD_ELANES, WD_PUSH, WD_PRODWAIT, WD_EITERS, WD_ELANESRUN, WD_PEVQ, WD_N };
+#define WSDIAG(i, v) (wd[(i) - WD_WITERS] += (uint64_t)(v))
+#else
+#define WSDIAG(i, v) do {} while (0)
+#endif
 
 template <bool LDS_FACES, int GM>
 __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ws_kernel(
@@ -130,13 +173,18 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     sh->lu[0][i] = sh->lu[1][i] = sh->lu[2][i] = 0;
   }
   for (uint32_t i = threadIdx.x; i < WS_RING; i += WS_THREADS) sh->meta[i] = 0;
+  for (uint32_t i = threadIdx.x; i < WS_EQ; i += WS_THREADS) sh->evq[i] = 0;
   if (threadIdx.x == 0) {
     sh->head = sh->tail = 0;
+    sh->ev_head = sh->ev_tail = 0;
     sh->alive = WS_PW;
   }
   __syncthreads();
 
-  uint32_t w_iters = 0;
+  uint32_t w_iters = 0, w_sdf = 0, w_dep = 0, hazards = 0;
+#ifdef SMCRT_DIAG
+  uint64_t wd[WD_N - WD_WITERS] = {};
+#endif
   if (wv < WS_PW) {
     // =================================================================== photon waves ======
     const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
@@ -156,7 +204,6 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     P.layer = P.xcell = P.ycell = P.zcell = 0;
     P.hop = P.loopc = P.seq = 0;
     P.rng.init(0);
-    uint32_t w_sdf = 0;
     uint64_t chunk_base = 0;
     uint32_t chunk_left = 0;
     bool more = true;
@@ -199,6 +246,31 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         if (!more && P.st == ST_FETCH) P.st = ST_IDLE;
         if (__ballot(P.st != ST_IDLE) == 0) break;  // (walkers finish this wave's segments)
       }
+      // an event lane's results (see "Event waves"): the photon evaluates this trip
+      if (P.has(LF_EVQ)) {
+        const uint32_t code = __hip_atomic_load(&sh->ev_code[pl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (code & EV_DONE) {
+          P.clr(LF_EVQ);
+          P.rng.draws = sh->ev_draws[pl];
+          P.rng.cached = sh->ev_cached[pl];
+          if (code & EV_ABSORB) {  // absorbed: recordWeight once the cells are in
+            P.set(LF_TFLAG);
+            P.st = ST_ABSORB;
+          } else {  // scattered (or after an emission), then the tauint2 entry
+            if (code & EV_RUNAWAY) P.set(LF_FAULT | LF_TFLAG);
+            P.dir = v3(sh->ev_dir[0][pl], sh->ev_dir[1][pl], sh->ev_dir[2][pl]);
+            P.tau = sh->ev_tau[pl];
+            P.taurun = 0.0;
+            P.hop = 0;
+            P.st = ST_H0;
+            p8();
+          }
+        }
+      }
+      WSDIAG(WD_PTRIPS, 1);
+      WSDIAG(WD_PIDLE, __popcll(__ballot(P.st == ST_IDLE)));
+      WSDIAG(WD_PWAIT, __popcll(__ballot(P.has(LF_WAIT))));
+      WSDIAG(WD_PEVQ, __popcll(__ballot(P.has(LF_EVQ))));
 
       // ---- EVAL: the SDF array at the photon's query point (lean_kernel) --------------------
       const bool have = (P.f & (LF_PEND | LF_REQ | LF_WAIT)) == LF_PEND;
@@ -210,6 +282,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, 0, 0);
         const bool counted = P.st == ST_H0 || P.st == ST_H1 || P.st == ST_H3 || P.st == ST_M1 || P.st == ST_G0;
         w_sdf += __popcll(__ballot(have && counted)) * (uint32_t)K.n_top;
+        WSDIAG(WD_ELANES, __popcll(__ballot(have)));
         if (have) P.clr(LF_PEND);
       }
 
@@ -316,6 +389,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           }
         }
         const uint64_t pm = __ballot(push);
+        WSDIAG(WD_PUSH, __popcll(pm));
+        WSDIAG(WD_PBLOCKED, __popcll(__ballot(P.has(LF_REQ))));
         if (pm) {
           const int first = __builtin_ctzll(pm);
           uint32_t base = 0;
@@ -327,15 +402,17 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             const uint32_t ix = t & (WS_RING - 1);
             // the entry's previous lap must have been consumed (see the header; no wait in practice)
             const uint32_t prev = t < WS_RING ? 0u : (ws_tick(t - WS_RING) | WS_CONSUMED);
-            while (__hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev)
+            while (__hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev) {
+              WSDIAG(WD_PRODWAIT, 1);
               __builtin_amdgcn_s_sleep(1);
+            }
             sh->ox[ix] = old.x; sh->oy[ix] = old.y; sh->oz[ix] = old.z;
             sh->dx[ix] = P.dir.x; sh->dy[ix] = P.dir.y; sh->dz[ix] = P.dir.z;
             sh->sl[ix] = P.d;
             atomicOr(&sh->busy[pl], 1u << slot);
             __hip_atomic_store(&sh->meta[ix], pl | (slot << 9) | (sync ? (1u << 11) : 0u) | ws_tick(t),
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            P.seq = P.seq + 1 == LEAN_SLOTS ? 0u : P.seq + 1;
+            P.seq = P.seq + 1 == WS_SLOTS ? 0u : P.seq + 1;
             P.clr(LF_CELLS);
             if (sync) P.set(LF_WAIT);
           }
@@ -343,8 +420,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
 
       // ---- P5: a synchronous segment finished; after a segment: next program point ---------
-      if (P.has(LF_WAIT) && !(ws_busy(sh, pl) & (1u << ((P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS)))) {
-        const unsigned long long w = sh->pcell[pl][(P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS];
+      if (P.has(LF_WAIT) && !(ws_busy(sh, pl) & (1u << ((P.seq + WS_SLOTS - 1) % WS_SLOTS)))) {
+        const unsigned long long w = sh->pcell[pl][(P.seq + WS_SLOTS - 1) % WS_SLOTS];
         P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
         P.set(LF_CELLS);
         if (w & LEAN_TFLAG) P.set(LF_TFLAG);
@@ -379,7 +456,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
       // the final cells of the photon's deferred segments, once they are all done
       if (!P.has(LF_CELLS) && (P.st == ST_ABSORB || (records_on && P.st == ST_DONE)) && ws_busy(sh, pl) == 0) {
-        const unsigned long long w = sh->pcell[pl][(P.seq + LEAN_SLOTS - 1) % LEAN_SLOTS];
+        const unsigned long long w = sh->pcell[pl][(P.seq + WS_SLOTS - 1) % WS_SLOTS];
         P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
         P.set(LF_CELLS);
       }
@@ -391,13 +468,47 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         P.st = ST_DONE;
       }
 
-      // ---- P7: photon events, batched as in lean_kernel --------------------------------------
+      // ---- P7: the interactions and tauint2 entries go to the event waves -------------------
       {
-        const bool ev = free_ && (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
+        const bool qev = free_ && !test_kernel && !P.has(LF_EVQ) &&
+                         ((P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT)) &&
+                           WLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS) ||
+                          P.st == ST_T2);
+        const uint64_t qm = __ballot(qev);
+        if (qm) {
+          const int first = __builtin_ctzll(qm);
+          uint32_t base = 0;
+          if (lane_id == first) base = atomicAdd(&sh->ev_tail, (uint32_t)__popcll(qm));
+          base = __builtin_amdgcn_readlane(base, first);
+          if (qev) {
+            const uint32_t t = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+            const uint32_t ix = t & (WS_EQ - 1);
+            const uint32_t prev = t < WS_EQ ? 0u : (ws_tick(t - WS_EQ) | WS_CONSUMED);
+            while (__hip_atomic_load(&sh->evq[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev)
+              __builtin_amdgcn_s_sleep(1);  // (never in practice: one queued event per photon)
+            sh->ev_dir[0][pl] = P.dir.x; sh->ev_dir[1][pl] = P.dir.y; sh->ev_dir[2][pl] = P.dir.z;
+            sh->ev_cached[pl] = P.rng.cached;
+            sh->ev_pid[0][pl] = P.rng.pid_lo; sh->ev_pid[1][pl] = P.rng.pid_hi;
+            sh->ev_draws[pl] = P.rng.draws;
+            sh->ev_code[pl] = (uint32_t)P.layer | ((P.st == ST_INTERACT ? WS_EV_INTERACT : WS_EV_TAU) << 16);
+            __hip_atomic_store(&sh->evq[ix], pl | ws_tick(t), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            P.set(LF_EVQ);
+          }
+        }
+      }
+      // ---- P7: the photon's other events, batched as in lean_kernel ---------------------------
+      {
+        const bool ev = free_ && !P.has(LF_EVQ) &&
+                        (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
         const uint64_t evm = __ballot(ev);
-        const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH);
+        const uint64_t busy = __ballot(P.st != ST_IDLE && P.st != ST_FETCH && !P.has(LF_EVQ));
         const uint32_t nev = __popcll(evm);
-        const bool run_ev = nev && (nev >= SMCRT_LEAN_EVENT_LANES || evm == busy);
+        // (test_kernel runs every event here; otherwise only emission, completion and the rare
+        // terminal interactions are left, one or two per photon: run them once a few wait)
+        const uint32_t batch = test_kernel ? (uint32_t)SMCRT_LEAN_EVENT_LANES : 4u;
+        const bool run_ev = nev && (nev >= batch || evm == busy);
+        WSDIAG(WD_P7, run_ev ? 1 : 0);
+        WSDIAG(WD_P7LANES, run_ev ? nev : 0);
         if (run_ev) {
           if (ev && P.st == ST_INTERACT) {  // kernelsMod.f90:1958-1975 / 2126-2170
             if (P.f & (LF_TFLAG | LF_FAULT)) {
@@ -500,27 +611,95 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       p8();
       // every photon of the wave waits for a walker (a synchronous segment or a free slot):
       // yield the issue slots to the walkers
-      if (__ballot(P.st != ST_IDLE && !(P.has(LF_WAIT) || P.has(LF_REQ) ||
-                                        (P.st == ST_ABSORB && !P.has(LF_CELLS)))) == 0)
+      if (__ballot(P.st != ST_IDLE && !(P.has(LF_WAIT) || P.has(LF_REQ) || P.has(LF_EVQ) ||
+                                        (P.st == ST_ABSORB && !P.has(LF_CELLS)))) == 0) {
+        WSDIAG(WD_PSLEEP, 1);
         __builtin_amdgcn_s_sleep(1);
+      }
     }
 #undef WLU
     if (lane_id == 0) atomicSub(&sh->alive, 1u);  // (after this wave's last push, in its LDS order)
-    // ---- per-wave counters (photon side) ---------------------------------------------------
-    unsigned long long* const counters = C->counters;
-    if (lane_id == 0) {
-      if (C->dep_ctl && sh->wctr[wv][LC_UPD]) atomicAdd(C->dep_ctl + 6, sh->wctr[wv][LC_UPD]);  // segments
-      if (counters) {
-        const uint32_t* c = sh->wctr[wv];
-        const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
-                                             0u,            c[LC_UPD],     c[LC_TAU],      0u,             0u,
-                                             0u,            c[LC_FAULTS],  c[LC_DRAWS],    0u,             c[LC_ESCAPED],
-                                             w_iters};
-        for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
-          if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
+  } else if (wv < WS_PW + WS_EW) {
+    // =================================================================== event waves =======
+    // An event lane holds a ticket of the event queue (as a walker lane holds a ring ticket),
+    // and when the queue entry shows written(ticket) it runs the owner's event: the code of
+    // lean_kernel's P7 on the owner's direction, layer and Philox stream (kernelsMod.f90:1958-1975,
+    // photon.f90:1045-1103, inttau2.f90:48-60), so the draws and results are the owner's own.
+    bool pend = false;
+    uint32_t tk = 0;
+    for (;; ++w_iters) {
+      const uint64_t cm = __ballot(!pend);
+      if (cm) {
+        const int first = __builtin_ctzll(cm);
+        uint32_t base = 0;
+        if (lane_id == first) base = atomicAdd(&sh->ev_head, (uint32_t)__popcll(cm));
+        base = __builtin_amdgcn_readlane(base, first);
+        if (!pend) {
+          tk = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+          pend = true;
+        }
       }
-      double* const nscatt = C->nscatt;
-      if (nscatt && sh->wctr[wv][LC_SCATTERS]) atomic_add_nr(nscatt, (double)sh->wctr[wv][LC_SCATTERS]);
+      bool run = false;
+      uint32_t o = 0;
+      if (pend) {
+        const uint32_t ix = tk & (WS_EQ - 1);
+        const uint32_t m = __hip_atomic_load(&sh->evq[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if ((m & WS_SEQ_MASK) == ws_tick(tk)) {
+          o = m & 511u;
+          __hip_atomic_store(&sh->evq[ix], ws_tick(tk) | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          run = true;
+          pend = false;
+        }
+      }
+      if (!__ballot(run)) {
+        // nothing queued: done once every photon wave has finished (the final tail is known)
+        if (ws_load(&sh->alive) == 0) {
+          const uint32_t T = ws_load(&sh->ev_tail);
+          if (pend && (int32_t)(tk - T) >= 0) pend = false;  // (a ticket nobody will write)
+          if (!__ballot(pend) && (int32_t)(ws_load(&sh->ev_head) - T) >= 0) break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      WSDIAG(WD_EITERS, 1);
+      WSDIAG(WD_ELANESRUN, __popcll(__ballot(run)));
+      if (run) {
+        Rng rg;
+        rg.pid_lo = sh->ev_pid[0][o]; rg.pid_hi = sh->ev_pid[1][o];
+        rg.draws = sh->ev_draws[o]; rg.cached = sh->ev_cached[o];
+        const uint32_t code = sh->ev_code[o];
+        const int32_t layer = (int32_t)(code & 0xFFFFu);
+        uint32_t res = 0;
+        bool tau_entry = (code >> 16) == WS_EV_TAU;
+        if ((code >> 16) == WS_EV_INTERACT) {  // kernelsMod.f90:1958-1975
+          const TopProps pr = props[layer - 1];
+          const double ran = rg.next(K.key0, K.key1);
+          ++sh->lu[LL_INTER][o];
+          if (!(ran < pr.albedo)) {
+            sh->lu[LL_STATUS][o] = 1;
+            ws_count(sh, LC_ABSORBED);
+            res = EV_ABSORB;
+          } else {
+            Lane L;  // scatter, photon.f90:1045-1103
+            L.dir = v3(sh->ev_dir[0][o], sh->ev_dir[1][o], sh->ev_dir[2][o]);
+            L.rng = rg; L.fault = false; L.tflag = false;
+            scatter(K, L, pr.hgg);
+            rg = L.rng;
+            if (L.fault) res = EV_RUNAWAY;  // (renormalisation runaway: tflag and a fault)
+            ++sh->lu[LL_NSCATT][o];
+            ws_count(sh, LC_SCATTERS);
+            sh->ev_dir[0][o] = L.dir.x; sh->ev_dir[1][o] = L.dir.y; sh->ev_dir[2][o] = L.dir.z;
+            tau_entry = true;
+          }
+        }
+        if (tau_entry) {  // tauint2 entry, inttau2.f90:48-60
+          ws_count(sh, LC_TAU);
+          sh->ev_tau[o] = -det_log(rg.next(K.key0, K.key1));
+        }
+        sh->ev_draws[o] = rg.draws;
+        sh->ev_cached[o] = rg.cached;
+        __hip_atomic_store(&sh->ev_code[o], res | EV_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   } else {
     // =================================================================== walker waves ======
@@ -534,57 +713,62 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     uint32_t wmeta = 0;
     BucketLog WB;
     WB.next = WB.end = 0;
-    uint32_t overflow = 0, hazards = 0, w_dep = 0;
+    uint32_t overflow = 0;
+    // A walker lane without a segment holds a ticket of its own (`tk`, taken with one
+    // wave-aggregated LDS add on `head`, which may run ahead of `tail`) and checks its entry
+    // once per iteration without waiting: its meta and fields are loaded together (LDS
+    // operations of one wave complete in order, and the producer stores meta last), and the lane
+    // takes the segment when meta shows written(tk). A ticket no photon will reserve (past the
+    // final tail once every photon wave has finished) is dropped.
+    bool pend = false;
+    uint32_t tk = 0;
     for (;; ++w_iters) {
-      // idle walkers take the oldest tickets of the ring (wave-uniform)
-      const uint64_t im = __ballot(!W.seg);
-      if (im) {
-        const uint32_t ni = (uint32_t)__popcll(im);
-        uint32_t base = 0, k = 0;
-        if (lane_id == 0) {
-          for (;;) {
-            const uint32_t h = ws_load(&sh->head), t = ws_load(&sh->tail);
-            k = t - h < ni ? t - h : ni;
-            if (k == 0) break;
-            uint32_t exp = h;
-            if (__hip_atomic_compare_exchange_strong(&sh->head, &exp, h + k, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP)) {
-              base = h;
-              break;
-            }
-          }
+      const uint64_t cm = __ballot(!W.seg && !pend);
+      if (cm) {
+        const int first = __builtin_ctzll(cm);
+        uint32_t base = 0;
+        if (lane_id == first) base = atomicAdd(&sh->head, (uint32_t)__popcll(cm));
+        base = __builtin_amdgcn_readlane(base, first);
+        if (!W.seg && !pend) {
+          tk = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+          pend = true;
         }
-        k = __builtin_amdgcn_readfirstlane(k);
-        base = __builtin_amdgcn_readfirstlane(base);
-        if (k) {
-          const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0u));
-          if (!W.seg && rank < k) {
-            const uint32_t t = base + rank;
-            const uint32_t ix = t & (WS_RING - 1);
-            const uint32_t want = ws_tick(t);
-            uint32_t m;
-            // the producer reserved the ticket before writing its entry: wait for written(t)
-            while (((m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) &
-                    WS_SEQ_MASK) != want)
-              __builtin_amdgcn_s_sleep(1);
-            W.old = v3(sh->ox[ix], sh->oy[ix], sh->oz[ix]);
-            wdir = v3(sh->dx[ix], sh->dy[ix], sh->dz[ix]);
-            W.slen = sh->sl[ix];
-            wmeta = m;
-            __hip_atomic_store(&sh->meta[ix], want | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            // the start cell, as the photon computed it from the same start (update_grids :401-415)
-            W.xcell = cell_of<GM>(W.old.x, K.nx, K.xmax, K.inv2x, K.fex);
-            W.ycell = cell_of<GM>(W.old.y, K.ny, K.ymax, K.inv2y, K.fey);
-            W.zcell = cell_of<GM>(W.old.z, K.nz, K.zmax, K.inv2z, K.fez);
-            W.sd = 0.0; W.dda_it = 0;
-            W.seg = true; W.tflag = false; W.fault = false;
-          }
+      }
+      if (pend) {
+        const uint32_t ix = tk & (WS_RING - 1);
+        const uint32_t m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the field loads stay after the meta load)
+        const V3 o = v3(sh->ox[ix], sh->oy[ix], sh->oz[ix]);
+        const V3 dd = v3(sh->dx[ix], sh->dy[ix], sh->dz[ix]);
+        const double l = sh->sl[ix];
+        if ((m & WS_SEQ_MASK) == ws_tick(tk)) {
+          __hip_atomic_store(&sh->meta[ix], ws_tick(tk) | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          W.old = o;
+          wdir = dd;
+          W.slen = l;
+          wmeta = m;
+          // the start cell, as the photon computed it from the same start (update_grids :401-415)
+          W.xcell = cell_of<GM>(W.old.x, K.nx, K.xmax, K.inv2x, K.fex);
+          W.ycell = cell_of<GM>(W.old.y, K.ny, K.ymax, K.inv2y, K.fey);
+          W.zcell = cell_of<GM>(W.old.z, K.nz, K.zmax, K.inv2z, K.fez);
+          W.sd = 0.0; W.dda_it = 0;
+          W.seg = true; W.tflag = false; W.fault = false;
+          pend = false;
         }
       }
       const uint64_t am = __ballot(W.seg);
+      WSDIAG(WD_WITERS, 1);
+      WSDIAG(WD_WIDLE, am ? 0 : 1);
+      WSDIAG(WD_WBUSY, __popcll(am));
+      WSDIAG(WD_WPEND, __popcll(__ballot(pend)));
       if (!am) {
-        // nothing to walk: done once every photon wave has finished and every ticket is taken
-        if (ws_load(&sh->alive) == 0 && ws_load(&sh->head) == ws_load(&sh->tail)) break;
+        // nothing to walk: once every photon wave has finished, the final tail is known and the
+        // tickets past it are never reserved; done when no lane holds an earlier one
+        if (ws_load(&sh->alive) == 0) {
+          const uint32_t T = ws_load(&sh->tail);
+          if (pend && (int32_t)(tk - T) >= 0) pend = false;  // (a ticket nobody will write)
+          if (!__ballot(pend) && (int32_t)(ws_load(&sh->head) - T) >= 0) break;
+        }
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
@@ -607,7 +791,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
     }
     close_buckets(K, C, WB, w_dep - overflow, overflow);
-    // ---- per-wave counters (walker side) ---------------------------------------------------
+  }
+  // ---- per-wave counters (each role adds its own) ------------------------------------------
+  {
     unsigned long long* const counters = C->counters;
     const uint32_t hz = wave_sum_u32(hazards);
     if (lane_id == 0) {
@@ -615,13 +801,25 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         atomicAdd(C->dep_ctl + 5, hz);
         atomicAdd(C->lean_hazards, (unsigned long long)hz);
       }
+      if (C->dep_ctl && sh->wctr[wv][LC_UPD]) atomicAdd(C->dep_ctl + 6, sh->wctr[wv][LC_UPD]);  // segments
       if (counters) {
-        if (w_dep) atomicAdd(counters + 5, (unsigned long long)w_dep);
-        if (hz) atomicAdd(counters + 11, (unsigned long long)hz);
-        atomicAdd(counters + 15, (unsigned long long)w_iters);
+        const uint32_t* c = sh->wctr[wv];
+        const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
+                                             w_dep,         c[LC_UPD],     c[LC_TAU],      0u,             0u,
+                                             0u,            c[LC_FAULTS] + hz, c[LC_DRAWS], 0u,             c[LC_ESCAPED],
+                                             w_iters};
+        for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
+          if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
       }
+      double* const nscatt = C->nscatt;
+      if (nscatt && sh->wctr[wv][LC_SCATTERS]) atomic_add_nr(nscatt, (double)sh->wctr[wv][LC_SCATTERS]);
     }
   }
+#ifdef SMCRT_DIAG
+  if (lane_id == 0)
+    for (int i = 0; i < WD_N - WD_WITERS; ++i)
+      if (wd[i]) atomicAdd(&::g_diag[WD_WITERS + i], (unsigned long long)wd[i]);
+#endif
   __syncthreads();  // every wave of the block is done depositing
   close_block_buckets(K, C, bstate);
 }

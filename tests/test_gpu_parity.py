@@ -374,13 +374,10 @@ def test_multi_launch_pool_reuse():
     assert np.array_equal(res.absorb, cpu.absorb)
 
 
-@pytest.mark.parametrize("ltab", ["0", "1"])
-def test_vessels_capsule_net(ltab, monkeypatch):
+def test_vessels_capsule_net():
     """M4 (build-defined): a capsule tree as separate top-level SDFs in a
-    dermis box, uniform source over the top face: a deep SDF array (49 SDFs per EVAL). With
-    SMCRT_CULL_LTAB=1 the culled EVALs read the capsules' parameters from LDS records instead
-    of the node table (cull.h CULL_LTAB); both must equal the oracle bit for bit."""
-    monkeypatch.setenv("SMCRT_CULL_LTAB", ltab)
+    dermis box, uniform source over the top face: a deep SDF array (49 SDFs per EVAL),
+    bit for bit against the oracle."""
     sc = builders.synthetic_vessels(n_capsules=48)
     g = scene.grid(48, 40, 44, 0.16, 0.09, 0.13)
     src = scene.uniform_source((-0.16, -0.09, 0.1299), (0.32, 0.0, 0.0), (0.0, 0.18, 0.0), (0.0, 0.0, -1.0))
