@@ -381,9 +381,6 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 // Sharing the words per block (round 2: per wave before) keeps 4x fewer buckets open, so
 // their partly written cache lines fit in L2 and leave it whole.
 // The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
-#ifndef SMCRT_REC_NT
-#define SMCRT_REC_NT 0
-#endif
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
 #ifndef SMCRT_BUCKET_BATCH
@@ -493,19 +490,7 @@ __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __r
     const uint32_t b = pos < BUCKET_RECORDS ? bw_cur(w) : bw_next(w);
     const bool slot = todo && pos < 2 * BUCKET_RECORDS;
     const bool ok = slot && b < K.n_buckets;
-#ifndef SMCRT_ABL_NO_RECSTORE  // timing ablation only: slots are claimed, records not written
-    if (ok) {
-      unsigned long long* const at = K.rec_pool + ((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1));
-#if SMCRT_REC_NT == 2  // experiment: every record store non-temporal
-      __builtin_nontemporal_store(pack_record(vox, val), at);
-#elif SMCRT_REC_NT == 1  // experiment: the store that completes a 128-B line non-temporal
-      if ((pos & 15u) == 15u) __builtin_nontemporal_store(pack_record(vox, val), at);
-      else *at = pack_record(vox, val);
-#else
-      *at = pack_record(vox, val);
-#endif
-    }
-#endif
+    if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
     const bool claim = todo && pos == BUCKET_RECORDS;
     const bool spill = slot && !ok;
     const bool wait = todo && !slot;  // both buckets full: a claim is pending in another wave
@@ -624,47 +609,16 @@ __global__ __launch_bounds__(BIN_THREADS) void bk_place(const uint32_t* __restri
 
 // ---- bk_reduce: one piece (buckets of one tile) per block, fp64 LDS sums into jmean --------
 // (blockDim.x must be 1024)
-#ifndef SMCRT_RED_STAGE
-#define SMCRT_RED_STAGE 512
-#endif
-#ifndef SMCRT_RED_UNROLL
-#define SMCRT_RED_UNROLL 16
-#endif
-constexpr uint32_t REDUCE_STAGE_BUCKETS = SMCRT_RED_STAGE;  // <= 1024 (one id per thread)
-constexpr int RED_UNROLL = SMCRT_RED_UNROLL;                // record loads in flight per thread
-// bk_reduce reads each record once. SMCRT_RED_NT=1 gives the loads the non-temporal hint, meant
-// to keep the fold's 25 GB stream from evicting the partly written bucket lines of the transport
-// kernels beside it: measured and not adopted (M1 same box: 210.0/210.3 vs 210.2/210.6 M
-// photons/s, the transport kernel's HBM writes 38.008 GB per launch either way,
-// profiles/r03_s3/nt_ab.txt), so the write amplification is not the fold's doing
-#ifndef SMCRT_RED_NT
-#define SMCRT_RED_NT 0
-#endif
-__device__ __forceinline__ unsigned long long red_load(const unsigned long long* p) {
-#if SMCRT_RED_NT
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
-}
-#ifndef SMCRT_RED_WAVE
-#define SMCRT_RED_WAVE 1
-#endif
-#ifndef SMCRT_RED_GROUP
-#define SMCRT_RED_GROUP 4
-#endif
-#ifndef SMCRT_RED_THREADS
-#define SMCRT_RED_THREADS 1024
-#endif
-constexpr uint32_t RED_THREADS = SMCRT_RED_THREADS;  // bk_reduce's block size
-#if SMCRT_RED_WAVE
+constexpr uint32_t RED_THREADS = 1024;  // bk_reduce's block size
 // One wave per bucket (round 4): wave w of the block takes buckets w, w + 16, w + 32, ... of the
 // piece, RED_GROUP at a time; a bucket's id and fill are scalar loads and its 256 records four
 // coalesced 512-B loads per wave. The next group's records are loaded before this group's LDS
 // adds are issued (software pipeline), so each wave keeps 2 * RED_GROUP * 4 records per lane
 // in flight and its memory latency overlaps its own LDS atomics; no ids/fills staging in LDS
 // and no block barrier inside a piece. Sums are the same fp64 LDS adds in a different order.
-constexpr int RED_GROUP = SMCRT_RED_GROUP;
+// (Measured and removed in round 5: a block-wide staged variant with 16 loads in flight per
+// thread, 5 % slower; non-temporal record loads, no change, profiles/r03_s3/nt_ab.txt.)
+constexpr int RED_GROUP = 4;
 __global__ __launch_bounds__(RED_THREADS) void bk_reduce(const unsigned long long* __restrict__ pool,
                                                   const uint32_t* __restrict__ order,
                                                   const uint32_t* __restrict__ bucket_fill,
@@ -695,7 +649,7 @@ __global__ __launch_bounds__(RED_THREADS) void bk_reduce(const unsigned long lon
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t slot = lane + 64u * (uint32_t)r;
-          x[4 * u + r] = slot < f ? red_load(base + slot) : ~0ull;
+          x[4 * u + r] = slot < f ? base[slot] : ~0ull;
         }
       }
     };
@@ -723,72 +677,6 @@ __global__ __launch_bounds__(RED_THREADS) void bk_reduce(const unsigned long lon
   }
   if (threadIdx.x == 0 && busy) atomicAdd(busy, __builtin_amdgcn_s_memrealtime() - t_start);
 }
-#else
-__global__ __launch_bounds__(1024) void bk_reduce(const unsigned long long* __restrict__ pool,
-                                                  const uint32_t* __restrict__ order,
-                                                  const uint32_t* __restrict__ bucket_fill,
-                                                  const Piece* __restrict__ pieces,
-                                                  const uint32_t* __restrict__ dep_ctl, uint64_t n_voxels,
-                                                  double* __restrict__ jmean, unsigned long long* __restrict__ busy) {
-  // busy: a running total of this kernel's workgroup run times (wall-clock counter ticks), so
-  // the host reports the fold's own work, not the time it queues behind transport launches
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  __shared__ double acc[TILE_VOXELS];
-  // bucket ids and fills of a stage, double-buffered: the next stage's ids are loaded while
-  // this stage's records are summed, and one barrier per stage suffices
-  __shared__ uint32_t ids[2][REDUCE_STAGE_BUCKETS], fills[2][REDUCE_STAGE_BUCKETS];
-  const uint32_t n_pieces = dep_ctl[2];
-  for (uint32_t pi = blockIdx.x; pi < n_pieces; pi += gridDim.x) {
-    const Piece p = pieces[pi];
-    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) acc[i] = 0.0;
-    uint32_t nid = 0;
-    if (threadIdx.x < REDUCE_STAGE_BUCKETS && threadIdx.x < p.count) nid = order[p.start + threadIdx.x];
-    uint32_t buf = 0;
-    for (uint32_t k0 = 0; k0 < p.count; k0 += REDUCE_STAGE_BUCKETS, buf ^= 1u) {
-      const uint32_t kn = p.count - k0 < REDUCE_STAGE_BUCKETS ? p.count - k0 : REDUCE_STAGE_BUCKETS;
-      if (threadIdx.x < kn) {
-        ids[buf][threadIdx.x] = nid;
-        fills[buf][threadIdx.x] = bucket_fill[nid];
-      }
-      __syncthreads();  // (also orders the previous use of this buffer, two stages ago)
-      const uint32_t k1 = k0 + REDUCE_STAGE_BUCKETS;
-      if (threadIdx.x < REDUCE_STAGE_BUCKETS && k1 + threadIdx.x < p.count) nid = order[p.start + k1 + threadIdx.x];
-      const uint32_t* const sid = ids[buf];
-      const uint32_t* const sfill = fills[buf];
-      const uint32_t slots = kn << BUCKET_SHIFT;
-      uint32_t s = threadIdx.x;
-      for (; s + (RED_UNROLL - 1) * 1024 < slots; s += RED_UNROLL * 1024) {
-        unsigned long long x[RED_UNROLL];
-        bool v[RED_UNROLL];
-#pragma unroll
-        for (int k = 0; k < RED_UNROLL; ++k) {
-          const uint32_t j = s + k * 1024, kb = j >> BUCKET_SHIFT, r = j & (BUCKET_RECORDS - 1);
-          v[k] = r < sfill[kb];
-          x[k] = v[k] ? red_load(pool + ((uint64_t)sid[kb] << BUCKET_SHIFT) + r) : 0ull;
-        }
-#pragma unroll
-        for (int k = 0; k < RED_UNROLL; ++k)
-          if (v[k]) atomicAdd(&acc[(uint32_t)(x[k] >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x[k]));
-      }
-      for (; s < slots; s += 1024) {
-        const uint32_t kb = s >> BUCKET_SHIFT, r = s & (BUCKET_RECORDS - 1);
-        if (r < sfill[kb]) {
-          const unsigned long long x = red_load(pool + ((uint64_t)sid[kb] << BUCKET_SHIFT) + r);
-          atomicAdd(&acc[(uint32_t)(x >> 32) & (TILE_VOXELS - 1)], (double)__uint_as_float((uint32_t)x));
-        }
-      }
-    }
-    __syncthreads();
-    const uint64_t base = (uint64_t)p.tile << TILE_SHIFT;
-    for (uint32_t i = threadIdx.x; i < TILE_VOXELS; i += blockDim.x) {
-      const double a = acc[i];
-      if (a != 0.0 && base + i < n_voxels) atomic_add_nr(jmean + base + i, a);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0 && busy) atomicAdd(busy, __builtin_amdgcn_s_memrealtime() - t_start);
-}
-#endif
 
 // ---- bin_reduce: one tile piece per block, fp64 LDS sums added into jmean ----------------
 // (blockDim.x must be 1024)

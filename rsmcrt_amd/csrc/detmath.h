@@ -52,15 +52,7 @@ struct Rng {
   __device__ __forceinline__ double next(uint32_t key0, uint32_t key1) {
     const uint32_t d = draws++;
     if (d & 1u) return cached;
-#ifdef SMCRT_ABL_CHEAP_RNG  // timing ablation only: not the engine's stream
-    Philox4 o;
-    {
-      uint32_t a = (d >> 1) * 0x9E3779B9u ^ pid_lo, b = pid_hi ^ key0 ^ (a * 0x85EBCA6Bu);
-      o.v[0] = a ^ (b >> 13); o.v[1] = b * 0xC2B2AE35u; o.v[2] = a * 0x27D4EB2Fu ^ b; o.v[3] = (a + b) * 0x165667B1u;
-    }
-#else
     const Philox4 o = philox4x32_10(d >> 1, 0u, pid_lo, pid_hi, key0, key1);
-#endif
     const uint64_t u0 = ((uint64_t)o.v[1] << 32) | o.v[0];
     const uint64_t u1 = ((uint64_t)o.v[3] << 32) | o.v[2];
     cached = (double)(u1 >> 11) * 0x1.0p-53;
@@ -93,18 +85,6 @@ __device__ __forceinline__ double ieee_div_tail_f64(double n, double d, double r
 }
 
 // natural log: fdlibm e_log.c algorithm (identical operation sequence to the oracle)
-#ifdef SMCRT_ABL_FAST_MATH  // timing ablation only: fp32 hardware log/sin/cos, not bit-exact
-__device__ __forceinline__ double det_log(double x) { return (double)__logf((float)x); }
-__device__ __forceinline__ void det_sincos(double x, double* s, double* c) {
-  float fs, fc;
-  __sincosf((float)x, &fs, &fc);
-  *s = fs; *c = fc;
-}
-__device__ __forceinline__ void det_sincos_any(double x, double* s, double* c) { det_sincos(x, s, c); }
-#define SMCRT_HAVE_FAST_MATH 1
-#endif
-
-#ifndef SMCRT_HAVE_FAST_MATH
 __device__ inline double det_log(double x) {
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
                two54 = 1.80143985094819840000e+16, Lg1 = 6.666666666666735130e-01,
@@ -213,7 +193,6 @@ __host__ __device__ __forceinline__ void det_sincos_any(double x, double* s, dou
   det_sincos(fabs(x), s, c);
   if (x < 0.0) *s = -*s;
 }
-#endif  // SMCRT_HAVE_FAST_MATH
 
 // atan (fdlibm s_atan.c), for the fibre detector's acceptance angle (detectors.f90:386).
 

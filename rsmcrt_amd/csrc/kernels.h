@@ -216,10 +216,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
       if (__ballot(L.st != ST_IDLE) == 0) break;
     }
 
-#ifdef SMCRT_DIAG_STATES
-#ifdef SMCRT_DIAG_TAIL  // only the trips of waves with at most 4 photons left (the launch's tail)
-    if (__popcll(__ballot(L.st != ST_IDLE)) <= 4)
-#endif
+#ifdef SMCRT_DIAG_STATES  // (diagnostic builds: lane states per trip into g_diag[0..66])
     {
       const uint32_t cls = (L.seg ? 32u : 0u) + (L.st & 31u);
       for (uint32_t c = 0; c < 64; ++c) {  // wave-uniform loop: count lanes per class
@@ -609,29 +606,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
     // ---- DDA phase: voxel crossings of pending deposit segments ------------------------
     // Placed after the program points that start segments (P3, P4) and before the ones that
     // consume them (P5), so a short segment is started, walked and finished in one trip.
-#ifdef SMCRT_ABL_NO_DDA  // timing ablation only: segments end at once, nothing is deposited
-    L.seg = false;
-#endif
     if (__ballot(L.seg)) {  // wave-uniform, so deposit records can be wave-compacted
 #pragma unroll
       for (int k = 0; k < SMCRT_DDA_PER_ITER; ++k) {
-#if SMCRT_DDA_MIN_ITERS < SMCRT_DDA_PER_ITER
-        // past the first crossings, walk on only while enough lanes still have a segment
-        if (k >= SMCRT_DDA_MIN_ITERS && __popcll(__ballot(L.seg)) < SMCRT_DDA_MIN_LANES) break;
-#endif
         bool dep = false;
         uint32_t vox = 0;
         double val = 0.0;
         if (L.seg) dda_step<GM>(K, L, L.dir, xf, yf, zf, dep, vox, val, L.weight);
         w_dep += __popcll(__ballot(dep));
-#ifdef SMCRT_ABL_NO_EMIT  // timing ablation only: deposits are computed but dropped
-        if (binned) { if (__ballot(dep) == 0x123ull) emit_deposits(K, C, W, dep, vox, val, overflow, whist); }
-#else
         if (binned) {
           if (K.bucket_tiles) emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
           else emit_deposits(K, C, W, dep, vox, val, overflow, whist);
         }
-#endif
         else if (dep) {
           double* const jm = C->jmean;
           if (jm) atomic_add_nr(jm + vox, val);

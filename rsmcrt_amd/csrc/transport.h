@@ -37,25 +37,14 @@ constexpr int64_t MAX_DDA_ITERS = 10000000;
 constexpr int MAX_RENORM_ITERS = 64;
 constexpr int64_t MAX_INTERACTIONS = 100000000;
 
-#ifndef SMCRT_DDA_PER_ITER
+// transport_kernel walks at most this many crossings of a lane's segment per trip (round 2:
+// more while many lanes still walk was box-dependent, profiles/r02_s3/dda_schedule_ab.txt)
 #define SMCRT_DDA_PER_ITER 3
-#endif
-// Crossings past the first SMCRT_DDA_MIN_ITERS of a trip run only while at least
-// SMCRT_DDA_MIN_LANES lanes of the wave still have a segment.
-#ifndef SMCRT_DDA_MIN_ITERS
-#define SMCRT_DDA_MIN_ITERS SMCRT_DDA_PER_ITER
-#endif
-#ifndef SMCRT_DDA_MIN_LANES
-#define SMCRT_DDA_MIN_LANES 1
-#endif
-// A wave runs the photon-event phase once this many lanes wait for it (or no lane has
-// anything else to do).
-#ifndef SMCRT_FETCH_CHUNK
+// photons a wave takes from the work queue with one atomic
 #define SMCRT_FETCH_CHUNK 64
-#endif
-#ifndef SMCRT_EVENT_LANES
+// transport_kernel runs its photon-event phase once this many lanes wait for it (or no lane
+// has anything else to do)
 #define SMCRT_EVENT_LANES 16
-#endif
 
 // Optical properties of a top-level SDF, derived as init_mono does
 // (opticalProperties.f90:107-125).
@@ -815,11 +804,7 @@ __device__ __forceinline__ void dda_step_r(const KParams& K, S& L, const V3 dir,
   const double rcp = lx ? rx : (ly ? ry : rz);
   const bool fast = fast0 && fabs(num) >= 0x1.0p-500;
   double dcell;
-#ifdef SMCRT_ABL_NO_SLOWDIV  // register-pressure analysis builds only (not exact)
-  if (true) {
-#else
   if (fast) {
-#endif
     dcell = ieee_div_tail_f64(num, den, rcp);  // == num / den bit for bit
   } else {
     double dx = -999.0, dy = -999.0, dz = -999.0;

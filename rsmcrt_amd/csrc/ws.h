@@ -19,14 +19,15 @@
 //     owner photon's slot, exactly as lean_kernel's walkers do.
 //   * event waves (round 5, session 2) run the photons' interactions: the albedo roulette,
 //     scatter and the next tauint2 entry (kernelsMod.f90:1958-1975, photon.f90:1045-1103,
-//     inttau2.f90:48-60), and the tauint2 entry after an emission. A photon with such an event
+//     inttau2.f90:48-60), the tauint2 entry after an emission, and the emission itself
+//     (kernelsMod.f90:1937-1945 with the source's draws, photon.f90:311-710). A photon with such an event
 //     writes its direction, RNG state and layer into its slot, queues its lane in the block's
 //     event queue and waits; an event lane takes the queued owner, runs the event on the
 //     owner's values with the owner's own Philox stream and writes the results back. The event
 //     code so runs on full waves: in lean_kernel a wave ran its events once 20 of its lanes
-//     waited (0.52 phases a trip with 21 lanes, 22 % of the wave time). Emission, completion,
-//     the rare terminal interactions and every event of test_kernel runs (moments) stay in the
-//     photon waves, batched as in lean_kernel.
+//     waited (0.52 phases a trip with 21 lanes, 22 % of the wave time). Completion, the rare
+//     terminal interactions and every event of test_kernel runs (moments) stay in the photon
+//     waves, batched as in lean_kernel.
 // A segment's walk is the pure function of (start, direction, length) it is in lean_kernel
 // (the start cell is recomputed from the start with the same cell_of), the deferred/synchronous
 // rule and the hazard accounting are lean.h's, and the photon side is lean_kernel's code, so the
@@ -98,7 +99,9 @@ struct WsShared {
   uint32_t wctr[WS_WAVES][LC_N];                 // per-wave counters
   // the event queue (see "Event waves" above): per photon lane an in/out slot, and a queue of
   // owner lanes with the ring's sequence lock
-  double ev_dir[3][WS_NPL];   // in: direction; out: the scattered direction
+  double ev_dir[3][WS_NPL];   // in: direction; out: the scattered (or emitted) direction
+  double ev_pos[3][WS_NPL];   // out: the emitted position
+  unsigned long long ev_cells[WS_NPL];  // out: the emitted cells (lean_pack)
   double ev_cached[WS_NPL];   // in/out: the RNG's cached half block
   double ev_tau[WS_NPL];      // out: the new optical depth
   uint32_t ev_pid[2][WS_NPL]; // in: photon index words
@@ -109,7 +112,7 @@ struct WsShared {
   uint32_t ev_head, ev_tail;  // event tickets: held by event lanes / reserved by photon waves
   uint32_t alive;
 };
-constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u;  // event kinds (ev_code bits 16-17)
+constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u, WS_EV_EMIT = 3u;  // event kinds (ev_code bits 16-17)
 
 __device__ __forceinline__ void ws_count(WsShared* sh, int c) {
   const uint64_t m = __ballot(1);
@@ -126,6 +129,11 @@ __device__ __forceinline__ uint32_t ws_load(uint32_t* p) {
 }
 
 
+#ifdef SMCRT_ASM_MARKERS  // analysis builds (tools/isa_phases.py --kernel ws): region boundaries in the ISA
+#define WS_MARK(i) asm volatile("; @@LPHASE " #i)
+#else
+#define WS_MARK(i) do {} while (0)
+#endif
 #ifdef SMCRT_DIAG
 // Diagnostic builds (-DSMCRT_DIAG): wave-uniform tallies of the schedule in g_diag[20..39]
 // (kernels.h), printed per launch by the host ([diag-ws]).
@@ -253,7 +261,17 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           P.clr(LF_EVQ);
           P.rng.draws = sh->ev_draws[pl];
           P.rng.cached = sh->ev_cached[pl];
-          if (code & EV_ABSORB) {  // absorbed: recordWeight once the cells are in
+          if (P.st == ST_EMIT) {  // the emitted photon (its tauint2 entry follows the layer search)
+            P.pos = v3(sh->ev_pos[0][pl], sh->ev_pos[1][pl], sh->ev_pos[2][pl]);
+            P.dir = v3(sh->ev_dir[0][pl], sh->ev_dir[1][pl], sh->ev_dir[2][pl]);
+            P.clr(LF_TFLAG);
+            P.layer = (int32_t)(code & 0xFFFFu);
+            const unsigned long long w = sh->ev_cells[pl];
+            P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
+            P.set(LF_CELLS);
+            if (code & EV_RUNAWAY) { P.set(LF_FAULT); P.st = ST_DONE; }  // (emission retries exhausted)
+            else { P.st = ST_LAYER; P.set(LF_PEND); }
+          } else if (code & EV_ABSORB) {  // absorbed: recordWeight once the cells are in
             P.set(LF_TFLAG);
             P.st = ST_ABSORB;
           } else {  // scattered (or after an emission), then the tauint2 entry
@@ -473,7 +491,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const bool qev = free_ && !test_kernel && !P.has(LF_EVQ) &&
                          ((P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT)) &&
                            WLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS) ||
-                          P.st == ST_T2);
+                          P.st == ST_T2 || P.st == ST_EMIT);
         const uint64_t qm = __ballot(qev);
         if (qm) {
           const int first = __builtin_ctzll(qm);
@@ -490,7 +508,12 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             sh->ev_cached[pl] = P.rng.cached;
             sh->ev_pid[0][pl] = P.rng.pid_lo; sh->ev_pid[1][pl] = P.rng.pid_hi;
             sh->ev_draws[pl] = P.rng.draws;
-            sh->ev_code[pl] = (uint32_t)P.layer | ((P.st == ST_INTERACT ? WS_EV_INTERACT : WS_EV_TAU) << 16);
+            if (P.st == ST_EMIT) {  // kernelsMod.f90:1937-1945: a fresh packet
+              P.clr(LF_FAULT); P.layer = 0;
+              WLU(LL_STATUS) = 0; WLU(LL_NSCATT) = 0; WLU(LL_INTER) = 0;
+            }
+            sh->ev_code[pl] = (uint32_t)P.layer |
+                              ((P.st == ST_INTERACT ? WS_EV_INTERACT : (P.st == ST_T2 ? WS_EV_TAU : WS_EV_EMIT)) << 16);
             __hip_atomic_store(&sh->evq[ix], pl | ws_tick(t), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             P.set(LF_EVQ);
           }
@@ -671,7 +694,25 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const int32_t layer = (int32_t)(code & 0xFFFFu);
         uint32_t res = 0;
         bool tau_entry = (code >> 16) == WS_EV_TAU;
-        if ((code >> 16) == WS_EV_INTERACT) {  // kernelsMod.f90:1958-1975
+        if ((code >> 16) == WS_EV_EMIT) {  // kernelsMod.f90:1937-1945 (emit until the cell is in the grid)
+          Lane L;
+          L.rng = rg; L.xcell = L.ycell = L.zcell = 0; L.layer = 0; L.tflag = false;
+          emit<GM, false>(K, C, L, 0u);
+          int64_t tries = 0;
+          bool fault = false;
+          while (cell_out(K, L)) {
+            if (++tries > MAX_EMIT_TRIES) { fault = true; break; }
+            ws_count(sh, LC_RETRIES);
+            emit<GM, false>(K, C, L, 0u);
+          }
+          rg = L.rng;
+          sh->ev_pos[0][o] = L.pos.x; sh->ev_pos[1][o] = L.pos.y; sh->ev_pos[2][o] = L.pos.z;
+          sh->ev_dir[0][o] = L.dir.x; sh->ev_dir[1][o] = L.dir.y; sh->ev_dir[2][o] = L.dir.z;
+          sh->ev_cells[o] = lean_pack(L.xcell, L.ycell, L.zcell);
+          if (!fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE) && C->emission)
+            atomic_add_nr(C->emission + lin(K, L.xcell, L.ycell, L.zcell), 1.0);
+          res = (fault ? EV_RUNAWAY : 0u) | ((uint32_t)L.layer & 0xFFFFu);
+        } else if ((code >> 16) == WS_EV_INTERACT) {  // kernelsMod.f90:1958-1975
           const TopProps pr = props[layer - 1];
           const double ran = rg.next(K.key0, K.key1);
           ++sh->lu[LL_INTER][o];
@@ -710,6 +751,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     W.dda_it = 0;
     W.seg = W.tflag = W.fault = false;
     V3 wdir = v3(0.0, 0.0, 0.0);
+    // the direction's refined reciprocals (ieee_rcp_f64, the first half of the IEEE division
+    // sequence, detmath.h), formed once per segment when it is taken instead of at every crossing
+    V3 wrcp = v3(0.0, 0.0, 0.0);
     uint32_t wmeta = 0;
     BucketLog WB;
     WB.next = WB.end = 0;
@@ -723,6 +767,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     bool pend = false;
     uint32_t tk = 0;
     for (;; ++w_iters) {
+      WS_MARK(11);
       const uint64_t cm = __ballot(!W.seg && !pend);
       if (cm) {
         const int first = __builtin_ctzll(cm);
@@ -745,6 +790,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           __hip_atomic_store(&sh->meta[ix], ws_tick(tk) | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           W.old = o;
           wdir = dd;
+          wrcp = v3(ieee_rcp_f64(dd.x), ieee_rcp_f64(dd.y), ieee_rcp_f64(dd.z));
           W.slen = l;
           wmeta = m;
           // the start cell, as the photon computed it from the same start (update_grids :401-415)
@@ -773,12 +819,15 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         continue;
       }
       // ---- one crossing of every held segment (dda_step: wall_dist, deposit, update_pos) ----
+      WS_MARK(12);
       bool dep = false;
       uint32_t vox = 0;
       double val = 0.0;
-      if (W.seg) dda_step<GM>(K, W, wdir, xf, yf, zf, dep, vox, val, 1.0);
+      if (W.seg) dda_step_r<GM>(K, W, wdir, wrcp, xf, yf, zf, dep, vox, val, 1.0);
       w_dep += __popcll(__ballot(dep));
+      WS_MARK(13);
       emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+      WS_MARK(14);
       // a finished segment: its cells and flags to the owner's slot, then the slot is free
       if ((am >> lane_id & 1ull) && !W.seg) {
         const uint32_t owner = wmeta & 511u, slot = (wmeta >> 9) & 3u;

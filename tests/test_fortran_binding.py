@@ -107,7 +107,10 @@ def test_example_multi_gpu_matches_single(lib_path, tmp_path):
         ctr = re.findall(r"counter (\d+) = (\d+)", o)
         return dict(ctr), re.search(r"nscatt =\s*(\S+)", o).group(1), float(re.search(r"jmean normalised\) =\s*(\S+)", o).group(1))
     (c0, n0, j0), (c1, n1, j1) = parse(outs[0]), parse(outs[1])
-    assert len(c0) == 16 and c0 == c1 and n0 == n1, outs
+    assert len(c0) == 16 and n0 == n1, outs
+    # (the engine counters, abi.ENGINE_COUNTERS, describe the schedule, not the photons)
+    eng = {str(abi.CTR[k]) for k in abi.ENGINE_COUNTERS}
+    assert {k: v for k, v in c0.items() if k not in eng} == {k: v for k, v in c1.items() if k not in eng}, outs
     assert abs(j0 - j1) <= 1e-9 * abs(j0)
 
 

@@ -19,6 +19,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NAMES = {1: "fetch", 2: "eval", 3: "p3p4", 4: "handout", 5: "walk", 6: "p5p6", 7: "p7events", 8: "p8+loop"}
+# ws_kernel (ws.h WS_MARK): the walker loop's regions
+WS_NAMES = {11: "w:claim+take", 12: "w:dda", 13: "w:emit", 14: "w:finish+loop", 0: "rest"}
 
 
 def classify(op):
@@ -75,7 +77,8 @@ def main(argv):
                     "-DSMCRT_ASM_MARKERS", "-o", out, os.path.join(ROOT, "rsmcrt_amd", "csrc", "kinst.hip")] + extra,
                    check=True, cwd="/tmp", stderr=subprocess.DEVNULL)
     s = open(out).read()
-    pat = r"^(_ZN5smcrt11lean_kernel\w+):" if kern == "lean" else r"^(_Z16transport_kernel\w+):"
+    pat = {"lean": r"^(_ZN5smcrt11lean_kernel\w+):", "ws": r"^(_ZN5smcrt9ws_kernel\w+):"}.get(
+        kern, r"^(_Z16transport_kernel\w+):")
     m = re.search(pat, s, re.M)
     start = m.start()
     end = s.index(".Lfunc_end", start)
@@ -88,7 +91,11 @@ def main(argv):
         t = line.strip()
         mk = re.match(r"; @@LPHASE (\d+)", t)
         if mk:
-            phase = int(mk.group(1)) % 8 + 1  # code after marker i belongs to phase i+1 (8 wraps to 1)
+            i = int(mk.group(1))
+            # lean: code after marker i belongs to phase i+1 (8 wraps to 1); ws: region i starts at marker i
+            phase = i if kern == "ws" else i % 8 + 1
+            if kern == "ws" and i == 14:
+                phase = 14
             continue
         if not t or t.startswith((".", ";", "_")) or t.endswith(":"):
             continue
@@ -103,7 +110,7 @@ def main(argv):
     for p in sorted(per):
         c = per[p]
         tot.update(c)
-        print(NAMES.get(p, str(p)).ljust(10) + "".join(str(c[k]).rjust(12) for k in classes) + str(sum(c.values())).rjust(8))
+        print((WS_NAMES if kern == "ws" else NAMES).get(p, str(p)).ljust(10) + "".join(str(c[k]).rjust(12) for k in classes) + str(sum(c.values())).rjust(8))
     print("all".ljust(10) + "".join(str(tot[k]).rjust(12) for k in classes) + str(sum(tot.values())).rjust(8))
 
 
