@@ -70,7 +70,10 @@ namespace smcrt {
 #ifndef SMCRT_WS_SLOTS
 #define SMCRT_WS_SLOTS 2
 #endif
-constexpr int WS_WAVES = 8;
+#ifndef SMCRT_WS_WAVES
+#define SMCRT_WS_WAVES 8
+#endif
+constexpr int WS_WAVES = SMCRT_WS_WAVES;  // waves per block (8: two blocks per CU, 16: one)
 constexpr int WS_THREADS = 64 * WS_WAVES;
 constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (waves 0 .. WS_PW-1)
 constexpr int WS_EW = SMCRT_WS_EVENT_WAVES;   // event waves (next), the rest walk
