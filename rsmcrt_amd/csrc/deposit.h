@@ -381,6 +381,9 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 // Sharing the words per block (round 2: per wave before) keeps 4x fewer buckets open, so
 // their partly written cache lines fit in L2 and leave it whole.
 // The fold (bk_scan, bk_place, bk_reduce) lists the buckets of each tile and sums them in LDS.
+#ifndef SMCRT_REC6
+#define SMCRT_REC6 1
+#endif
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
 #ifndef SMCRT_BUCKET_BATCH
@@ -490,7 +493,18 @@ __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __r
     const uint32_t b = pos < BUCKET_RECORDS ? bw_cur(w) : bw_next(w);
     const bool slot = todo && pos < 2 * BUCKET_RECORDS;
     const bool ok = slot && b < K.n_buckets;
-    if (ok) K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
+    if (ok) {
+#if SMCRT_REC6
+      // 6-byte records (round 5): the bucket's tile is implied, so a record is its f32 value
+      // (first KiB of the bucket) and its 14-bit voxel within the tile (the next 512 B)
+      uint32_t* const bv = (uint32_t*)(K.rec_pool + ((uint64_t)b << BUCKET_SHIFT));
+      const uint32_t slot = pos & (BUCKET_RECORDS - 1);
+      bv[slot] = __float_as_uint((float)val);
+      ((uint16_t*)(bv + BUCKET_RECORDS))[slot] = (uint16_t)(vox & (TILE_VOXELS - 1));
+#else
+      K.rec_pool[((uint64_t)b << BUCKET_SHIFT) + (pos & (BUCKET_RECORDS - 1))] = pack_record(vox, val);
+#endif
+    }
     const bool claim = todo && pos == BUCKET_RECORDS;
     const bool spill = slot && !ok;
     const bool wait = todo && !slot;  // both buckets full: a claim is pending in another wave
@@ -646,11 +660,21 @@ __global__ __launch_bounds__(RED_THREADS) void bk_reduce(const unsigned long lon
           f = uniform(bucket_fill[id]);
         }
         const unsigned long long* __restrict__ base = pool + ((uint64_t)id << BUCKET_SHIFT);
+#if SMCRT_REC6
+        const uint32_t* __restrict__ bv = (const uint32_t*)base;
+        const uint16_t* __restrict__ bi = (const uint16_t*)(bv + BUCKET_RECORDS);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t slot = lane + 64u * (uint32_t)r;
+          x[4 * u + r] = slot < f ? ((unsigned long long)bi[slot] << 32) | bv[slot] : ~0ull;
+        }
+#else
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const uint32_t slot = lane + 64u * (uint32_t)r;
           x[4 * u + r] = slot < f ? base[slot] : ~0ull;
         }
+#endif
       }
     };
     const uint32_t ng = (p.count + NW * RED_GROUP - 1) / (NW * RED_GROUP);  // groups of the piece (wave 0's count)

@@ -1,7 +1,7 @@
 // kernel_ptrs.h — the transport kernel instantiations, reached through pointers.
 //
 // build.py compiles kinst.hip once per (LDS faces F, grid mode G) with -DKI_F=F -DKI_G=G, so
-// the 27 instantiations of transport_kernel and lean_kernel (kernels.h) build in parallel
+// the 27 instantiations of transport_kernel and ws_kernel (kernels.h, ws.h) build in parallel
 // instead of in one translation unit. Each object exports these getters; hipLaunchKernel and
 // the occupancy queries take the host stubs they return.
 #pragma once
@@ -9,14 +9,12 @@
 
 namespace smcrt {
 
-size_t kinst_lean_shared_bytes();  // sizeof(LeanShared), lean_kernel's static LDS
 size_t kinst_ws_shared_bytes();    // sizeof(WsShared), ws_kernel's static LDS
 int kinst_ws_threads();            // ws_kernel's block size
 int kinst_ws_photon_lanes();       // photon lanes per ws_kernel block
 
 #define SMCRT_KINST_DECL(F, G)                                                               \
   const void* kinst_transport_##F##_##G(int xsrc, int coop);                                 \
-  const void* kinst_lean_##F##_##G();                                                        \
   const void* kinst_ws_##F##_##G();                                                          \
   void kinst_diag_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6);
 SMCRT_KINST_DECL(0, 0)
@@ -39,16 +37,6 @@ inline const void* transport_kernel_ptr(bool lds_faces, int gm, bool xsrc, bool 
     case 3: return kinst_transport_1_0(x, c);
     case 4: return kinst_transport_1_1(x, c);
     default: return kinst_transport_1_2(x, c);
-  }
-}
-inline const void* lean_kernel_ptr(bool lds_faces, int gm) {
-  switch ((lds_faces ? 3 : 0) + gm) {
-    case 0: return kinst_lean_0_0();
-    case 1: return kinst_lean_0_1();
-    case 2: return kinst_lean_0_2();
-    case 3: return kinst_lean_1_0();
-    case 4: return kinst_lean_1_1();
-    default: return kinst_lean_1_2();
   }
 }
 inline const void* ws_kernel_ptr(bool lds_faces, int gm) {

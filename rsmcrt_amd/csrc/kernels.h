@@ -1,4 +1,4 @@
-// kernels.h — the transport kernels (transport_kernel here, lean_kernel in lean.h) as templates.
+// kernels.h — the transport kernels (transport_kernel here, ws_kernel in ws.h) as templates.
 //
 // Included only by kinst.hip, which build.py compiles once per (LDS faces, grid mode) pair so
 // the instantiations build in parallel; smcrt.hip reaches them through the pointers of

@@ -24,7 +24,6 @@ const void* KI_NAME(kinst_transport)(int xsrc, int coop) {
 }
 
 #if KI_F == 0 && KI_G == 0
-size_t kinst_lean_shared_bytes() { return sizeof(LeanShared); }  // (one object defines it)
 size_t kinst_ws_shared_bytes() { return sizeof(WsShared); }
 int kinst_ws_threads() { return WS_THREADS; }
 int kinst_ws_photon_lanes() { return (int)WS_NPL; }
@@ -32,7 +31,6 @@ int kinst_ws_photon_lanes() { return (int)WS_NPL; }
 
 const void* KI_NAME(kinst_ws)() { return (const void*)ws_kernel<KI_F != 0, KI_G>; }
 
-const void* KI_NAME(kinst_lean)() { return (const void*)lean_kernel<KI_F != 0, KI_G>; }
 
 void KI_NAME(kinst_diag)(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6) {
 #ifdef SMCRT_DIAG

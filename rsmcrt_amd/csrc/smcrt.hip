@@ -137,12 +137,10 @@ struct smcrt_scene {
   hipStream_t stream = nullptr;
   int grid_blocks = 0;
   int grid_blocks_x = 0;  // the XSRC (general emitter) instantiation
-  int grid_blocks_lean = 0;  // lean_kernel (lean.h)
-  int grid_blocks_ws = 0;    // ws_kernel (ws.h): the lean path with photon and walker waves
-  // the lean path runs ws_kernel (SMCRT_LEAN_WS=0: lean_kernel) when its LDS fits
-  bool ws_ok = false;
-  // lean_kernel serves this scene: equal refractive indices, no detectors, a few tops, bucketed
-  // deposition, axes below 2^20 cells (SMCRT_LEAN=0 keeps transport_kernel)
+  int grid_blocks_ws = 0;    // ws_kernel (ws.h): the lean path with photon, event and walker waves
+  // the lean path (ws_kernel) serves this scene: equal refractive indices, no detectors, a few
+  // tops, bucketed deposition, axes below 2^20 cells, its LDS fits (SMCRT_LEAN=0 keeps
+  // transport_kernel)
   bool lean_ok = false;
   // deferred lean-kernel segments that ended in tflag or an error stop (lean.h "hazards"):
   // running total d_queue[MAX_SLOTS + 3], reported by smcrt_scene_kernel_times and counted in
@@ -251,9 +249,7 @@ static const void* transport_fn(const smcrt_scene* s, bool xsrc) {
   return transport_kernel_ptr(s->lds_faces, s->grid_mode, xsrc, s->coop_lanes > 0);
 }
 
-// lean_kernel (lean.h) of this scene's face staging and grid mode
-static const void* lean_fn(const smcrt_scene* s) { return lean_kernel_ptr(s->lds_faces, s->grid_mode); }
-// its dynamic LDS: staged props + faces, then the block's bucket words
+// the lean path's dynamic LDS (ws_kernel): staged props + faces, then the block's bucket words
 static size_t lean_lds(const smcrt_scene* s) {
   return (s->lds_faces ? s->face_bytes : 0) + (size_t)2 * s->n_tiles * sizeof(uint32_t);
 }
@@ -648,17 +644,14 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     }
     s->grid_mode = f2 ? 2 : (p2 ? 1 : 0);
   }
-  {  // lean_kernel (lean.h): scenes without Fresnel events or detectors, a few tops
+  {  // the lean path (ws.h): scenes without Fresnel events or detectors, a few tops
     bool ok = n_dets == 0 && s->bucketed && s->coop_lanes == 0 && grid->nx < (1 << 20) - 2 &&
               grid->ny < (1 << 20) - 2 && grid->nz < (1 << 20) - 2;
     for (int32_t i = 1; ok && i < n_top; ++i) ok = s->h_props[i].n == s->h_props[0].n;
-    ok = ok && lean_lds(s) + kinst_lean_shared_bytes() <= 65536;
+    ok = ok && lean_lds(s) + kinst_ws_shared_bytes() <= 163840;
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
     s->lean_ok = ok && s->lean_mode != 0 && !s->nested;
-    const char* wsv = std::getenv("SMCRT_LEAN_WS");
-    s->ws_ok = s->lean_ok && !(wsv && std::string(wsv) == "0") &&
-               lean_lds(s) + kinst_ws_shared_bytes() <= 163840;
     const char* dm = std::getenv("SMCRT_DEBUG_LEAN_MARGIN");
     s->lean_debug = dm ? (std::string(dm) == "all" ? 2u : (std::string(dm) == "0" ? 1u : 0u)) : 0u;
   }
@@ -669,20 +662,15 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) s->wall_khz = khz;
   }
   if (s->lean_ok) {
-    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lean_fn(s), 256, lean_lds(s));
-    if (oe != hipSuccess || per_cu < 1) per_cu = 1;
-    s->grid_blocks_lean = cus * per_cu;
-  }
-  if (s->ws_ok) {
     hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ws_kernel_ptr(s->lds_faces, s->grid_mode),
                                                                  kinst_ws_threads(), lean_lds(s));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     s->grid_blocks_ws = cus * per_cu;
   }
   if (std::getenv("SMCRT_VERBOSE"))
-    std::fprintf(stderr, "[smcrt] scene: lean %d ws %d (blocks/CU %d, static LDS %zu + dynamic %zu B), lean grid %d, "
-                 "transport grid %d\n", (int)s->lean_ok, (int)s->ws_ok, s->grid_blocks_ws / std::max(1, cus),
-                 kinst_ws_shared_bytes(), lean_lds(s), s->grid_blocks_lean, s->grid_blocks);
+    std::fprintf(stderr, "[smcrt] scene: lean %d (ws blocks/CU %d, static LDS %zu + dynamic %zu B), transport grid %d\n",
+                 (int)s->lean_ok, s->grid_blocks_ws / std::max(1, cus), kinst_ws_shared_bytes(), lean_lds(s),
+                 s->grid_blocks);
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
     hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, 256, transport_lds(s, dep_words(s), x == 1));
@@ -913,27 +901,23 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   }
   const uint64_t waves_needed = (Ch.n_photons + 63) / 64;
   const uint64_t blocks_needed = (waves_needed + 3) / 4;
-  // lean_kernel (lean.h) when the scene and the run qualify: bucketed path-length deposition,
-  // unit weights (no survival bias), a plain source
+  // the lean path (ws_kernel, ws.h) when the scene and the run qualify: bucketed path-length
+  // deposition, unit weights (no survival bias), a plain source
   const bool lean = !xsrc && s->lean_ok && K.bucket_tiles && (K.flags & SMCRT_FLAG_PATHLENGTH) &&
                     !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
                     (s->lean_mode == 1 || !s->xps_measured || s->xps <= LEAN_MAX_XPS);
-  const bool ws = lean && s->ws_ok;
   const uint64_t ws_needed = (Ch.n_photons + kinst_ws_photon_lanes() - 1) / kinst_ws_photon_lanes();
   const int blocks = (int)std::min<uint64_t>(
-      (uint64_t)(ws ? s->grid_blocks_ws : (lean ? s->grid_blocks_lean : (xsrc ? s->grid_blocks_x : s->grid_blocks))),
-      std::max<uint64_t>(1, ws ? ws_needed : blocks_needed));
+      (uint64_t)(lean ? s->grid_blocks_ws : (xsrc ? s->grid_blocks_x : s->grid_blocks)),
+      std::max<uint64_t>(1, lean ? ws_needed : blocks_needed));
   if (lean) {
     ++s->lean_launches;
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;
     const ProgOp* a_prog = K.prog;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&Cc};
-    if (ws)
-      HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode), dim3(blocks), dim3(kinst_ws_threads()), args,
-                             lean_lds(s), stream));
-    else
-      HIPCHK(hipLaunchKernel(lean_fn(s), dim3(blocks), dim3(256), args, lean_lds(s), stream));
+    HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode), dim3(blocks), dim3(kinst_ws_threads()), args,
+                           lean_lds(s), stream));
   } else {
     const KCold* Cc = C;
     const smcrt_sdf_node* a_nodes = K.nodes;
@@ -994,7 +978,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     unsigned long long h[72], ht[9], hc[6];
     HIPCHK(hipStreamSynchronize(stream));
     kinst_diag_gather(h, ht, hc);
-    if (lean && s->ws_ok) {  // ws_kernel's tallies (ws.h WD_*)
+    if (lean) {  // ws_kernel's tallies (ws.h WD_*)
       const double wi = (double)std::max(1ull, h[20]), pt = (double)std::max(1ull, h[24]);
       std::fprintf(stderr, "[diag-ws] walker iters %llu: idle %.3f, busy lanes/iter %.1f, pending lanes/iter %.1f | "
                    "photon trips %llu: sleep %.3f, idle lanes %.1f, sync-waiting %.2f, slot-blocked %.2f, EVAL lanes "
@@ -1003,15 +987,6 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
                    h[20], h[21] / wi, h[22] / wi, h[23] / wi, h[24], h[25] / pt, h[30] / pt, h[27] / pt, h[26] / pt,
                    h[31] / pt, h[32] / pt, h[28] / pt, (double)h[29] / (double)std::max(1ull, h[28]), h[36] / pt, h[33],
                    h[34], (double)h[35] / (double)std::max(1ull, h[34]));
-    } else if (lean) {  // lean_kernel's tallies (lean.h LD_*)
-      const double tr = (double)std::max(1ull, h[0]);
-      std::fprintf(stderr, "[diag-lean] wave trips %llu | walk steps/trip %.3f, busy walkers/step %.1f | pushes/trip %.2f"
-                   " (sync %.3f), blocked req/trip %.2f | EVAL phases/trip %.3f lanes/EVAL %.1f | P7 runs/trip %.3f,"
-                   " event lanes waiting/trip %.2f, reverts %llu | lanes waiting sync/trip %.2f, idle %.2f, busy %.2f |"
-                   " ring fill %.1f | pool runs/trip %.3f items/run %.1f | local P7 lanes/run %.1f\n", h[0], h[1] / tr,
-                   (double)h[2] / std::max(1ull, h[1]), h[3] / tr, h[4] / tr, h[5] / tr, h[6] / tr,
-                   (double)h[7] / std::max(1ull, h[6]), h[8] / tr, h[13] / tr, h[9], h[10] / tr, h[11] / tr, h[14] / tr,
-                   h[12] / tr, h[15] / tr, (double)h[16] / std::max(1ull, h[15]), (double)h[17] / std::max(1ull, h[8]));
     }
     unsigned long long lt = 0;
     for (int i = 0; i < 64; ++i) lt += h[i];

@@ -1,37 +1,33 @@
-// ws.h — the lean transport kernel with wave-specialised blocks (photon waves, walker waves).
+// ws.h — the lean path's transport kernel: wave-specialised blocks (photon, event and walker waves).
 //
-// Same path, same program points and same arithmetic as lean_kernel (lean.h: noBiasPropagation
-// kernelsMod.f90:1901-1976 -> tauint2 inttau2.f90:15-364 -> update_grids :367-465), same
-// results bit for bit, for the same scenes (no Fresnel events, no detectors, no survival bias,
-// a plain source, bucketed path-length deposition).
+// The path is noBiasPropagation kernelsMod.f90:1901-1976 -> tauint2 inttau2.f90:15-364 ->
+// update_grids :367-465, restated with transport_kernel's arithmetic (kernels.h), with the same
+// results bit for bit, for the scenes lean.h names (no Fresnel events, no detectors, no survival
+// bias, a plain source, bucketed path-length deposition).
 //
-// Why. In lean_kernel every wave is both: 64 photons and 64 walkers. Its register peak is the
-// walk (a crossing and the bucket emit) on top of the photons' live state, 167 VGPRs, so a SIMD
-// holds three waves; compiled for four it spills 36 dwords a lane. The
-// photon code alone fits four waves (128 VGPRs, 2 dwords of scratch), and a walker holds no
-// photon state at all. Here a block of WS_WAVES = 8 waves runs WS_PW photon waves and
-// 8 - WS_PW walker waves:
-//   * photon waves run fetch, EVAL, P3/P4, the segment hand-out, P5/P6, the events and P8 on
-//     their 64 photons; a segment (update_grids entry) goes into the BLOCK's ring in LDS;
+// Why. A photon and its voxel walk want different code and different registers: the walk (a
+// crossing and the bucket emit) holds no photon state, the photon's code holds no walk. Round 4
+// ran both in every wave (lean_kernel, 167 VGPRs, three waves a SIMD); here a block of
+// WS_WAVES = 8 waves splits them, each role within 128 VGPRs (four waves a SIMD):
+//   * photon waves (WS_PW) run fetch, EVAL, P3/P4, the segment hand-out, P5/P6 and P8 on their
+//     64 photons; a segment (update_grids entry) goes into the BLOCK's ring in LDS;
 //   * walker waves take the oldest segments of the ring into idle lanes, walk them one
-//     crossing per iteration with dda_step (transport.h), file the records into the block's
+//     crossing per iteration with dda_step_r (transport.h), file the records into the block's
 //     buckets (deposit.h) and, at a segment's end, write its final cells and flags into the
-//     owner photon's slot, exactly as lean_kernel's walkers do.
-//   * event waves (round 5, session 2) run the photons' interactions: the albedo roulette,
-//     scatter and the next tauint2 entry (kernelsMod.f90:1958-1975, photon.f90:1045-1103,
-//     inttau2.f90:48-60), the tauint2 entry after an emission, and the emission itself
-//     (kernelsMod.f90:1937-1945 with the source's draws, photon.f90:311-710). A photon with such an event
-//     writes its direction, RNG state and layer into its slot, queues its lane in the block's
-//     event queue and waits; an event lane takes the queued owner, runs the event on the
-//     owner's values with the owner's own Philox stream and writes the results back. The event
-//     code so runs on full waves: in lean_kernel a wave ran its events once 20 of its lanes
-//     waited (0.52 phases a trip with 21 lanes, 22 % of the wave time). Completion, the rare
-//     terminal interactions and every event of test_kernel runs (moments) stay in the photon
-//     waves, batched as in lean_kernel.
-// A segment's walk is the pure function of (start, direction, length) it is in lean_kernel
-// (the start cell is recomputed from the start with the same cell_of), the deferred/synchronous
-// rule and the hazard accounting are lean.h's, and the photon side is lean_kernel's code, so the
-// records, counters and tallies are lean_kernel's; only the order of the fp64 jmean sums differs.
+//     owner photon's slot;
+//   * event waves (WS_EW) run the photons' interactions: the albedo roulette, scatter and the
+//     next tauint2 entry (kernelsMod.f90:1958-1975, photon.f90:1045-1103, inttau2.f90:48-60),
+//     the tauint2 entry after an emission, and the emission itself (kernelsMod.f90:1937-1945
+//     with the source's draws, photon.f90:311-710). A photon with such an event writes its
+//     direction, RNG state and layer into its slot, queues its lane in the block's event queue
+//     and waits; an event lane takes the queued owner, runs the event on the owner's values
+//     with the owner's own Philox stream and writes the results back, so the event code runs on
+//     full waves. Completion, the rare terminal interactions and every event of test_kernel
+//     runs (moments) stay in the photon waves, batched once SMCRT_LEAN_EVENT_LANES lanes wait.
+// A segment's walk is a pure function of (start, direction, length) (the start cell is
+// recomputed from the start with the same cell_of) and the deferred/synchronous rule and the
+// hazard accounting are lean.h's, so the records, counters and tallies are transport_kernel's;
+// only the order of the fp64 jmean sums differs.
 //
 // The block ring (multi-producer, multi-consumer, LDS). Tickets are matched one to one: photon
 // waves take them from `tail` (one reserved per segment), walker lanes from `head` (one held
@@ -197,6 +193,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   uint64_t wd[WD_N - WD_WITERS] = {};
 #endif
   if (wv < WS_PW) {
+    WS_MARK(1);
     // =================================================================== photon waves ======
     const bool test_kernel = (K.flags & SMCRT_FLAG_TEST_KERNEL) != 0;
     const bool records_on = (K.flags & SMCRT_FLAG_RECORD_PHOTONS) != 0 && C->records != nullptr;
@@ -228,7 +225,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
     };
     for (;; ++w_iters) {
-      // ---- photon fetch (wave-aggregated work queue), as lean_kernel ----------------------
+      // ---- photon fetch (wave-aggregated work queue) ------------------------------------------
       {
         uint64_t need = __ballot(P.st == ST_FETCH);
         while (need && more) {
@@ -293,7 +290,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       WSDIAG(WD_PWAIT, __popcll(__ballot(P.has(LF_WAIT))));
       WSDIAG(WD_PEVQ, __popcll(__ballot(P.has(LF_EVQ))));
 
-      // ---- EVAL: the SDF array at the photon's query point (lean_kernel) --------------------
+      // ---- EVAL: the SDF array at the photon's query point ------------------------------------
       const bool have = (P.f & (LF_PEND | LF_REQ | LF_WAIT)) == LF_PEND;
       EvalOut R;
       R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
@@ -307,7 +304,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         if (have) P.clr(LF_PEND);
       }
 
-      // ---- P3: consume the EVAL result (lean_kernel's P3) ----------------------------------
+      // ---- P3: consume the EVAL result -----------------------------------------------------
       if (have && (P.st == ST_H0 || P.st == ST_H3 || P.st == ST_M1)) {
         const uint32_t st0 = P.st;
         P.minabs = R.minabs;
@@ -522,7 +519,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           }
         }
       }
-      // ---- P7: the photon's other events, batched as in lean_kernel ---------------------------
+      // ---- P7: the photon's other events, batched ---------------------------------------------
       {
         const bool ev = free_ && !P.has(LF_EVQ) &&
                         (P.st == ST_INTERACT || P.st == ST_T2 || P.st == ST_EMIT || P.st == ST_DONE);
@@ -646,10 +643,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
 #undef WLU
     if (lane_id == 0) atomicSub(&sh->alive, 1u);  // (after this wave's last push, in its LDS order)
   } else if (wv < WS_PW + WS_EW) {
+    WS_MARK(2);
     // =================================================================== event waves =======
     // An event lane holds a ticket of the event queue (as a walker lane holds a ring ticket),
     // and when the queue entry shows written(ticket) it runs the owner's event: the code of
-    // lean_kernel's P7 on the owner's direction, layer and Philox stream (kernelsMod.f90:1958-1975,
+    // P7 on the owner's direction, layer and Philox stream (kernelsMod.f90:1958-1975,
     // photon.f90:1045-1103, inttau2.f90:48-60), so the draws and results are the owner's own.
     bool pend = false;
     uint32_t tk = 0;
@@ -746,6 +744,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
     }
   } else {
+    WS_MARK(10);
     // =================================================================== walker waves ======
     WalkSeg W;
     W.old = v3(0.0, 0.0, 0.0);
@@ -842,8 +841,10 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         __hip_atomic_fetch_and(&sh->busy[owner], ~(1u << slot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+    WS_MARK(15);
     close_buckets(K, C, WB, w_dep - overflow, overflow);
   }
+  WS_MARK(16);
   // ---- per-wave counters (each role adds its own) ------------------------------------------
   {
     unsigned long long* const counters = C->counters;

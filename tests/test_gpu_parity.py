@@ -916,15 +916,15 @@ def test_multi_accumulate_dynamic_chunks_one_collect(monkeypatch):
 
 @pytest.mark.parametrize("case", ["absorbing", "boundary-source", "test-kernel"])
 def test_lean_kernel_paths(monkeypatch, case):
-    """The lean kernel (lean.h: Fresnel-free, detector-free scenes, the voxel walk decoupled
-    from the photon) against the oracle, photon by photon, on the paths it adds:
+    """The lean path (ws_kernel, ws.h: Fresnel-free, detector-free scenes, the voxel walk and
+    the interactions decoupled from the photon) against the oracle, photon by photon, on the paths it adds:
     * absorbing: mua = 2 (albedo 0.83), so many photons are absorbed while their last
       segment is still being walked (ST_ABSORB waits for the cells recordWeight needs);
     * boundary-source: a uniform source on the top face, so segments near the grid faces are
       synchronous (the photon waits for tflag/cells) and escapes through the walk are common;
     * test-kernel: test_kernel semantics (no re-emission, ds<=0 mask, scatter moments).
-    Each case runs the wave-specialised lean kernel (ws.h, the default), lean_kernel
-    (SMCRT_LEAN_WS=0) and transport_kernel (SMCRT_LEAN=0): same counters and records."""
+    Each case runs the lean path and transport_kernel (SMCRT_LEAN=0): same counters and
+    records."""
     from rsmcrt_amd.engine import Engine as E
     flags = abi.FLAG_PATHLENGTH
     g = scene.grid(48, 48, 48, 1, 1, 1)
@@ -938,15 +938,14 @@ def test_lean_kernel_paths(monkeypatch, case):
         sc, src, n = builders.setup_scat_test(10.0), scene.point_source(), 20000
         flags |= abi.FLAG_TEST_KERNEL
     runs = {}
-    for lean, ws in (("1", "1"), ("1", "0"), ("0", "1")):
+    for lean in ("1", "0"):
         monkeypatch.setenv("SMCRT_LEAN", lean)
-        monkeypatch.setenv("SMCRT_LEAN_WS", ws)
         with E(sc, g) as eng:
             eng.kernel_times()
-            runs[lean + ws] = eng.run(src, n, seed=SEED, flags=flags, records=True)
+            runs[lean] = eng.run(src, n, seed=SEED, flags=flags, records=True)
             kt = eng.kernel_times()
         assert (kt["lean_launches"] > 0) == (lean == "1"), (lean, kt)
-        if lean == "1":  # the lean kernels run only on the bucketed path: bk_reduce ran and was timed
+        if lean == "1":  # the lean path runs only on the bucketed path: bk_reduce ran and was timed
             assert 0.0 < kt["fold_cu_ms"] < 1e3, kt
     cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True)
     for r in runs.values():
@@ -954,8 +953,7 @@ def test_lean_kernel_paths(monkeypatch, case):
     if case == "absorbing":
         assert cpu.counter("absorbed") > n // 2
     if case == "test-kernel":
-        for k in ("11", "10"):
-            np.testing.assert_allclose(runs[k].moments, cpu.moments, rtol=1e-12)
+        np.testing.assert_allclose(runs["1"].moments, cpu.moments, rtol=1e-12)
 
 
 @pytest.mark.parametrize("knob", ["0", "all"])

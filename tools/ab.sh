@@ -3,7 +3,7 @@
 # ROUNDS interleaved rounds. A variant is "base" (the in-tree library), "lib:NAME"
 # (tools/diag_libs/libsmcrt_NAME.so, built by tools/variants.sh) or "env:K=V[,K2=V2]" (the
 # in-tree library with those variables); "lib:NAME,env:K=V" combines both.
-#   AB="base lib:pw3 env:SMCRT_LEAN_WS=0" [WL=m1] [ROUNDS=2] [STEPS=10] [TESTS="pytest -k expr"] bash tools/ab.sh
+#   AB="base lib:pw3 env:SMCRT_LEAN=0" [WL=m1] [ROUNDS=2] [STEPS=10] [TESTS="pytest -k expr"] bash tools/ab.sh
 # Every GPU step has its own time limit; a fault, abort or timeout stops the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp

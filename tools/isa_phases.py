@@ -1,15 +1,14 @@
 #!/usr/bin/env python3
-"""Static ISA breakdown of lean_kernel<F, G> by program phase (no GPU needed).
+"""Static ISA breakdown of ws_kernel<F, G> (or transport_kernel) by region (no GPU needed).
 
 Compiles rsmcrt_amd/csrc/kinst.hip for one (LDS faces, grid mode) slice with
--DSMCRT_ASM_MARKERS, which turns lean.h's LDIAG_T(i) phase boundaries into `; @@LPHASE i`
-comments in the device assembly, takes the lean kernel's body and counts its instructions per
-phase and class. Phase i is the code between marker i-1 and marker i in program order (the
-markers are placed at the end of each phase, lean.h: 1 fetch, 2 EVAL, 3 P3/P4, 4 hand-out,
-5 walk, 6 P5/P6, 7 P7 events, 8 P8 + loop head). Static counts: what the phase's code holds,
+-DSMCRT_ASM_MARKERS, which turns ws.h's WS_MARK(i) region starts into `; @@LPHASE i` comments
+in the device assembly, takes the kernel's body and counts its instructions per region and
+class (ws.h: 1 photon waves, 2 event waves, 10-15 the walker waves: setup, claim + take,
+crossing step, record emit, finish, exit; 16 the counters flush). Static counts: what the code holds,
 not how often it runs (DESIGN.md §4.3b has the dynamic shares).
 
-usage: isa_phases.py [--kernel lean|transport] [--f 1] [--g 2] [extra hipcc flags...]
+usage: isa_phases.py [--kernel ws|transport] [--f 1] [--g 2] [extra hipcc flags...]
 """
 import collections
 import os
@@ -18,9 +17,9 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-NAMES = {1: "fetch", 2: "eval", 3: "p3p4", 4: "handout", 5: "walk", 6: "p5p6", 7: "p7events", 8: "p8+loop"}
 # ws_kernel (ws.h WS_MARK): the walker loop's regions
-WS_NAMES = {11: "w:claim+take", 12: "w:dda", 13: "w:emit", 14: "w:finish+loop", 0: "rest"}
+WS_NAMES = {0: "prologue", 1: "photon", 2: "event", 10: "w:setup", 11: "w:claim+take", 12: "w:dda", 13: "w:emit",
+            14: "w:finish", 15: "w:exit", 16: "epilogue"}
 
 
 def classify(op):
@@ -56,7 +55,7 @@ def classify(op):
 
 
 def main(argv):
-    kern, f, g, extra = "lean", "1", "2", []
+    kern, f, g, extra = "ws", "1", "2", []
     i = 0
     while i < len(argv):
         if argv[i] in ("--kernel", "--f", "--g"):
@@ -77,8 +76,7 @@ def main(argv):
                     "-DSMCRT_ASM_MARKERS", "-o", out, os.path.join(ROOT, "rsmcrt_amd", "csrc", "kinst.hip")] + extra,
                    check=True, cwd="/tmp", stderr=subprocess.DEVNULL)
     s = open(out).read()
-    pat = {"lean": r"^(_ZN5smcrt11lean_kernel\w+):", "ws": r"^(_ZN5smcrt9ws_kernel\w+):"}.get(
-        kern, r"^(_Z16transport_kernel\w+):")
+    pat = r"^(_ZN5smcrt9ws_kernel\w+):" if kern == "ws" else r"^(_Z16transport_kernel\w+):"
     m = re.search(pat, s, re.M)
     start = m.start()
     end = s.index(".Lfunc_end", start)
@@ -92,10 +90,7 @@ def main(argv):
         mk = re.match(r"; @@LPHASE (\d+)", t)
         if mk:
             i = int(mk.group(1))
-            # lean: code after marker i belongs to phase i+1 (8 wraps to 1); ws: region i starts at marker i
-            phase = i if kern == "ws" else i % 8 + 1
-            if kern == "ws" and i == 14:
-                phase = 14
+            phase = i  # region i starts at marker i
             continue
         if not t or t.startswith((".", ";", "_")) or t.endswith(":"):
             continue
@@ -110,7 +105,7 @@ def main(argv):
     for p in sorted(per):
         c = per[p]
         tot.update(c)
-        print((WS_NAMES if kern == "ws" else NAMES).get(p, str(p)).ljust(10) + "".join(str(c[k]).rjust(12) for k in classes) + str(sum(c.values())).rjust(8))
+        print(WS_NAMES.get(p, str(p)).ljust(10) + "".join(str(c[k]).rjust(12) for k in classes) + str(sum(c.values())).rjust(8))
     print("all".ljust(10) + "".join(str(tot[k]).rjust(12) for k in classes) + str(sum(tot.values())).rjust(8))
 
 
