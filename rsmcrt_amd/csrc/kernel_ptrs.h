@@ -1,7 +1,7 @@
 // kernel_ptrs.h — the transport kernel instantiations, reached through pointers.
 //
 // build.py compiles kinst.hip once per (LDS faces F, grid mode G) with -DKI_F=F -DKI_G=G, so
-// the 27 instantiations of transport_kernel and ws_kernel (kernels.h, ws.h) build in parallel
+// the instantiations of transport_kernel and ws_kernel (kernels.h, ws.h) build in parallel
 // instead of in one translation unit. Each object exports these getters; hipLaunchKernel and
 // the occupancy queries take the host stubs they return.
 #pragma once
@@ -12,10 +12,11 @@ namespace smcrt {
 size_t kinst_ws_shared_bytes();    // sizeof(WsShared), ws_kernel's static LDS
 int kinst_ws_threads();            // ws_kernel's block size
 int kinst_ws_photon_lanes();       // photon lanes per ws_kernel block
+size_t kinst_ws_scratch_bytes(size_t lanes);  // ws_kernel lane scratch (ws.h WX_*) of that many photon lanes
 
 #define SMCRT_KINST_DECL(F, G)                                                               \
   const void* kinst_transport_##F##_##G(int xsrc, int coop);                                 \
-  const void* kinst_ws_##F##_##G();                                                          \
+  const void* kinst_ws_##F##_##G(int xf);                                                    \
   void kinst_diag_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6);
 SMCRT_KINST_DECL(0, 0)
 SMCRT_KINST_DECL(0, 1)
@@ -39,14 +40,16 @@ inline const void* transport_kernel_ptr(bool lds_faces, int gm, bool xsrc, bool 
     default: return kinst_transport_1_2(x, c);
   }
 }
-inline const void* ws_kernel_ptr(bool lds_faces, int gm) {
+// ws_kernel<lds_faces, gm, xf> (xf: the Fresnel/detector program points, ws.h)
+inline const void* ws_kernel_ptr(bool lds_faces, int gm, bool xf) {
+  const int x = xf ? 1 : 0;
   switch ((lds_faces ? 3 : 0) + gm) {
-    case 0: return kinst_ws_0_0();
-    case 1: return kinst_ws_0_1();
-    case 2: return kinst_ws_0_2();
-    case 3: return kinst_ws_1_0();
-    case 4: return kinst_ws_1_1();
-    default: return kinst_ws_1_2();
+    case 0: return kinst_ws_0_0(x);
+    case 1: return kinst_ws_0_1(x);
+    case 2: return kinst_ws_0_2(x);
+    case 3: return kinst_ws_1_0(x);
+    case 4: return kinst_ws_1_1(x);
+    default: return kinst_ws_1_2(x);
   }
 }
 // diagnostic builds: the kernels' tallies summed over the objects (each is cleared)

@@ -27,9 +27,12 @@ const void* KI_NAME(kinst_transport)(int xsrc, int coop) {
 size_t kinst_ws_shared_bytes() { return sizeof(WsShared); }
 int kinst_ws_threads() { return WS_THREADS; }
 int kinst_ws_photon_lanes() { return (int)WS_NPL; }
+size_t kinst_ws_scratch_bytes(size_t lanes) { return ws_scratch_bytes(lanes); }
 #endif
 
-const void* KI_NAME(kinst_ws)() { return (const void*)ws_kernel<KI_F != 0, KI_G>; }
+const void* KI_NAME(kinst_ws)(int xf) {
+  return xf ? (const void*)ws_kernel<KI_F != 0, KI_G, true> : (const void*)ws_kernel<KI_F != 0, KI_G, false>;
+}
 
 
 void KI_NAME(kinst_diag)(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6) {

@@ -92,6 +92,7 @@ enum : uint32_t {
   LF_CELLS = 32u,  // xcell/ycell/zcell are the photon's cells
   LF_MOVE_FWD = 64u, LF_MOVE_BACK = 128u,  // the move after the request
   LF_EVQ = 256u,   // the photon's event is queued for the event waves (ws.h)
+  LF_SSP = 512u,   // a refraction: X1 moves to the smallStepPos kept in the lane scratch (ws.h)
 };
 // event results (ws.h ev_code; the low 16 bits carry an emitted photon's layer)
 enum : uint32_t { EV_DONE = 1u << 31, EV_ABSORB = 1u << 30, EV_RUNAWAY = 1u << 29 };

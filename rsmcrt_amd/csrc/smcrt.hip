@@ -138,9 +138,12 @@ struct smcrt_scene {
   int grid_blocks = 0;
   int grid_blocks_x = 0;  // the XSRC (general emitter) instantiation
   int grid_blocks_ws = 0;    // ws_kernel (ws.h): the lean path with photon, event and walker waves
-  // the lean path (ws_kernel) serves this scene: equal refractive indices, no detectors, a few
-  // tops, bucketed deposition, axes below 2^20 cells, its LDS fits (SMCRT_LEAN=0 keeps
-  // transport_kernel)
+  // ws_kernel's lane scratch (ws.h WX_*) for scenes with Fresnel interfaces or detectors: one
+  // region per launch stream (queue index, launch_one), lscratch_stride bytes apart
+  double* d_lscratch = nullptr;
+  size_t lscratch_stride = 0;
+  // the lean path (ws_kernel) serves this scene: a few tops, bucketed deposition, axes below
+  // 2^20 cells, its LDS fits (SMCRT_LEAN=0 keeps transport_kernel)
   bool lean_ok = false;
   // deferred lean-kernel segments that ended in tflag or an error stop (lean.h "hazards"):
   // running total d_queue[MAX_SLOTS + 3], reported by smcrt_scene_kernel_times and counted in
@@ -296,7 +299,7 @@ void smcrt_scene_destroy(smcrt_scene* s) {
   (void)hipSetDevice(s->device);
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   if (s->fstream) (void)hipStreamSynchronize(s->fstream);
-  void* ptrs[] = {s->d_ctab, s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
+  void* ptrs[] = {s->d_lscratch, s->d_ctab, s->d_nodes, s->d_prog, s->d_props, s->d_faces, s->d_dets, s->d_det_off, s->d_spec,
                   s->d_queue, s->d_cold, s->d_grids, s->d_small, s->d_counters, s->d_records,
                   s->d_sorted, s->d_tile_count, s->d_tile_start, s->d_pieces, s->d_order, s->d_cull, s->d_cull_data};
   for (int i = 0; i < MAX_SLOTS; ++i) {
@@ -644,10 +647,11 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     }
     s->grid_mode = f2 ? 2 : (p2 ? 1 : 0);
   }
-  {  // the lean path (ws.h): scenes without Fresnel events or detectors, a few tops
-    bool ok = n_dets == 0 && s->bucketed && s->coop_lanes == 0 && grid->nx < (1 << 20) - 2 &&
-              grid->ny < (1 << 20) - 2 && grid->nz < (1 << 20) - 2;
-    for (int32_t i = 1; ok && i < n_top; ++i) ok = s->h_props[i].n == s->h_props[0].n;
+  bool fresnel = false;  // two tops with different refractive indices
+  for (int32_t i = 1; i < n_top; ++i) fresnel = fresnel || s->h_props[i].n != s->h_props[0].n;
+  {  // the lean path (ws.h): scenes with a few tops
+    bool ok = s->bucketed && s->coop_lanes == 0 && grid->nx < (1 << 20) - 2 && grid->ny < (1 << 20) - 2 &&
+              grid->nz < (1 << 20) - 2;
     ok = ok && lean_lds(s) + kinst_ws_shared_bytes() <= 163840;
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
@@ -662,10 +666,18 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) s->wall_khz = khz;
   }
   if (s->lean_ok) {
-    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ws_kernel_ptr(s->lds_faces, s->grid_mode),
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ws_kernel_ptr(s->lds_faces, s->grid_mode, s->d_lscratch != nullptr),
                                                                  kinst_ws_threads(), lean_lds(s));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     s->grid_blocks_ws = cus * per_cu;
+    if (fresnel || n_dets > 0) {  // the lane scratch, per launch stream
+      s->lscratch_stride = (kinst_ws_scratch_bytes((size_t)s->grid_blocks_ws * kinst_ws_photon_lanes()) + 255) & ~(size_t)255;
+      if (hipMalloc((void**)&s->d_lscratch, s->lscratch_stride * (MAX_SLOTS + 1)) != hipSuccess) {
+        (void)hipGetLastError();
+        s->d_lscratch = nullptr;
+        s->lean_ok = false;  // (transport_kernel needs none)
+      }
+    }
   }
   if (std::getenv("SMCRT_VERBOSE"))
     std::fprintf(stderr, "[smcrt] scene: lean %d (ws blocks/CU %d, static LDS %zu + dynamic %zu B), transport grid %d\n",
@@ -874,6 +886,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   const bool binned = K.rec_pool != nullptr;
   if (binned && s->f_pending[sl]) HIPCHK(hipStreamWaitEvent(stream, s->ev_f[sl], 0));  // slot free
   Ch.queue = s->d_queue + qi;  // (a queue head per stream: overlapped launches run concurrently)
+  Ch.lane_scratch = s->d_lscratch ? (double*)((char*)s->d_lscratch + (size_t)qi * s->lscratch_stride) : nullptr;
   HIPCHK(hipMemsetAsync(Ch.queue, 0, sizeof(unsigned long long), stream));
   // this launch's cold parameters: a ring slot, written in stream order before the kernel.
   // (Each stream has its own ring of slots, so a slot is only ever rewritten in stream order
@@ -916,7 +929,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     const smcrt_sdf_node* a_nodes = K.nodes;
     const ProgOp* a_prog = K.prog;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode), dim3(blocks), dim3(kinst_ws_threads()), args,
+    HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode, s->d_lscratch != nullptr), dim3(blocks), dim3(kinst_ws_threads()), args,
                            lean_lds(s), stream));
   } else {
     const KCold* Cc = C;
@@ -1103,6 +1116,7 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.queue = nullptr;  // (set per launch: launch_one)
   Ch.far_steps = s->d_queue + MAX_SLOTS + 1;
   Ch.lean_hazards = s->d_queue + MAX_SLOTS + 3;
+  Ch.lane_scratch = nullptr;  // (per launch stream: launch_one)
   K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
   {
     const char* cd = std::getenv("SMCRT_DEBUG_CLAIM_DELAY");

@@ -75,6 +75,7 @@ struct KCold {
   uint32_t* tile_nb;          // bucketed path: buckets claimed per tile
   unsigned long long* far_steps;  // march steps taken by the far-field march (far.h), running total
   unsigned long long* lean_hazards;  // deferred lean segments ending in tflag / a fault (lean.h), running total
+  double* lane_scratch;       // ws_kernel's per-photon-lane Fresnel/detector state (ws.h WX_*), or null
   SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
 

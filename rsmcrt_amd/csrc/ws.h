@@ -113,6 +113,19 @@ struct WsShared {
 };
 constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u, WS_EV_EMIT = 3u;  // event kinds (ev_code bits 16-17)
 
+// The lane scratch (global memory, KCold::lane_scratch, scenes with Fresnel interfaces or
+// detectors): per photon lane the state of the rare program points that the photon's
+// registers do not hold, structure of arrays over the launch's photon lanes
+// (blockIdx.x * WS_NPL + pl). Doubles: the tauint2 entry's pos and dir (the bounce abort
+// returns to them, inttau2.f90:313-315), the detector start point (startp, :125-131), the
+// Fresnel ds pair (F0) and the calcNormal taps (N1-N3, then the refraction's smallStepPos);
+// then 32-bit words: the new layer, the normal's SDF (Ls) and the bounce count.
+enum : int { WX_ENTRY = 0, WX_START = 6, WX_DS = 9, WX_TAP = 11, WX_ND = 14 };
+enum : int { WXI_NEWL = 0, WXI_LS, WXI_BOUNCES, WXI_N };
+__host__ __device__ constexpr size_t ws_scratch_bytes(size_t lanes) {
+  return lanes * (WX_ND * sizeof(double) + WXI_N * sizeof(uint32_t));
+}
+
 __device__ __forceinline__ void ws_count(WsShared* sh, int c) {
   const uint64_t m = __ballot(1);
   if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&sh->wctr[threadIdx.x >> 6][c], (uint32_t)__popcll(m));
@@ -143,7 +156,9 @@ enum : int { WD_WITERS = 20, WD_WIDLE, WD_WBUSY, WD_WPEND, WD_PTRIPS, WD_PSLEEP,
 #define WSDIAG(i, v) do {} while (0)
 #endif
 
-template <bool LDS_FACES, int GM>
+// XF: scenes with Fresnel interfaces or detectors (their program points cost the photon waves
+// registers, so the other scenes run an instantiation without them)
+template <bool LDS_FACES, int GM, bool XF>
 __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ws_kernel(
     KParams K, const smcrt_sdf_node* __restrict__ nodes, const ProgOp* __restrict__ prog,
     const KCold* __restrict__ C) {
@@ -204,7 +219,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     const double mx = mf * (double)(K.nx + 2), my = mf * (double)(K.ny + 2), mz = mf * (double)(K.nz + 2);
     const double ex = 2.0 * K.xmax - mx, ey = 2.0 * K.ymax - my, ez = 2.0 * K.zmax - mz;
     const bool defer_all = K.lean_debug == 2u;
-
+    // the lane scratch (see WX_*): field f of this lane at X[f * xs]
+    const size_t xs = (size_t)gridDim.x * WS_NPL;
+    double* const X = XF ? C->lane_scratch + (size_t)blockIdx.x * WS_NPL + pl : nullptr;
+    uint32_t* const XI = XF ? (uint32_t*)(C->lane_scratch + WX_ND * xs) + (size_t)blockIdx.x * WS_NPL + pl
+                                         : nullptr;
     LeanPhoton P;
     P.st = ST_FETCH; P.f = LF_CELLS;
     P.pos = P.dir = v3(0.0, 0.0, 0.0);
@@ -215,6 +234,14 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     uint64_t chunk_base = 0;
     uint32_t chunk_left = 0;
     bool more = true;
+    // tauint2 entry (inttau2.f90:48-60): the bounce abort's return point and the detector start
+    auto t2_entry = [&]() {
+      if constexpr (XF) {
+        X[(WX_ENTRY + 0) * xs] = P.pos.x; X[(WX_ENTRY + 1) * xs] = P.pos.y; X[(WX_ENTRY + 2) * xs] = P.pos.z;
+        X[(WX_ENTRY + 3) * xs] = P.dir.x; X[(WX_ENTRY + 4) * xs] = P.dir.y; X[(WX_ENTRY + 5) * xs] = P.dir.z;
+        X[(WX_START + 0) * xs] = P.pos.x; X[(WX_START + 1) * xs] = P.pos.y; X[(WX_START + 2) * xs] = P.pos.z;
+      }
+    };
 
     // P8: arrive at the hop-loop head, inttau2.f90:61
     auto p8 = [&]() {
@@ -281,6 +308,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             P.taurun = 0.0;
             P.hop = 0;
             P.st = ST_H0;
+            t2_entry();
             p8();
           }
         }
@@ -296,8 +324,22 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
       if (__ballot(have)) {
         const bool mask_le = test_kernel && P.st == ST_LAYER;
-        const V3 q = (P.st == ST_H1 || P.st == ST_G0) ? P.pos + smul(P.d, P.dir) : P.pos;
-        R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, 0, 0);
+        V3 q = (P.st == ST_H1 || P.st == ST_G0 || P.st == ST_F1) ? P.pos + smul(P.d, P.dir) : P.pos;
+        // Fresnel: ds(new), ds(old) (F0, F1) and the calcNormal taps of Ls (N1-N4,
+        // sdf_base.f90:176-184) read those SDFs' values
+        int32_t capi = 0, capj = 0;
+        if (XF && have && P.st >= ST_F0 && P.st <= ST_N4) {
+          const bool fres = P.st == ST_F0 || P.st == ST_F1;
+          capi = (int32_t)XI[(fres ? WXI_NEWL : WXI_LS) * xs];
+          capj = fres ? P.layer : 0;
+          if (!fres) {
+            const double t = 1e-6;
+            q = P.st == ST_N1 ? P.pos + mul(v3(1.0, -1.0, -1.0), t)
+              : P.st == ST_N2 ? P.pos + mul(v3(-1.0, -1.0, 1.0), t)
+              : P.st == ST_N3 ? P.pos + mul(v3(-1.0, 1.0, -1.0), t) : P.pos + mul(v3(1.0, 1.0, 1.0), t);
+          }
+        }
+        R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, capi, capj);
         const bool counted = P.st == ST_H0 || P.st == ST_H1 || P.st == ST_H3 || P.st == ST_M1 || P.st == ST_G0;
         w_sdf += __popcll(__ballot(have && counted)) * (uint32_t)K.n_top;
         WSDIAG(WD_ELANES, __popcll(__ballot(have)));
@@ -317,6 +359,74 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         uint32_t ns = st0 == ST_M1 ? (out ? (uint32_t)ST_B0 : (uint32_t)ST_M0) : (done ? (uint32_t)ST_T2END : (uint32_t)ST_M0);
         if (small) { ns = ST_H1; P.set(LF_PEND); }
         P.st = ns;
+      } else if (XF && have && P.st >= ST_F0 && P.st <= ST_N4) {  // reflect_refract's program points
+        switch (P.st) {
+          case ST_F0:  // ds(new), ds(old) at pos
+            X[WX_DS * xs] = R.va; X[(WX_DS + 1) * xs] = R.vb;
+            P.st = ST_F1; P.set(LF_PEND);
+            break;
+          case ST_F1: {  // which SDF's normal, :250-277
+            const double ds_new = X[WX_DS * xs], ds_old = X[(WX_DS + 1) * xs], dn_new = R.va, dn_old = R.vb;
+            const int32_t new_layer = (int32_t)XI[WXI_NEWL * xs];
+            int32_t ls = 0;
+            if (dn_new < 0.0 && ds_new >= 0.0) ls = new_layer;
+            else if (dn_old >= 0.0 && ds_old < 0.0) ls = P.layer;
+            else if (dn_new < 0.0 && dn_old < 0.0) ls = new_layer;
+            else if (ds_old >= 0.0 && dn_old >= 0.0) ls = P.layer;
+            if (ls == 0) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; break; }  // error stop :264-277
+            XI[WXI_LS * xs] = (uint32_t)ls;
+            P.st = ST_N1; P.set(LF_PEND);
+            break;
+          }
+          case ST_N1: case ST_N2: case ST_N3:  // calcNormal taps
+            X[(WX_TAP + (int)(P.st - ST_N1)) * xs] = R.va;
+            P.st = P.st + 1; P.set(LF_PEND);
+            break;
+          case ST_N4: {  // calcNormal (sdf_base.f90:166-190) + reflect_refract (surfaces.f90:14-84)
+            const double e1 = X[WX_TAP * xs], e2 = X[(WX_TAP + 1) * xs], e3 = X[(WX_TAP + 2) * xs], e4 = R.va;
+            const V3 xyy = v3(1.0, -1.0, -1.0), yyx = v3(-1.0, -1.0, 1.0), yxy = v3(-1.0, 1.0, -1.0),
+                     xxx = v3(1.0, 1.0, 1.0);
+            const V3 nn = ((mul(xyy, e1) + mul(yyx, e2)) + mul(yxy, e3)) + mul(xxx, e4);
+            const double ln = len(nn);
+            const V3 N = v3(nn.x / ln, nn.y / ln, nn.z / ln);
+            const int32_t new_layer = (int32_t)XI[WXI_NEWL * xs];
+            const double n1 = props[P.layer - 1].n, n2 = props[new_layer - 1].n;
+            ws_count(sh, LC_FRES);
+            const double Rf = fresnel(P.dir, N, n1, n2);
+            if (P.rng.next(K.key0, K.key1) <= Rf) {  // reflect :42-55, :304-316
+              const double s2 = 2.0 * dot(N, P.dir);
+              P.dir = P.dir - smul(s2, N);
+              ws_count(sh, LC_REFL);
+              X[WX_START * xs] = P.pos.x; X[(WX_START + 1) * xs] = P.pos.y; X[(WX_START + 2) * xs] = P.pos.z;
+              const uint32_t nb = XI[WXI_BOUNCES * xs] + 1u;
+              XI[WXI_BOUNCES * xs] = nb;
+              if (nb > 1000u) {  // :313-315: return without write-back
+                ws_count(sh, LC_BABORT);
+                P.pos = v3(X[WX_ENTRY * xs], X[(WX_ENTRY + 1) * xs], X[(WX_ENTRY + 2) * xs]);
+                P.dir = v3(X[(WX_ENTRY + 3) * xs], X[(WX_ENTRY + 4) * xs], X[(WX_ENTRY + 5) * xs]);
+                P.st = ST_INTERACT;
+              } else {
+                P.st = ST_H0;  // arrives in P8
+              }
+            } else {  // refract :57-84, transmit :284-303 (pos = smallStepPos, formed on the old dir)
+              const V3 ssp = P.pos + smul(P.d, P.dir);
+              X[WX_TAP * xs] = ssp.x; X[(WX_TAP + 1) * xs] = ssp.y; X[(WX_TAP + 2) * xs] = ssp.z;
+              const double eta = n1 / n2;
+              V3 Nt = N;
+              double c1 = dot(Nt, P.dir);
+              if (c1 < 0.0) c1 = -c1;
+              else Nt = smul(-1.0, N);
+              const double c2 = sqrt(1.0 - (eta * eta) * (1.0 - c1 * c1));
+              P.dir = smul(eta, P.dir) + smul(eta * c1 - c2, Nt);
+              P.layer = new_layer;
+              P.st = ST_X1;
+              P.set(LF_REQ | LF_SSP);
+            }
+            break;
+          }
+          default:
+            break;
+        }
       } else if (have) {
         switch (P.st) {
           case ST_LAYER:  // kernelsMod.f90:1948-1952 (test_kernel: mask ds<=0, :2136)
@@ -347,6 +457,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
               break;
             }
             if (new_layer == 0) { P.set(LF_TFLAG); P.st = ST_T2END; break; }
+            if (XF && props[P.layer - 1].n != props[new_layer - 1].n) {  // reflect_refract, :248
+              XI[WXI_NEWL * xs] = (uint32_t)new_layer;
+              P.st = ST_F0; P.set(LF_PEND);
+              break;
+            }
             P.layer = new_layer;
             P.st = ST_X1;
             P.set(LF_REQ);
@@ -448,9 +563,18 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
       const bool free_ = !(P.f & (LF_REQ | LF_WAIT));
       if (free_ && (P.st == ST_H2 || P.st == ST_B0 || P.st == ST_X1)) {
-        if (P.st == ST_X1) {  // :326-335 (pos = smallStepPos)
+        if (P.st == ST_X1) {  // :326-335 / :294-303 (pos = smallStepPos)
           P.taurun = P.taurun + P.d * props[P.layer - 1].kappa;
-          P.pos = P.pos + smul(P.d, P.dir);
+          if (XF && P.has(LF_SSP)) P.pos = v3(X[WX_TAP * xs], X[(WX_TAP + 1) * xs], X[(WX_TAP + 2) * xs]);
+          else P.pos = P.pos + smul(P.d, P.dir);
+          P.clr(LF_SSP);
+        }
+        if (XF && K.n_dets) {  // detectors, :125-131 / 195-201 (from startp to pos along dir)
+          const V3 st = v3(X[WX_START * xs], X[(WX_START + 1) * xs], X[(WX_START + 2) * xs]);
+          const double sep = pointsep(P.pos, st);
+          X[WX_START * xs] = P.pos.x; X[(WX_START + 1) * xs] = P.pos.y; X[(WX_START + 2) * xs] = P.pos.z;
+          const uint32_t hits = record_hits(K, C->det_bins, K.dets, K.det_off, st, P.dir, sep, P.layer, 1.0);
+          if (hits) atomicAdd(&sh->wctr[wv][LC_HITS], hits);
         }
         if (P.st == ST_H2) {
           P.st = ST_H3; P.set(LF_PEND);
@@ -511,6 +635,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             if (P.st == ST_EMIT) {  // kernelsMod.f90:1937-1945: a fresh packet
               P.clr(LF_FAULT); P.layer = 0;
               WLU(LL_STATUS) = 0; WLU(LL_NSCATT) = 0; WLU(LL_INTER) = 0;
+              if constexpr (XF) XI[WXI_BOUNCES * xs] = 0;
             }
             sh->ev_code[pl] = (uint32_t)P.layer |
                               ((P.st == ST_INTERACT ? WS_EV_INTERACT : (P.st == ST_T2 ? WS_EV_TAU : WS_EV_EMIT)) << 16);
@@ -578,6 +703,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           }
           if (ev && P.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
             ws_count(sh, LC_TAU);
+            t2_entry();
             P.tau = -det_log(P.rng.next(K.key0, K.key1));
             P.taurun = 0.0;
             P.hop = 0;
@@ -586,6 +712,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           if (ev && P.st == ST_EMIT) {  // kernelsMod.f90:1937-1945
             P.clr(LF_FAULT); P.layer = 0;
             WLU(LL_STATUS) = 0; WLU(LL_NSCATT) = 0; WLU(LL_INTER) = 0;
+            if constexpr (XF) XI[WXI_BOUNCES * xs] = 0;
             Lane L;
             L.rng = P.rng; L.xcell = L.ycell = L.zcell = 0; L.layer = 0; L.tflag = false;
             emit<GM, false>(K, C, L, 0u);
@@ -620,7 +747,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
               r->cell[0] = P.xcell; r->cell[1] = P.ycell; r->cell[2] = P.zcell;
               r->layer = P.layer;
               r->nscatt = WLU(LL_NSCATT);
-              r->bounces = 0;
+              r->bounces = XF ? XI[WXI_BOUNCES * xs] : 0u;
               r->draws = P.rng.draws;
               r->status = WLU(LL_STATUS);
             }

@@ -914,7 +914,8 @@ def test_multi_accumulate_dynamic_chunks_one_collect(monkeypatch):
     assert a.nscatt[0] == b.nscatt[0]
 
 
-@pytest.mark.parametrize("case", ["absorbing", "boundary-source", "test-kernel"])
+@pytest.mark.parametrize("case", ["absorbing", "boundary-source", "test-kernel", "fresnel", "detectors",
+                                  "bounce-abort"])
 def test_lean_kernel_paths(monkeypatch, case):
     """The lean path (ws_kernel, ws.h: Fresnel-free, detector-free scenes, the voxel walk and
     the interactions decoupled from the photon) against the oracle, photon by photon, on the paths it adds:
@@ -922,13 +923,32 @@ def test_lean_kernel_paths(monkeypatch, case):
       segment is still being walked (ST_ABSORB waits for the cells recordWeight needs);
     * boundary-source: a uniform source on the top face, so segments near the grid faces are
       synchronous (the photon waits for tflag/cells) and escapes through the walk are common;
-    * test-kernel: test_kernel semantics (no re-emission, ds<=0 mask, scatter moments).
+    * test-kernel: test_kernel semantics (no re-emission, ds<=0 mask, scatter moments);
+    * fresnel: the Tran & Jacques sphere (n=1.33 in air, M3's scene): reflect_refract's program
+      points (F0/F1, the calcNormal taps, reflection and refraction) in the photon waves;
+    * detectors: M5's layered skin with Fresnel at every interface and a circle and an annulus
+      detector at the top face (record_hits from each segment's start point);
+    * bounce-abort: an almost transparent n=1.5 sphere with an off-centre source, so photons
+      caught by total internal reflection reach 1000 bounces and return to their tauint2
+      entry (inttau2.f90:313-315).
     Each case runs the lean path and transport_kernel (SMCRT_LEAN=0): same counters and
     records."""
     from rsmcrt_amd.engine import Engine as E
     flags = abi.FLAG_PATHLENGTH
     g = scene.grid(48, 48, 48, 1, 1, 1)
-    if case == "absorbing":
+    dets = []
+    if case == "fresnel":
+        sc, n = builders.setup_tran_and_jacques(), 30000
+        src = scene.uniform_source((-0.25, 0.0, 0.99999), (0.5, 0.0, 0.0), (0.0, 0.0, 0.0), (0.0, 0.0, -1.0))
+    elif case == "detectors":
+        sc, n, g = builders.skin_layers(), 30000, scene.grid(48, 48, 48, 0.05, 0.05, 0.05)
+        src = scene.pencil_source((0.0, 0.0, 0.0499), (0.0, 0.0, -1.0))
+        dets = [scene.circle_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.05, 50),
+                scene.annulus_dect((0.0, 0.0, 0.0499), (0.0, 0.0, 1.0), 1, 0.005, 0.02, 25)]
+    elif case == "bounce-abort":
+        sc, n, g = builders.setup_sphere(1e-4, 1e-5, 0.0, 1.5, 1.0), 100, scene.grid(32, 32, 32, 1, 1, 1)
+        src = scene.point_source((0.85, 0.0, 0.0))
+    elif case == "absorbing":
         sc, src, n = builders.setup_sphere(10.0, 2.0, 0.9, 1.0, 1.0), scene.point_source(), 30000
     elif case == "boundary-source":
         sc = builders.setup_sphere(5.0, 0.5, 0.8, 1.0, 1.0)
@@ -940,16 +960,22 @@ def test_lean_kernel_paths(monkeypatch, case):
     runs = {}
     for lean in ("1", "0"):
         monkeypatch.setenv("SMCRT_LEAN", lean)
-        with E(sc, g) as eng:
+        with E(sc, g, dets) as eng:
             eng.kernel_times()
             runs[lean] = eng.run(src, n, seed=SEED, flags=flags, records=True)
             kt = eng.kernel_times()
         assert (kt["lean_launches"] > 0) == (lean == "1"), (lean, kt)
         if lean == "1":  # the lean path runs only on the bucketed path: bk_reduce ran and was timed
             assert 0.0 < kt["fold_cu_ms"] < 1e3, kt
-    cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True)
+    cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True, dets=dets)
     for r in runs.values():
         compare(r, cpu)
+    if case in ("fresnel", "detectors"):
+        assert cpu.counter("fresnel") > n and cpu.counter("reflections") > 0
+    if case == "detectors":
+        assert cpu.counter("detector_hits") > 0
+    if case == "bounce-abort":
+        assert cpu.counter("bounce_aborts") > 0
     if case == "absorbing":
         assert cpu.counter("absorbed") > n // 2
     if case == "test-kernel":

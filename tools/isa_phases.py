@@ -8,7 +8,7 @@ class (ws.h: 1 photon waves, 2 event waves, 10-15 the walker waves: setup, claim
 crossing step, record emit, finish, exit; 16 the counters flush). Static counts: what the code holds,
 not how often it runs (DESIGN.md §4.3b has the dynamic shares).
 
-usage: isa_phases.py [--kernel ws|transport] [--f 1] [--g 2] [extra hipcc flags...]
+usage: isa_phases.py [--kernel ws|wsx|transport] [--f 1] [--g 2] [extra hipcc flags...]
 """
 import collections
 import os
@@ -76,7 +76,7 @@ def main(argv):
                     "-DSMCRT_ASM_MARKERS", "-o", out, os.path.join(ROOT, "rsmcrt_amd", "csrc", "kinst.hip")] + extra,
                    check=True, cwd="/tmp", stderr=subprocess.DEVNULL)
     s = open(out).read()
-    pat = r"^(_ZN5smcrt9ws_kernel\w+):" if kern == "ws" else r"^(_Z16transport_kernel\w+):"
+    pat = r"^(_ZN5smcrt9ws_kernelILb\d+ELi\d+ELb" + ("1" if kern == "wsx" else "0") + r"E\w+):" if kern.startswith("ws") else r"^(_Z16transport_kernel\w+):"
     m = re.search(pat, s, re.M)
     start = m.start()
     end = s.index(".Lfunc_end", start)
@@ -105,7 +105,7 @@ def main(argv):
     for p in sorted(per):
         c = per[p]
         tot.update(c)
-        print(WS_NAMES.get(p, str(p)).ljust(10) + "".join(str(c[k]).rjust(12) for k in classes) + str(sum(c.values())).rjust(8))
+        print((WS_NAMES if kern.startswith("ws") else {}).get(p, str(p)).ljust(10) + "".join(str(c[k]).rjust(12) for k in classes) + str(sum(c.values())).rjust(8))
     print("all".ljust(10) + "".join(str(tot[k]).rjust(12) for k in classes) + str(sum(tot.values())).rjust(8))
 
 
