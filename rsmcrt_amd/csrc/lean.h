@@ -39,7 +39,10 @@
 // same path length, and k <= n_a (the walk is monotonic along each axis). The line between
 // the segment's ends stays inside the box shrunk by lean_margin (convexity), so with
 // lean_margin_a = 2 * delta * (n_a + 2) no snap can reach a boundary face. The remaining
-// error stops need NaNs or an overshoot of one ulp at an exact tie of two wall distances
+// error stops need a start outside its own cell (faces and cells rounded separately: a start
+// within an ulp of a face, e.g. a source on a mid-plane of a grid whose spacing is not a power
+// of two; ws.h makes every such segment synchronous), NaNs or an overshoot of one ulp at an
+// exact tie of two wall distances
 // (probability ~1e-16 per crossing); a deferred segment that nevertheless ends in one (a
 // "hazard": its photon has gone on as if the walk had stayed inside) is counted in
 // SMCRT_CTR_FAULTS and in smcrt_kernel_times.lean_hazards, never silently dropped. The debug

@@ -519,6 +519,16 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                                 e.z <= ez;
             push = true;
             sync = !inside && !defer_all;
+            if constexpr (GM != 2) {
+              // faces k*2max/n and the cell of a point are rounded separately, so a start
+              // within an ulp of a face may lie outside its own cell: the walk's first wall
+              // distance is then negative, an error stop (:510-516) the photon must see. (GM 2:
+              // both exact, never.) Such a start is synchronous.
+              const bool in_cell = face<GM>(xf, ci - 1, K.fex) <= old.x && old.x <= face<GM>(xf, ci, K.fex) &&
+                                   face<GM>(yf, cj - 1, K.fey) <= old.y && old.y <= face<GM>(yf, cj, K.fey) &&
+                                   face<GM>(zf, ck - 1, K.fez) <= old.z && old.z <= face<GM>(zf, ck, K.fez);
+              if (!in_cell) sync = true;
+            }
           }
         }
         const uint64_t pm = __ballot(push);
@@ -985,8 +995,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       if (counters) {
         const uint32_t* c = sh->wctr[wv];
         const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
-                                             w_dep,         c[LC_UPD],     c[LC_TAU],      0u,             0u,
-                                             0u,            c[LC_FAULTS] + hz, c[LC_DRAWS], 0u,             c[LC_ESCAPED],
+                                             w_dep,         c[LC_UPD],     c[LC_TAU],      c[LC_FRES],     c[LC_REFL],
+                                             c[LC_BABORT],  c[LC_FAULTS] + hz, c[LC_DRAWS], c[LC_HITS],   c[LC_ESCAPED],
                                              w_iters};
         for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
           if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);

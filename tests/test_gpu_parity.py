@@ -967,6 +967,7 @@ def test_lean_kernel_paths(monkeypatch, case):
         assert (kt["lean_launches"] > 0) == (lean == "1"), (lean, kt)
         if lean == "1":  # the lean path runs only on the bucketed path: bk_reduce ran and was timed
             assert 0.0 < kt["fold_cu_ms"] < 1e3, kt
+            assert kt["lean_hazards"] == 0, kt  # (detectors: starts outside their cell are synchronous)
     cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True, dets=dets)
     for r in runs.values():
         compare(r, cpu)
