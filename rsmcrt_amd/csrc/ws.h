@@ -58,7 +58,7 @@
 namespace smcrt {
 
 #ifndef SMCRT_WS_PHOTON_WAVES
-#define SMCRT_WS_PHOTON_WAVES 4
+#define SMCRT_WS_PHOTON_WAVES 8
 #endif
 #ifndef SMCRT_WS_EVENT_WAVES
 #define SMCRT_WS_EVENT_WAVES 1
@@ -67,7 +67,7 @@ namespace smcrt {
 #define SMCRT_WS_SLOTS 2
 #endif
 #ifndef SMCRT_WS_WAVES
-#define SMCRT_WS_WAVES 8
+#define SMCRT_WS_WAVES 16
 #endif
 constexpr int WS_WAVES = SMCRT_WS_WAVES;  // waves per block (8: two blocks per CU, 16: one)
 constexpr int WS_THREADS = 64 * WS_WAVES;
