@@ -50,7 +50,7 @@ def main():
     if not os.path.exists(tr):
         tr = find(a.dir, "trace", "kernel_trace")
     disp = defaultdict(list)
-    for r in read(tr):
+    for r in (read(tr) if tr else []):
         k = short(r["Kernel_Name"])
         disp[k].append((int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6,
                         int(r["VGPR_Count"]), int(r["SGPR_Count"])))
@@ -69,7 +69,9 @@ def main():
             per[short(r["Kernel_Name"])][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
         for k, cs in per.items():
             if k not in out:
-                continue
+                if tr:
+                    continue
+                out[k] = {"dispatches": 0, "avg_ms_last": 0.0, "total_ms": 0.0}  # (a PMC-only directory)
             for c, v in cs.items():
                 v.sort()
                 tail = v[-a.last:]
@@ -77,8 +79,8 @@ def main():
     for k, d in out.items():
         if "WRITE_SIZE" in d or "FETCH_SIZE" in d:
             d["hbm_bytes_per_dispatch"] = 1024.0 * (d.get("WRITE_SIZE", 0.0) + 2.0 * d.get("FETCH_SIZE", 0.0))
-            d["hbm_GBps"] = d["hbm_bytes_per_dispatch"] / (d["avg_ms_last"] * 1e-3) / 1e9
-    tot = sum(d["avg_ms_last"] for k, d in out.items() if "rocclr" not in k and "elementwise" not in k)
+            d["hbm_GBps"] = d["hbm_bytes_per_dispatch"] / (d["avg_ms_last"] * 1e-3) / 1e9 if d["avg_ms_last"] else 0.0
+    tot = sum(d["avg_ms_last"] for k, d in out.items() if "rocclr" not in k and "elementwise" not in k) or 1.0
     for k, d in sorted(out.items(), key=lambda kv: -kv[1]["avg_ms_last"]):
         if "rocclr" in k or "elementwise" in k:
             continue
@@ -87,7 +89,7 @@ def main():
         print(f"{k:28s} n={d['dispatches']:3d} avg={d['avg_ms_last']:8.3f} ms ({100*d['avg_ms_last']/tot:5.1f}%)"
               f"{hb}{extra}")
     if a.traffic:
-        k = next((k for k in out if k.startswith(("transport_kernel", "lean_kernel")) and
+        k = next((k for k in out if k.startswith(("transport_kernel", "ws_kernel")) and
                   "hbm_bytes_per_dispatch" in out[k]), None)
         if k:
             # the whole step: the transport kernel plus the deposit-fold kernels that follow each
