@@ -66,6 +66,9 @@ namespace smcrt {
 #ifndef SMCRT_WS_SLOTS
 #define SMCRT_WS_SLOTS 2
 #endif
+#ifndef SMCRT_WS_DDA
+#define SMCRT_WS_DDA 2  // crossing steps per walker iteration (1: -2.5 %, profiles/r05_ws/ab_walker.txt)
+#endif
 #ifndef SMCRT_WS_WAVES
 #define SMCRT_WS_WAVES 16
 #endif
@@ -899,10 +902,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     uint32_t overflow = 0;
     // A walker lane without a segment holds a ticket of its own (`tk`, taken with one
     // wave-aggregated LDS add on `head`, which may run ahead of `tail`) and checks its entry
-    // once per iteration without waiting: its meta and fields are loaded together (LDS
-    // operations of one wave complete in order, and the producer stores meta last), and the lane
-    // takes the segment when meta shows written(tk). A ticket no photon will reserve (past the
-    // final tail once every photon wave has finished) is dropped.
+    // once per iteration without waiting: when its meta word shows written(tk) (acquire: the
+    // producer stores meta last, with release) the lane loads the fields and takes the segment.
+    // (Loading the fields with the meta word, before the check, measured the same.) Each
+    // iteration walks SMCRT_WS_DDA crossings of every held segment. A ticket no photon will
+    // reserve (past the final tail once every photon wave has finished) is dropped.
     bool pend = false;
     uint32_t tk = 0;
     for (;; ++w_iters) {
@@ -920,12 +924,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
       if (pend) {
         const uint32_t ix = tk & (WS_RING - 1);
-        const uint32_t m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (the field loads stay after the meta load)
-        const V3 o = v3(sh->ox[ix], sh->oy[ix], sh->oz[ix]);
-        const V3 dd = v3(sh->dx[ix], sh->dy[ix], sh->dz[ix]);
-        const double l = sh->sl[ix];
+        const uint32_t m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((m & WS_SEQ_MASK) == ws_tick(tk)) {
+          const V3 o = v3(sh->ox[ix], sh->oy[ix], sh->oz[ix]);
+          const V3 dd = v3(sh->dx[ix], sh->dy[ix], sh->dz[ix]);
+          const double l = sh->sl[ix];
           __hip_atomic_store(&sh->meta[ix], ws_tick(tk) | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
           W.old = o;
           wdir = dd;
@@ -959,13 +962,17 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
       // ---- one crossing of every held segment (dda_step: wall_dist, deposit, update_pos) ----
       WS_MARK(12);
-      bool dep = false;
-      uint32_t vox = 0;
-      double val = 0.0;
-      if (W.seg) dda_step_r<GM>(K, W, wdir, wrcp, xf, yf, zf, dep, vox, val, 1.0);
-      w_dep += __popcll(__ballot(dep));
-      WS_MARK(13);
-      emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+#pragma unroll
+      for (int k = 0; k < SMCRT_WS_DDA; ++k) {
+        if (k > 0 && !__ballot(W.seg)) break;
+        bool dep = false;
+        uint32_t vox = 0;
+        double val = 0.0;
+        if (W.seg) dda_step_r<GM>(K, W, wdir, wrcp, xf, yf, zf, dep, vox, val, 1.0);
+        w_dep += __popcll(__ballot(dep));
+        WS_MARK(13);
+        emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
+      }
       WS_MARK(14);
       // a finished segment: its cells and flags to the owner's slot, then the slot is free
       if ((am >> lane_id & 1ull) && !W.seg) {
