@@ -1004,6 +1004,18 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
                    h[20], h[21] / wi, h[22] / wi, h[23] / wi, h[24], h[25] / pt, h[30] / pt, h[27] / pt, h[26] / pt,
                    h[31] / pt, h[32] / pt, h[28] / pt, (double)h[29] / (double)std::max(1ull, h[28]), h[36] / pt, h[33],
                    h[34], (double)h[35] / (double)std::max(1ull, h[34]));
+      // region times (ws.h WST): shares of each role's wave time
+      const char* np[8] = {"fetch", "poll", "eval", "p3p4", "handout", "p5p6", "p7", "p8"};
+      double tp = 0, tw = 0, te = 0;
+      for (int i = 0; i < 8; ++i) tp += (double)h[37 + i];
+      for (int i = 0; i < 4; ++i) tw += (double)h[45 + i];
+      te = (double)h[49] + (double)h[50];
+      std::fprintf(stderr, "[diag-ws-time] photon:");
+      for (int i = 0; i < 8; ++i) std::fprintf(stderr, " %s=%.3f", np[i], (double)h[37 + i] / std::max(1.0, tp));
+      std::fprintf(stderr, " | walker: claim=%.3f idle=%.3f walk=%.3f finish=%.3f | event: run=%.3f idle=%.3f | "
+                   "ticks photon/walker/event %.3g/%.3g/%.3g\n", h[45] / std::max(1.0, tw), h[46] / std::max(1.0, tw),
+                   h[47] / std::max(1.0, tw), h[48] / std::max(1.0, tw), h[49] / std::max(1.0, te),
+                   h[50] / std::max(1.0, te), tp, tw, te);
     }
     unsigned long long lt = 0;
     for (int i = 0; i < 64; ++i) lt += h[i];

@@ -153,10 +153,21 @@ __device__ __forceinline__ uint32_t ws_load(uint32_t* p) {
 // Diagnostic builds (-DSMCRT_DIAG): wave-uniform tallies of the schedule in g_diag[20..39]
 // (kernels.h), printed per launch by the host ([diag-ws]).
 enum : int { WD_WITERS = 20, WD_WIDLE, WD_WBUSY, WD_WPEND, WD_PTRIPS, WD_PSLEEP, WD_PBLOCKED, WD_PWAIT, WD_P7,
-             WD_P7LANES, WD_PIDLE, WD_ELANES, WD_PUSH, WD_PRODWAIT, WD_EITERS, WD_ELANESRUN, WD_PEVQ, WD_N };
+             WD_P7LANES, WD_PIDLE, WD_ELANES, WD_PUSH, WD_PRODWAIT, WD_EITERS, WD_ELANESRUN, WD_PEVQ,
+             // s_memtime ticks per region (WST): photon waves, walker waves, event waves
+             WD_TP_FETCH, WD_TP_POLL, WD_TP_EVAL, WD_TP_P34, WD_TP_HAND, WD_TP_P56, WD_TP_P7, WD_TP_P8,
+             WD_TW_CLAIM, WD_TW_IDLE, WD_TW_WALK, WD_TW_FIN, WD_TE_RUN, WD_TE_IDLE, WD_N };
+static_assert(WD_N <= 64, "g_diag[64..] belongs to transport_kernel");
 #define WSDIAG(i, v) (wd[(i) - WD_WITERS] += (uint64_t)(v))
+#define WST(i)                                                \
+  do {                                                        \
+    const uint64_t now_ = __builtin_amdgcn_s_memtime();       \
+    wd[(i) - WD_WITERS] += now_ - tprev;                      \
+    tprev = now_;                                             \
+  } while (0)
 #else
 #define WSDIAG(i, v) do {} while (0)
+#define WST(i) do {} while (0)
 #endif
 
 // XF: scenes with Fresnel interfaces or detectors (their program points cost the photon waves
@@ -209,6 +220,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   uint32_t w_iters = 0, w_sdf = 0, w_dep = 0, hazards = 0;
 #ifdef SMCRT_DIAG
   uint64_t wd[WD_N - WD_WITERS] = {};
+  uint64_t tprev = __builtin_amdgcn_s_memtime();
 #endif
   if (wv < WS_PW) {
     WS_MARK(1);
@@ -284,6 +296,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         if (!more && P.st == ST_FETCH) P.st = ST_IDLE;
         if (__ballot(P.st != ST_IDLE) == 0) break;  // (walkers finish this wave's segments)
       }
+      WST(WD_TP_FETCH);
       // an event lane's results (see "Event waves"): the photon evaluates this trip
       if (P.has(LF_EVQ)) {
         const uint32_t code = __hip_atomic_load(&sh->ev_code[pl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -321,6 +334,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       WSDIAG(WD_PWAIT, __popcll(__ballot(P.has(LF_WAIT))));
       WSDIAG(WD_PEVQ, __popcll(__ballot(P.has(LF_EVQ))));
 
+      WST(WD_TP_POLL);
       // ---- EVAL: the SDF array at the photon's query point ------------------------------------
       const bool have = (P.f & (LF_PEND | LF_REQ | LF_WAIT)) == LF_PEND;
       EvalOut R;
@@ -349,6 +363,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         if (have) P.clr(LF_PEND);
       }
 
+      WST(WD_TP_EVAL);
       // ---- P3: consume the EVAL result -----------------------------------------------------
       if (have && (P.st == ST_H0 || P.st == ST_H3 || P.st == ST_M1)) {
         const uint32_t st0 = P.st;
@@ -496,6 +511,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
       }
 
+      WST(WD_TP_P34);
       // ---- hand the new segments to the block's ring (update_grids entry, :401-415) ------------
       if (__ballot(P.has(LF_REQ))) {
         bool push = false, sync = false;
@@ -565,6 +581,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
       }
 
+      WST(WD_TP_HAND);
       // ---- P5: a synchronous segment finished; after a segment: next program point ---------
       if (P.has(LF_WAIT) && !(ws_busy(sh, pl) & (1u << ((P.seq + WS_SLOTS - 1) % WS_SLOTS)))) {
         const unsigned long long w = sh->pcell[pl][(P.seq + WS_SLOTS - 1) % WS_SLOTS];
@@ -623,6 +640,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         P.st = ST_DONE;
       }
 
+      WST(WD_TP_P56);
       // ---- P7: the interactions and tauint2 entries go to the event waves -------------------
       {
         const bool qev = free_ && !test_kernel && !P.has(LF_EVQ) &&
@@ -770,6 +788,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
       }
 
+      WST(WD_TP_P7);
       // ---- P8: arrive at the hop-loop head, :61 ---------------------------------------------
       p8();
       // every photon of the wave waits for a walker (a synchronous segment or a free slot):
@@ -779,6 +798,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         WSDIAG(WD_PSLEEP, 1);
         __builtin_amdgcn_s_sleep(1);
       }
+      WST(WD_TP_P8);
     }
 #undef WLU
     if (lane_id == 0) atomicSub(&sh->alive, 1u);  // (after this wave's last push, in its LDS order)
@@ -823,6 +843,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           if (!__ballot(pend) && (int32_t)(ws_load(&sh->ev_head) - T) >= 0) break;
         }
         __builtin_amdgcn_s_sleep(2);
+        WST(WD_TE_IDLE);
         continue;
       }
       WSDIAG(WD_EITERS, 1);
@@ -882,6 +903,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         sh->ev_cached[o] = rg.cached;
         __hip_atomic_store(&sh->ev_code[o], res | EV_DONE, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      WST(WD_TE_RUN);
     }
   } else {
     WS_MARK(10);
@@ -949,6 +971,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       WSDIAG(WD_WIDLE, am ? 0 : 1);
       WSDIAG(WD_WBUSY, __popcll(am));
       WSDIAG(WD_WPEND, __popcll(__ballot(pend)));
+      WST(WD_TW_CLAIM);
       if (!am) {
         // nothing to walk: once every photon wave has finished, the final tail is known and the
         // tickets past it are never reserved; done when no lane holds an earlier one
@@ -958,6 +981,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           if (!__ballot(pend) && (int32_t)(ws_load(&sh->head) - T) >= 0) break;
         }
         __builtin_amdgcn_s_sleep(2);
+        WST(WD_TW_IDLE);
         continue;
       }
       // ---- one crossing of every held segment (dda_step: wall_dist, deposit, update_pos) ----
@@ -974,6 +998,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         emit_bucketed(K, C, WB, dep, vox, val, overflow, bstate);
       }
       WS_MARK(14);
+      WST(WD_TW_WALK);
       // a finished segment: its cells and flags to the owner's slot, then the slot is free
       if ((am >> lane_id & 1ull) && !W.seg) {
         const uint32_t owner = wmeta & 511u, slot = (wmeta >> 9) & 3u;
@@ -984,6 +1009,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         // (release: the slot's cells before the bit; the owner reads the bit with acquire)
         __hip_atomic_fetch_and(&sh->busy[owner], ~(1u << slot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      WST(WD_TW_FIN);
     }
     WS_MARK(15);
     close_buckets(K, C, WB, w_dep - overflow, overflow);
