@@ -9,14 +9,14 @@
 
 namespace smcrt {
 
-size_t kinst_ws_shared_bytes();    // sizeof(WsShared), ws_kernel's static LDS
+size_t kinst_ws_shared_bytes(int slots);  // sizeof(WsSharedT<slots>), ws_kernel's static LDS (slots 2 or 3)
 int kinst_ws_threads();            // ws_kernel's block size
 int kinst_ws_photon_lanes();       // photon lanes per ws_kernel block
 size_t kinst_ws_scratch_bytes(size_t lanes);  // ws_kernel lane scratch (ws.h WX_*) of that many photon lanes
 
 #define SMCRT_KINST_DECL(F, G)                                                               \
   const void* kinst_transport_##F##_##G(int xsrc, int coop);                                 \
-  const void* kinst_ws_##F##_##G(int xf);                                                    \
+  const void* kinst_ws_##F##_##G(int xf, int slots);                                         \
   void kinst_diag_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6);
 SMCRT_KINST_DECL(0, 0)
 SMCRT_KINST_DECL(0, 1)
@@ -40,16 +40,16 @@ inline const void* transport_kernel_ptr(bool lds_faces, int gm, bool xsrc, bool 
     default: return kinst_transport_1_2(x, c);
   }
 }
-// ws_kernel<lds_faces, gm, xf> (xf: the Fresnel/detector program points, ws.h)
-inline const void* ws_kernel_ptr(bool lds_faces, int gm, bool xf) {
+// ws_kernel<lds_faces, gm, xf, slots> (xf: the Fresnel/detector program points; slots 2 or 3, ws.h)
+inline const void* ws_kernel_ptr(bool lds_faces, int gm, bool xf, int slots) {
   const int x = xf ? 1 : 0;
   switch ((lds_faces ? 3 : 0) + gm) {
-    case 0: return kinst_ws_0_0(x);
-    case 1: return kinst_ws_0_1(x);
-    case 2: return kinst_ws_0_2(x);
-    case 3: return kinst_ws_1_0(x);
-    case 4: return kinst_ws_1_1(x);
-    default: return kinst_ws_1_2(x);
+    case 0: return kinst_ws_0_0(x, slots);
+    case 1: return kinst_ws_0_1(x, slots);
+    case 2: return kinst_ws_0_2(x, slots);
+    case 3: return kinst_ws_1_0(x, slots);
+    case 4: return kinst_ws_1_1(x, slots);
+    default: return kinst_ws_1_2(x, slots);
   }
 }
 // diagnostic builds: the kernels' tallies summed over the objects (each is cleared)

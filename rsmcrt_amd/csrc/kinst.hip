@@ -24,14 +24,15 @@ const void* KI_NAME(kinst_transport)(int xsrc, int coop) {
 }
 
 #if KI_F == 0 && KI_G == 0
-size_t kinst_ws_shared_bytes() { return sizeof(WsShared); }
+size_t kinst_ws_shared_bytes(int slots) { return slots == 3 ? sizeof(WsSharedT<3>) : sizeof(WsSharedT<2>); }
 int kinst_ws_threads() { return WS_THREADS; }
 int kinst_ws_photon_lanes() { return (int)WS_NPL; }
 size_t kinst_ws_scratch_bytes(size_t lanes) { return ws_scratch_bytes(lanes); }
 #endif
 
-const void* KI_NAME(kinst_ws)(int xf) {
-  return xf ? (const void*)ws_kernel<KI_F != 0, KI_G, true> : (const void*)ws_kernel<KI_F != 0, KI_G, false>;
+const void* KI_NAME(kinst_ws)(int xf, int slots) {
+  if (xf) return slots == 3 ? (const void*)ws_kernel<KI_F != 0, KI_G, true, 3> : (const void*)ws_kernel<KI_F != 0, KI_G, true, 2>;
+  return slots == 3 ? (const void*)ws_kernel<KI_F != 0, KI_G, false, 3> : (const void*)ws_kernel<KI_F != 0, KI_G, false, 2>;
 }
 
 

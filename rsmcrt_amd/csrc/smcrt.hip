@@ -138,6 +138,7 @@ struct smcrt_scene {
   int grid_blocks = 0;
   int grid_blocks_x = 0;  // the XSRC (general emitter) instantiation
   int grid_blocks_ws = 0;    // ws_kernel (ws.h): the lean path with photon, event and walker waves
+  int ws_slots = 3;          // its segment slots per photon: 3, or 2 when 3 do not fit the LDS (ws.h)
   // ws_kernel's lane scratch (ws.h WX_*) for scenes with Fresnel interfaces or detectors: one
   // region per launch stream (queue index, launch_one), lscratch_stride bytes apart
   double* d_lscratch = nullptr;
@@ -652,7 +653,11 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   {  // the lean path (ws.h): scenes with a few tops
     bool ok = s->bucketed && s->coop_lanes == 0 && grid->nx < (1 << 20) - 2 && grid->ny < (1 << 20) - 2 &&
               grid->nz < (1 << 20) - 2;
-    ok = ok && lean_lds(s) + kinst_ws_shared_bytes() <= 163840;
+    // three segment slots per photon when their LDS fits beside the tile words and faces, else
+    // two (SMCRT_WS_SLOTS=2 forces two)
+    const char* wsl = std::getenv("SMCRT_WS_SLOTS");
+    s->ws_slots = (!(wsl && wsl[0] == '2') && lean_lds(s) + kinst_ws_shared_bytes(3) <= 163840) ? 3 : 2;
+    ok = ok && lean_lds(s) + kinst_ws_shared_bytes(s->ws_slots) <= 163840;
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
     // Scenes with Fresnel interfaces or detectors (ws_kernel's XF instantiation) take the lean
@@ -670,7 +675,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0) s->wall_khz = khz;
   }
   if (s->lean_ok) {
-    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ws_kernel_ptr(s->lds_faces, s->grid_mode, s->d_lscratch != nullptr),
+    hipError_t oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ws_kernel_ptr(s->lds_faces, s->grid_mode, fresnel || n_dets > 0,
+                                                                               s->ws_slots),
                                                                  kinst_ws_threads(), lean_lds(s));
     if (oe != hipSuccess || per_cu < 1) per_cu = 1;
     s->grid_blocks_ws = cus * per_cu;
@@ -684,8 +690,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     }
   }
   if (std::getenv("SMCRT_VERBOSE"))
-    std::fprintf(stderr, "[smcrt] scene: lean %d (ws blocks/CU %d, static LDS %zu + dynamic %zu B), transport grid %d\n",
-                 (int)s->lean_ok, s->grid_blocks_ws / std::max(1, cus), kinst_ws_shared_bytes(), lean_lds(s),
+    std::fprintf(stderr, "[smcrt] scene: lean %d (ws slots %d, blocks/CU %d, static LDS %zu + dynamic %zu B), transport grid %d\n",
+                 (int)s->lean_ok, s->ws_slots, s->grid_blocks_ws / std::max(1, cus), kinst_ws_shared_bytes(s->ws_slots), lean_lds(s),
                  s->grid_blocks);
   for (int x = 0; x < 2; ++x) {
     const void* kfn = transport_fn(s, x == 1);
@@ -933,7 +939,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
     const smcrt_sdf_node* a_nodes = K.nodes;
     const ProgOp* a_prog = K.prog;
     void* args[] = {(void*)&K, (void*)&a_nodes, (void*)&a_prog, (void*)&Cc};
-    HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode, s->d_lscratch != nullptr), dim3(blocks), dim3(kinst_ws_threads()), args,
+    HIPCHK(hipLaunchKernel(ws_kernel_ptr(s->lds_faces, s->grid_mode, s->d_lscratch != nullptr, s->ws_slots), dim3(blocks), dim3(kinst_ws_threads()), args,
                            lean_lds(s), stream));
   } else {
     const KCold* Cc = C;

@@ -29,16 +29,19 @@
 // hazard accounting are lean.h's, so the records, counters and tallies are transport_kernel's;
 // only the order of the fp64 jmean sums differs.
 //
-// The block ring (multi-producer, multi-consumer, LDS). Tickets are matched one to one: photon
-// waves take them from `tail` (one reserved per segment), walker lanes from `head` (one held
-// per idle lane; head may run ahead of tail). Ticket t uses entry t mod WS_RING, whose `meta`
-// word is a sequence lock ordering the entry's laps:
+// Segments and the block ring. A photon's segment lives in one of its WS_SLOTS slots (`seg`,
+// structure of arrays over the photon lanes), which its busy bit guards: the photon writes a
+// slot only while the bit is clear and sets it, the walker clears it when the walk is done. The
+// ring (multi-producer, multi-consumer, LDS) carries only tokens: owner, slot, synchronous flag.
+// Tickets are matched one to one: photon waves take them from `tail` (one reserved per
+// segment), walker lanes from `head` (one held per idle lane; head may run ahead of tail).
+// Ticket t uses ring word t mod WS_RING, a sequence lock ordering the word's laps:
 //     written(t) -> consumed(t) -> written(t + WS_RING) -> consumed(t + WS_RING) -> ...
-//   * a photon wave reserves n tickets with one LDS add on `tail`; for each ticket t it waits
-//     until meta shows consumed(t - WS_RING) (the initial 0 for t < WS_RING), writes the entry
-//     and then meta = written(t) (owner, slot, sync flag, ticket) with a release store;
-//   * a walker lane that holds ticket t checks its entry once per iteration (no wait); when
-//     meta shows written(t) it takes the fields, stores meta = consumed(t) (release) and walks;
+//   * a photon wave reserves n tickets with one LDS add on `tail`; for each ticket t the lane
+//     writes its slot, sets its busy bit, waits until the word shows consumed(t - WS_RING) (the
+//     initial 0 for t < WS_RING) and stores written(t) with release (the slot before the token);
+//   * a walker lane that holds ticket t checks its word once per iteration (no wait); when it
+//     shows written(t) (acquire) the lane stores consumed(t), reads the owner's slot and walks;
 //   * every wait is a producer's, for the consumption of a strictly smaller ticket whose holder
 //     checks it every iteration, so the waits cannot form a cycle. In practice a producer never
 //     waits: a photon has at most WS_SLOTS segments in flight (its busy bits), WS_RING >=
@@ -48,7 +51,8 @@
 //     or past it, and a walker wave ends when it holds no segment and no earlier ticket.
 // Otherwise no wave waits for another except a photon for its synchronous segment (and the
 // bucket claims of deposit.h among the walker waves, whose bound is unchanged: only walkers
-// deposit).
+// deposit). An emission's position comes back in the start fields of the photon's next slot,
+// which must be free when the emission is queued.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -63,9 +67,6 @@ namespace smcrt {
 #ifndef SMCRT_WS_EVENT_WAVES
 #define SMCRT_WS_EVENT_WAVES 1
 #endif
-#ifndef SMCRT_WS_SLOTS
-#define SMCRT_WS_SLOTS 2
-#endif
 #ifndef SMCRT_WS_DDA
 #define SMCRT_WS_DDA 2  // crossing steps per walker iteration (1: -2.5 %, profiles/r05_ws/ab_walker.txt)
 #endif
@@ -77,38 +78,41 @@ constexpr int WS_THREADS = 64 * WS_WAVES;
 constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (waves 0 .. WS_PW-1)
 constexpr int WS_EW = SMCRT_WS_EVENT_WAVES;   // event waves (next), the rest walk
 static_assert(WS_PW >= 1 && WS_EW >= 1 && WS_PW + WS_EW < WS_WAVES, "a block needs all three roles");
-constexpr uint32_t WS_SLOTS = SMCRT_WS_SLOTS;  // segments a photon may have in flight (<= 4)
-static_assert(WS_SLOTS >= 1 && WS_SLOTS <= 4, "two slot bits in a meta word");
 constexpr uint32_t WS_NPL = 64u * WS_PW;  // photon lanes per block (<= 512: 9 owner bits)
 constexpr uint32_t ws_pow2(uint32_t v) { return v <= 1 ? 1 : 2 * ws_pow2((v + 1) / 2); }
 constexpr uint32_t WS_EQ = ws_pow2(WS_NPL);  // event queue entries (a photon has at most one event queued)
-constexpr uint32_t WS_RING = ws_pow2(WS_NPL * WS_SLOTS);
-static_assert(WS_RING >= WS_NPL * WS_SLOTS && WS_RING < (1u << 18), "ring bound");
 // meta word: owner (9 bits) | slot << 9 (2 bits) | synchronous << 11 | consumed << 12 |
 // ((ticket + 1) mod 2^19) << 13; 0 = never written
 constexpr uint32_t WS_CONSUMED = 1u << 12;
 constexpr uint32_t WS_SEQ_MASK = 0xFFFFF000u;  // ticket and consumed bit
 __device__ __forceinline__ uint32_t ws_tick(uint32_t t) { return ((t + 1u) & 0x7FFFFu) << 13; }
 
-struct WsShared {
-  double ox[WS_RING], oy[WS_RING], oz[WS_RING];  // start, corner coordinates
-  double dx[WS_RING], dy[WS_RING], dz[WS_RING];  // direction
-  double sl[WS_RING];                            // length
-  uint32_t meta[WS_RING];                        // written last (see above)
-  unsigned long long pcell[WS_NPL][WS_SLOTS];  // a finished segment: cells | tflag | fault
+enum : int { SG_OX = 0, SG_OY, SG_OZ, SG_DX, SG_DY, SG_DZ, SG_LEN, SG_N };  // segment fields
+// SL: segments a photon may have in flight (its slots). Three measured +2 % over two on M1
+// (profiles/r05_ws/ab_slots.txt); they need 146 KiB of LDS, so grids whose tile words and faces
+// do not fit beside them run the two-slot instantiation (109 KiB).
+template <uint32_t SL>
+struct WsSharedT {
+  static constexpr uint32_t SLOTS = SL;
+  static constexpr uint32_t RING = ws_pow2(WS_NPL * SL);  // ring words
+  static_assert(SL >= 1 && SL <= 4, "two slot bits in a meta word");
+  static_assert(RING >= WS_NPL * SL && RING < (1u << 18), "ring bound");
+  // a photon's segments in flight, one per slot (its busy bit guards the slot): start (corner
+  // coordinates), direction, length; the emitted position (EMIT, in a free slot's start)
+  double seg[SL][SG_N][WS_NPL];
+  uint32_t meta[RING];                           // the ring: owner, slot, flags, sequence lock
+  unsigned long long pcell[WS_NPL][SL];          // a finished segment: cells | tflag | fault
   uint32_t busy[WS_NPL];                         // bit s: slot s holds a segment in flight
   uint32_t lu[3][WS_NPL];                        // interactions, nscatt, status (LL_*)
   uint32_t wctr[WS_WAVES][LC_N];                 // per-wave counters
   // the event queue (see "Event waves" above): per photon lane an in/out slot, and a queue of
   // owner lanes with the ring's sequence lock
   double ev_dir[3][WS_NPL];   // in: direction; out: the scattered (or emitted) direction
-  double ev_pos[3][WS_NPL];   // out: the emitted position
-  unsigned long long ev_cells[WS_NPL];  // out: the emitted cells (lean_pack)
   double ev_cached[WS_NPL];   // in/out: the RNG's cached half block
   double ev_tau[WS_NPL];      // out: the new optical depth
   uint32_t ev_pid[2][WS_NPL]; // in: photon index words
   uint32_t ev_draws[WS_NPL];  // in/out: draws taken
-  uint32_t ev_code[WS_NPL];   // in: layer | kind << 16; out: EV_DONE | result bits (stored last)
+  uint32_t ev_code[WS_NPL];   // in: layer | kind << 16 | slot << 18; out: EV_DONE | result bits (stored last)
   uint32_t evq[WS_EQ];        // owner | consumed | ticket, as the ring's meta
   uint32_t head, tail;        // ring tickets: handed to walker lanes / reserved by photon waves
   uint32_t ev_head, ev_tail;  // event tickets: held by event lanes / reserved by photon waves
@@ -129,13 +133,15 @@ __host__ __device__ constexpr size_t ws_scratch_bytes(size_t lanes) {
   return lanes * (WX_ND * sizeof(double) + WXI_N * sizeof(uint32_t));
 }
 
-__device__ __forceinline__ void ws_count(WsShared* sh, int c) {
+template <class S>
+__device__ __forceinline__ void ws_count(S* sh, int c) {
   const uint64_t m = __ballot(1);
   if ((int)(threadIdx.x & 63) == __builtin_ctzll(m)) atomicAdd(&sh->wctr[threadIdx.x >> 6][c], (uint32_t)__popcll(m));
 }
 
 // the owner's view of its busy bits (another wave's walker clears them)
-__device__ __forceinline__ uint32_t ws_busy(WsShared* sh, uint32_t pl) {
+template <class S>
+__device__ __forceinline__ uint32_t ws_busy(S* sh, uint32_t pl) {
   return __hip_atomic_load(&sh->busy[pl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -172,10 +178,12 @@ static_assert(WD_N <= 64, "g_diag[64..] belongs to transport_kernel");
 
 // XF: scenes with Fresnel interfaces or detectors (their program points cost the photon waves
 // registers, so the other scenes run an instantiation without them)
-template <bool LDS_FACES, int GM, bool XF>
+template <bool LDS_FACES, int GM, bool XF, uint32_t SL>
 __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void ws_kernel(
     KParams K, const smcrt_sdf_node* __restrict__ nodes, const ProgOp* __restrict__ prog,
     const KCold* __restrict__ C) {
+  using WsShared = WsSharedT<SL>;
+  constexpr uint32_t WS_SLOTS = SL, WS_RING = WsShared::RING;
   __shared__ WsShared shm;
   WsShared* sh = &shm;
   const double eps = 1e-8;  // inttau2.f90:56
@@ -305,12 +313,14 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           P.rng.draws = sh->ev_draws[pl];
           P.rng.cached = sh->ev_cached[pl];
           if (P.st == ST_EMIT) {  // the emitted photon (its tauint2 entry follows the layer search)
-            P.pos = v3(sh->ev_pos[0][pl], sh->ev_pos[1][pl], sh->ev_pos[2][pl]);
+            P.pos = v3(sh->seg[P.seq][SG_OX][pl], sh->seg[P.seq][SG_OY][pl], sh->seg[P.seq][SG_OZ][pl]);
             P.dir = v3(sh->ev_dir[0][pl], sh->ev_dir[1][pl], sh->ev_dir[2][pl]);
             P.clr(LF_TFLAG);
             P.layer = (int32_t)(code & 0xFFFFu);
-            const unsigned long long w = sh->ev_cells[pl];
-            P.xcell = lean_cell(w, 0); P.ycell = lean_cell(w, 1); P.zcell = lean_cell(w, 2);
+            // (emit's own cells: vox_of of the emitted position, transport.h emit)
+            P.xcell = vox_of<GM>(P.pos.x, K.nx, K.xmax, K.inv2x, K.fex);
+            P.ycell = vox_of<GM>(P.pos.y, K.ny, K.ymax, K.inv2y, K.fey);
+            P.zcell = vox_of<GM>(P.pos.z, K.nz, K.zmax, K.inv2z, K.fez);
             P.set(LF_CELLS);
             if (code & EV_RUNAWAY) { P.set(LF_FAULT); P.st = ST_DONE; }  // (emission retries exhausted)
             else { P.st = ST_LAYER; P.set(LF_PEND); }
@@ -562,16 +572,18 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
             const uint32_t t = base + rank;
             const uint32_t ix = t & (WS_RING - 1);
-            // the entry's previous lap must have been consumed (see the header; no wait in practice)
+            // the segment into its slot (free: its busy bit is clear), then the ring token
+            double* const sg = &sh->seg[slot][0][pl];
+            sg[SG_OX * WS_NPL] = old.x; sg[SG_OY * WS_NPL] = old.y; sg[SG_OZ * WS_NPL] = old.z;
+            sg[SG_DX * WS_NPL] = P.dir.x; sg[SG_DY * WS_NPL] = P.dir.y; sg[SG_DZ * WS_NPL] = P.dir.z;
+            sg[SG_LEN * WS_NPL] = P.d;
+            atomicOr(&sh->busy[pl], 1u << slot);
+            // the token's previous lap must have been consumed (see the header; no wait in practice)
             const uint32_t prev = t < WS_RING ? 0u : (ws_tick(t - WS_RING) | WS_CONSUMED);
-            while (__hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev) {
+            while (__hip_atomic_load(&sh->meta[ix], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != prev) {
               WSDIAG(WD_PRODWAIT, 1);
               __builtin_amdgcn_s_sleep(1);
             }
-            sh->ox[ix] = old.x; sh->oy[ix] = old.y; sh->oz[ix] = old.z;
-            sh->dx[ix] = P.dir.x; sh->dy[ix] = P.dir.y; sh->dz[ix] = P.dir.z;
-            sh->sl[ix] = P.d;
-            atomicOr(&sh->busy[pl], 1u << slot);
             __hip_atomic_store(&sh->meta[ix], pl | (slot << 9) | (sync ? (1u << 11) : 0u) | ws_tick(t),
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             P.seq = P.seq + 1 == WS_SLOTS ? 0u : P.seq + 1;
@@ -646,7 +658,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const bool qev = free_ && !test_kernel && !P.has(LF_EVQ) &&
                          ((P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT)) &&
                            WLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS) ||
-                          P.st == ST_T2 || P.st == ST_EMIT);
+                          P.st == ST_T2 || (P.st == ST_EMIT && !(ws_busy(sh, pl) & (1u << P.seq))));
         const uint64_t qm = __ballot(qev);
         if (qm) {
           const int first = __builtin_ctzll(qm);
@@ -669,7 +681,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
               if constexpr (XF) XI[WXI_BOUNCES * xs] = 0;
             }
             sh->ev_code[pl] = (uint32_t)P.layer |
-                              ((P.st == ST_INTERACT ? WS_EV_INTERACT : (P.st == ST_T2 ? WS_EV_TAU : WS_EV_EMIT)) << 16);
+                              ((P.st == ST_INTERACT ? WS_EV_INTERACT : (P.st == ST_T2 ? WS_EV_TAU : WS_EV_EMIT)) << 16) |
+                              (P.seq << 18);
             __hip_atomic_store(&sh->evq[ix], pl | ws_tick(t), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             P.set(LF_EVQ);
           }
@@ -855,8 +868,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const uint32_t code = sh->ev_code[o];
         const int32_t layer = (int32_t)(code & 0xFFFFu);
         uint32_t res = 0;
-        bool tau_entry = (code >> 16) == WS_EV_TAU;
-        if ((code >> 16) == WS_EV_EMIT) {  // kernelsMod.f90:1937-1945 (emit until the cell is in the grid)
+        const uint32_t kind = (code >> 16) & 3u;
+        bool tau_entry = kind == WS_EV_TAU;
+        if (kind == WS_EV_EMIT) {  // kernelsMod.f90:1937-1945 (emit until the cell is in the grid)
           Lane L;
           L.rng = rg; L.xcell = L.ycell = L.zcell = 0; L.layer = 0; L.tflag = false;
           emit<GM, false>(K, C, L, 0u);
@@ -868,13 +882,13 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             emit<GM, false>(K, C, L, 0u);
           }
           rg = L.rng;
-          sh->ev_pos[0][o] = L.pos.x; sh->ev_pos[1][o] = L.pos.y; sh->ev_pos[2][o] = L.pos.z;
+          const uint32_t es = (code >> 18) & 3u;  // the owner's free slot carries the position
+          sh->seg[es][SG_OX][o] = L.pos.x; sh->seg[es][SG_OY][o] = L.pos.y; sh->seg[es][SG_OZ][o] = L.pos.z;
           sh->ev_dir[0][o] = L.dir.x; sh->ev_dir[1][o] = L.dir.y; sh->ev_dir[2][o] = L.dir.z;
-          sh->ev_cells[o] = lean_pack(L.xcell, L.ycell, L.zcell);
           if (!fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE) && C->emission)
             atomic_add_nr(C->emission + lin(K, L.xcell, L.ycell, L.zcell), 1.0);
           res = (fault ? EV_RUNAWAY : 0u) | ((uint32_t)L.layer & 0xFFFFu);
-        } else if ((code >> 16) == WS_EV_INTERACT) {  // kernelsMod.f90:1958-1975
+        } else if (kind == WS_EV_INTERACT) {  // kernelsMod.f90:1958-1975
           const TopProps pr = props[layer - 1];
           const double ran = rg.next(K.key0, K.key1);
           ++sh->lu[LL_INTER][o];
@@ -948,10 +962,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const uint32_t ix = tk & (WS_RING - 1);
         const uint32_t m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if ((m & WS_SEQ_MASK) == ws_tick(tk)) {
-          const V3 o = v3(sh->ox[ix], sh->oy[ix], sh->oz[ix]);
-          const V3 dd = v3(sh->dx[ix], sh->dy[ix], sh->dz[ix]);
-          const double l = sh->sl[ix];
-          __hip_atomic_store(&sh->meta[ix], ws_tick(tk) | WS_CONSUMED, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __hip_atomic_store(&sh->meta[ix], ws_tick(tk) | WS_CONSUMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          const double* const sg = &sh->seg[(m >> 9) & 3u][0][m & 511u];
+          const V3 o = v3(sg[SG_OX * WS_NPL], sg[SG_OY * WS_NPL], sg[SG_OZ * WS_NPL]);
+          const V3 dd = v3(sg[SG_DX * WS_NPL], sg[SG_DY * WS_NPL], sg[SG_DZ * WS_NPL]);
+          const double l = sg[SG_LEN * WS_NPL];
           W.old = o;
           wdir = dd;
           wrcp = v3(ieee_rcp_f64(dd.x), ieee_rcp_f64(dd.y), ieee_rcp_f64(dd.z));

@@ -931,8 +931,9 @@ def test_lean_kernel_paths(monkeypatch, case):
     * bounce-abort: an almost transparent n=1.5 sphere with an off-centre source, so photons
       caught by total internal reflection reach 1000 bounces and return to their tauint2
       entry (inttau2.f90:313-315).
-    Each case runs the lean path and transport_kernel (SMCRT_LEAN=0): same counters and
-    records."""
+    Each case runs the lean path with three and with two segment slots per photon
+    (SMCRT_WS_SLOTS=2, the instantiation of grids whose LDS cannot hold three) and
+    transport_kernel (SMCRT_LEAN=0): same counters and records."""
     from rsmcrt_amd.engine import Engine as E
     flags = abi.FLAG_PATHLENGTH
     g = scene.grid(48, 48, 48, 1, 1, 1)
@@ -958,11 +959,12 @@ def test_lean_kernel_paths(monkeypatch, case):
         sc, src, n = builders.setup_scat_test(10.0), scene.point_source(), 20000
         flags |= abi.FLAG_TEST_KERNEL
     runs = {}
-    for lean in ("1", "0"):
+    for lean, slots in (("1", "3"), ("1", "2"), ("0", "3")):
         monkeypatch.setenv("SMCRT_LEAN", lean)
+        monkeypatch.setenv("SMCRT_WS_SLOTS", slots)
         with E(sc, g, dets) as eng:
             eng.kernel_times()
-            runs[lean] = eng.run(src, n, seed=SEED, flags=flags, records=True)
+            runs[lean + slots] = eng.run(src, n, seed=SEED, flags=flags, records=True)
             kt = eng.kernel_times()
         assert (kt["lean_launches"] > 0) == (lean == "1"), (lean, kt)
         if lean == "1":  # the lean path runs only on the bucketed path: bk_reduce ran and was timed
@@ -980,7 +982,8 @@ def test_lean_kernel_paths(monkeypatch, case):
     if case == "absorbing":
         assert cpu.counter("absorbed") > n // 2
     if case == "test-kernel":
-        np.testing.assert_allclose(runs["1"].moments, cpu.moments, rtol=1e-12)
+        for k in ("13", "12"):
+            np.testing.assert_allclose(runs[k].moments, cpu.moments, rtol=1e-12)
 
 
 @pytest.mark.parametrize("knob", ["0", "all"])
