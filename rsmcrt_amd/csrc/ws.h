@@ -940,8 +940,10 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     // wave-aggregated LDS add on `head`, which may run ahead of `tail`) and checks its entry
     // once per iteration without waiting: when its meta word shows written(tk) (acquire: the
     // producer stores meta last, with release) the lane loads the fields and takes the segment.
-    // (Loading the fields with the meta word, before the check, measured the same.) Each
-    // iteration walks SMCRT_WS_DDA crossings of every held segment. A ticket no photon will
+    // (Loading the fields with the meta word, before the check, measured the same; a lane
+    // holding the ticket of its next segment while it walks, -15 %: the segment waits behind the
+    // lane's current one instead of going to an idle lane.) Each iteration walks SMCRT_WS_DDA
+    // crossings of every held segment. A ticket no photon will
     // reserve (past the final tail once every photon wave has finished) is dropped.
     bool pend = false;
     uint32_t tk = 0;
