@@ -817,6 +817,11 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     if (lane_id == 0) atomicSub(&sh->alive, 1u);  // (after this wave's last push, in its LDS order)
   } else if (wv < WS_PW + WS_EW) {
     WS_MARK(2);
+    // The event wave issues first on its SIMD (s_setprio 3): one event wave serves the block's
+    // 512 photons, and a photon waiting for its event waits for that wave's turn behind three
+    // other waves. +4.5-5 % on M1 (243-246 -> 256-258 M photons/s); the photon waves at 1 or 2
+    // changed nothing, the walkers at 1 lost 35 % (profiles/r05_ws/ab_prio.txt).
+    __builtin_amdgcn_s_setprio(3);
     // =================================================================== event waves =======
     // An event lane holds a ticket of the event queue (as a walker lane holds a ring ticket),
     // and when the queue entry shows written(ticket) it runs the owner's event: the code of
