@@ -97,8 +97,9 @@ enum : uint32_t {
   LF_EVQ = 256u,   // the photon's event is queued for the event waves (ws.h)
   LF_SSP = 512u,   // a refraction: X1 moves to the smallStepPos kept in the lane scratch (ws.h)
 };
-// event results (ws.h ev_code; the low 16 bits carry an emitted photon's layer)
-enum : uint32_t { EV_DONE = 1u << 31, EV_ABSORB = 1u << 30, EV_RUNAWAY = 1u << 29 };
+// event results (ws.h ev_code; the low 16 bits carry an emitted photon's layer); a Fresnel
+// event reports a fault (EV_RUNAWAY), a reflection or (neither) a refraction
+enum : uint32_t { EV_DONE = 1u << 31, EV_ABSORB = 1u << 30, EV_RUNAWAY = 1u << 29, EV_FR_REFLECT = 1u << 28 };
 struct LeanPhoton {
   V3 pos, dir;
   Rng rng;

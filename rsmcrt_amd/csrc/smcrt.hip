@@ -660,11 +660,11 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     ok = ok && lean_lds(s) + kinst_ws_shared_bytes(s->ws_slots) <= 163840;
     const char* le = std::getenv("SMCRT_LEAN");
     s->lean_mode = le ? (std::string(le) == "0" ? 0 : 1) : -1;
-    // Scenes with Fresnel interfaces or detectors (ws_kernel's XF instantiation) take the lean
-    // path only when forced (SMCRT_LEAN=1): their photon waves are the bottleneck (M5: walkers
-    // idle 64 % of their iterations) and transport_kernel measured faster, M3 145 vs 137.5 and
-    // M5 42.5 vs 31-38 M photons/s (profiles/r05_ws/ab_m1_blocks_m3_m5.txt)
-    s->lean_ok = ok && !s->nested && (s->lean_mode == 1 || (s->lean_mode != 0 && !fresnel && n_dets == 0));
+    // Scenes with detectors take the lean path only when forced (SMCRT_LEAN=1): record_hits at
+    // every segment end keeps their photon waves the bottleneck, and transport_kernel measured
+    // faster on M5 (43.0 vs 30.3-31.1 M photons/s). Fresnel scenes take it (reflect_refract runs
+    // in the event waves): M3 169.2-169.8 vs 144.0-144.3 (profiles/r05_ws/ab_m3_m5_fresnel_events.txt)
+    s->lean_ok = ok && !s->nested && (s->lean_mode == 1 || (s->lean_mode != 0 && n_dets == 0));
     const char* dm = std::getenv("SMCRT_DEBUG_LEAN_MARGIN");
     s->lean_debug = dm ? (std::string(dm) == "all" ? 2u : (std::string(dm) == "0" ? 1u : 0u)) : 0u;
   }

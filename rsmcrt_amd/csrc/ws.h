@@ -112,23 +112,25 @@ struct WsSharedT {
   double ev_tau[WS_NPL];      // out: the new optical depth
   uint32_t ev_pid[2][WS_NPL]; // in: photon index words
   uint32_t ev_draws[WS_NPL];  // in/out: draws taken
-  uint32_t ev_code[WS_NPL];   // in: layer | kind << 16 | slot << 18; out: EV_DONE | result bits (stored last)
+  uint32_t ev_code[WS_NPL];   // in: layer | kind << 16 | slot << 19; out: EV_DONE | result bits (stored last)
   uint32_t evq[WS_EQ];        // owner | consumed | ticket, as the ring's meta
   uint32_t head, tail;        // ring tickets: handed to walker lanes / reserved by photon waves
   uint32_t ev_head, ev_tail;  // event tickets: held by event lanes / reserved by photon waves
   uint32_t alive;
 };
-constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u, WS_EV_EMIT = 3u;  // event kinds (ev_code bits 16-17)
+// event kinds (ev_code bits 16-18; the photon's free slot in bits 19-20)
+constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u, WS_EV_EMIT = 3u, WS_EV_FRESNEL = 4u;
 
 // The lane scratch (global memory, KCold::lane_scratch, scenes with Fresnel interfaces or
 // detectors): per photon lane the state of the rare program points that the photon's
 // registers do not hold, structure of arrays over the launch's photon lanes
 // (blockIdx.x * WS_NPL + pl). Doubles: the tauint2 entry's pos and dir (the bounce abort
 // returns to them, inttau2.f90:313-315), the detector start point (startp, :125-131), the
-// Fresnel ds pair (F0) and the calcNormal taps (N1-N3, then the refraction's smallStepPos);
-// then 32-bit words: the new layer, the normal's SDF (Ls) and the bounce count.
-enum : int { WX_ENTRY = 0, WX_START = 6, WX_DS = 9, WX_TAP = 11, WX_ND = 14 };
-enum : int { WXI_NEWL = 0, WXI_LS, WXI_BOUNCES, WXI_N };
+// refraction's smallStepPos; then 32-bit words: the new layer and the bounce count. Only the
+// photon's own lane touches its scratch (what reflect_refract's event lane needs and returns
+// travels through LDS: the photon's free slot and its event slot).
+enum : int { WX_ENTRY = 0, WX_START = 6, WX_SSP = 9, WX_ND = 12 };
+enum : int { WXI_NEWL = 0, WXI_BOUNCES, WXI_N };
 __host__ __device__ constexpr size_t ws_scratch_bytes(size_t lanes) {
   return lanes * (WX_ND * sizeof(double) + WXI_N * sizeof(uint32_t));
 }
@@ -324,6 +326,32 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             P.set(LF_CELLS);
             if (code & EV_RUNAWAY) { P.set(LF_FAULT); P.st = ST_DONE; }  // (emission retries exhausted)
             else { P.st = ST_LAYER; P.set(LF_PEND); }
+          } else if (XF && P.st == ST_F0) {  // reflect_refract's outcome (surfaces.f90:14-84)
+            if (code & EV_RUNAWAY) {  // error stop :264-277
+              P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END;
+            } else if (code & EV_FR_REFLECT) {  // :304-316
+              X[WX_START * xs] = P.pos.x; X[(WX_START + 1) * xs] = P.pos.y; X[(WX_START + 2) * xs] = P.pos.z;
+              const uint32_t nb = XI[WXI_BOUNCES * xs] + 1u;
+              XI[WXI_BOUNCES * xs] = nb;
+              if (nb > 1000u) {  // :313-315: return without write-back, back to the tauint2 entry
+                ws_count(sh, LC_BABORT);
+                P.pos = v3(X[WX_ENTRY * xs], X[(WX_ENTRY + 1) * xs], X[(WX_ENTRY + 2) * xs]);
+                P.dir = v3(X[(WX_ENTRY + 3) * xs], X[(WX_ENTRY + 4) * xs], X[(WX_ENTRY + 5) * xs]);
+                P.st = ST_INTERACT;
+              } else {
+                P.dir = v3(sh->ev_dir[0][pl], sh->ev_dir[1][pl], sh->ev_dir[2][pl]);
+                P.st = ST_H0;
+                p8();
+              }
+            } else {  // refracted: cross with the new direction from smallStepPos, :284-303
+              X[WX_SSP * xs] = sh->seg[P.seq][SG_DX][pl];
+              X[(WX_SSP + 1) * xs] = sh->seg[P.seq][SG_DY][pl];
+              X[(WX_SSP + 2) * xs] = sh->seg[P.seq][SG_DZ][pl];
+              P.dir = v3(sh->ev_dir[0][pl], sh->ev_dir[1][pl], sh->ev_dir[2][pl]);
+              P.layer = (int32_t)XI[WXI_NEWL * xs];
+              P.st = ST_X1;
+              P.set(LF_REQ | LF_SSP);
+            }
           } else if (code & EV_ABSORB) {  // absorbed: recordWeight once the cells are in
             P.set(LF_TFLAG);
             P.st = ST_ABSORB;
@@ -351,22 +379,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       R.minabs = R.minv = R.va = R.vb = 0.0; R.maxloc = 0;
       if (__ballot(have)) {
         const bool mask_le = test_kernel && P.st == ST_LAYER;
-        V3 q = (P.st == ST_H1 || P.st == ST_G0 || P.st == ST_F1) ? P.pos + smul(P.d, P.dir) : P.pos;
-        // Fresnel: ds(new), ds(old) (F0, F1) and the calcNormal taps of Ls (N1-N4,
-        // sdf_base.f90:176-184) read those SDFs' values
-        int32_t capi = 0, capj = 0;
-        if (XF && have && P.st >= ST_F0 && P.st <= ST_N4) {
-          const bool fres = P.st == ST_F0 || P.st == ST_F1;
-          capi = (int32_t)XI[(fres ? WXI_NEWL : WXI_LS) * xs];
-          capj = fres ? P.layer : 0;
-          if (!fres) {
-            const double t = 1e-6;
-            q = P.st == ST_N1 ? P.pos + mul(v3(1.0, -1.0, -1.0), t)
-              : P.st == ST_N2 ? P.pos + mul(v3(-1.0, -1.0, 1.0), t)
-              : P.st == ST_N3 ? P.pos + mul(v3(-1.0, 1.0, -1.0), t) : P.pos + mul(v3(1.0, 1.0, 1.0), t);
-          }
-        }
-        R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, capi, capj);
+        const V3 q = (P.st == ST_H1 || P.st == ST_G0) ? P.pos + smul(P.d, P.dir) : P.pos;
+        R = eval_sdfs(nodes, prog, K.n_prog, q, mask_le, 0, 0);
         const bool counted = P.st == ST_H0 || P.st == ST_H1 || P.st == ST_H3 || P.st == ST_M1 || P.st == ST_G0;
         w_sdf += __popcll(__ballot(have && counted)) * (uint32_t)K.n_top;
         WSDIAG(WD_ELANES, __popcll(__ballot(have)));
@@ -387,74 +401,6 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         uint32_t ns = st0 == ST_M1 ? (out ? (uint32_t)ST_B0 : (uint32_t)ST_M0) : (done ? (uint32_t)ST_T2END : (uint32_t)ST_M0);
         if (small) { ns = ST_H1; P.set(LF_PEND); }
         P.st = ns;
-      } else if (XF && have && P.st >= ST_F0 && P.st <= ST_N4) {  // reflect_refract's program points
-        switch (P.st) {
-          case ST_F0:  // ds(new), ds(old) at pos
-            X[WX_DS * xs] = R.va; X[(WX_DS + 1) * xs] = R.vb;
-            P.st = ST_F1; P.set(LF_PEND);
-            break;
-          case ST_F1: {  // which SDF's normal, :250-277
-            const double ds_new = X[WX_DS * xs], ds_old = X[(WX_DS + 1) * xs], dn_new = R.va, dn_old = R.vb;
-            const int32_t new_layer = (int32_t)XI[WXI_NEWL * xs];
-            int32_t ls = 0;
-            if (dn_new < 0.0 && ds_new >= 0.0) ls = new_layer;
-            else if (dn_old >= 0.0 && ds_old < 0.0) ls = P.layer;
-            else if (dn_new < 0.0 && dn_old < 0.0) ls = new_layer;
-            else if (ds_old >= 0.0 && dn_old >= 0.0) ls = P.layer;
-            if (ls == 0) { P.set(LF_FAULT | LF_TFLAG); P.st = ST_T2END; break; }  // error stop :264-277
-            XI[WXI_LS * xs] = (uint32_t)ls;
-            P.st = ST_N1; P.set(LF_PEND);
-            break;
-          }
-          case ST_N1: case ST_N2: case ST_N3:  // calcNormal taps
-            X[(WX_TAP + (int)(P.st - ST_N1)) * xs] = R.va;
-            P.st = P.st + 1; P.set(LF_PEND);
-            break;
-          case ST_N4: {  // calcNormal (sdf_base.f90:166-190) + reflect_refract (surfaces.f90:14-84)
-            const double e1 = X[WX_TAP * xs], e2 = X[(WX_TAP + 1) * xs], e3 = X[(WX_TAP + 2) * xs], e4 = R.va;
-            const V3 xyy = v3(1.0, -1.0, -1.0), yyx = v3(-1.0, -1.0, 1.0), yxy = v3(-1.0, 1.0, -1.0),
-                     xxx = v3(1.0, 1.0, 1.0);
-            const V3 nn = ((mul(xyy, e1) + mul(yyx, e2)) + mul(yxy, e3)) + mul(xxx, e4);
-            const double ln = len(nn);
-            const V3 N = v3(nn.x / ln, nn.y / ln, nn.z / ln);
-            const int32_t new_layer = (int32_t)XI[WXI_NEWL * xs];
-            const double n1 = props[P.layer - 1].n, n2 = props[new_layer - 1].n;
-            ws_count(sh, LC_FRES);
-            const double Rf = fresnel(P.dir, N, n1, n2);
-            if (P.rng.next(K.key0, K.key1) <= Rf) {  // reflect :42-55, :304-316
-              const double s2 = 2.0 * dot(N, P.dir);
-              P.dir = P.dir - smul(s2, N);
-              ws_count(sh, LC_REFL);
-              X[WX_START * xs] = P.pos.x; X[(WX_START + 1) * xs] = P.pos.y; X[(WX_START + 2) * xs] = P.pos.z;
-              const uint32_t nb = XI[WXI_BOUNCES * xs] + 1u;
-              XI[WXI_BOUNCES * xs] = nb;
-              if (nb > 1000u) {  // :313-315: return without write-back
-                ws_count(sh, LC_BABORT);
-                P.pos = v3(X[WX_ENTRY * xs], X[(WX_ENTRY + 1) * xs], X[(WX_ENTRY + 2) * xs]);
-                P.dir = v3(X[(WX_ENTRY + 3) * xs], X[(WX_ENTRY + 4) * xs], X[(WX_ENTRY + 5) * xs]);
-                P.st = ST_INTERACT;
-              } else {
-                P.st = ST_H0;  // arrives in P8
-              }
-            } else {  // refract :57-84, transmit :284-303 (pos = smallStepPos, formed on the old dir)
-              const V3 ssp = P.pos + smul(P.d, P.dir);
-              X[WX_TAP * xs] = ssp.x; X[(WX_TAP + 1) * xs] = ssp.y; X[(WX_TAP + 2) * xs] = ssp.z;
-              const double eta = n1 / n2;
-              V3 Nt = N;
-              double c1 = dot(Nt, P.dir);
-              if (c1 < 0.0) c1 = -c1;
-              else Nt = smul(-1.0, N);
-              const double c2 = sqrt(1.0 - (eta * eta) * (1.0 - c1 * c1));
-              P.dir = smul(eta, P.dir) + smul(eta * c1 - c2, Nt);
-              P.layer = new_layer;
-              P.st = ST_X1;
-              P.set(LF_REQ | LF_SSP);
-            }
-            break;
-          }
-          default:
-            break;
-        }
       } else if (have) {
         switch (P.st) {
           case ST_LAYER:  // kernelsMod.f90:1948-1952 (test_kernel: mask ds<=0, :2136)
@@ -486,8 +432,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             }
             if (new_layer == 0) { P.set(LF_TFLAG); P.st = ST_T2END; break; }
             if (XF && props[P.layer - 1].n != props[new_layer - 1].n) {  // reflect_refract, :248
+              // (to the event waves: F0/F1, the calcNormal taps and the surface, see below)
               XI[WXI_NEWL * xs] = (uint32_t)new_layer;
-              P.st = ST_F0; P.set(LF_PEND);
+              P.st = ST_F0;
               break;
             }
             P.layer = new_layer;
@@ -607,7 +554,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       if (free_ && (P.st == ST_H2 || P.st == ST_B0 || P.st == ST_X1)) {
         if (P.st == ST_X1) {  // :326-335 / :294-303 (pos = smallStepPos)
           P.taurun = P.taurun + P.d * props[P.layer - 1].kappa;
-          if (XF && P.has(LF_SSP)) P.pos = v3(X[WX_TAP * xs], X[(WX_TAP + 1) * xs], X[(WX_TAP + 2) * xs]);
+          if (XF && P.has(LF_SSP)) P.pos = v3(X[WX_SSP * xs], X[(WX_SSP + 1) * xs], X[(WX_SSP + 2) * xs]);
           else P.pos = P.pos + smul(P.d, P.dir);
           P.clr(LF_SSP);
         }
@@ -658,7 +605,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const bool qev = free_ && !test_kernel && !P.has(LF_EVQ) &&
                          ((P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT)) &&
                            WLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS) ||
-                          P.st == ST_T2 || (P.st == ST_EMIT && !(ws_busy(sh, pl) & (1u << P.seq))));
+                          P.st == ST_T2 || (P.st == ST_EMIT && !(ws_busy(sh, pl) & (1u << P.seq))) ||
+                          (XF && P.st == ST_F0 && !(ws_busy(sh, pl) & (1u << P.seq))));
         const uint64_t qm = __ballot(qev);
         if (qm) {
           const int first = __builtin_ctzll(qm);
@@ -675,14 +623,20 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             sh->ev_cached[pl] = P.rng.cached;
             sh->ev_pid[0][pl] = P.rng.pid_lo; sh->ev_pid[1][pl] = P.rng.pid_hi;
             sh->ev_draws[pl] = P.rng.draws;
+            if (XF && P.st == ST_F0) {  // reflect_refract's inputs: pos and step in the free slot, the new layer
+              sh->seg[P.seq][SG_OX][pl] = P.pos.x; sh->seg[P.seq][SG_OY][pl] = P.pos.y;
+              sh->seg[P.seq][SG_OZ][pl] = P.pos.z; sh->seg[P.seq][SG_LEN][pl] = P.d;
+              sh->ev_tau[pl] = (double)XI[WXI_NEWL * xs];
+            }
             if (P.st == ST_EMIT) {  // kernelsMod.f90:1937-1945: a fresh packet
               P.clr(LF_FAULT); P.layer = 0;
               WLU(LL_STATUS) = 0; WLU(LL_NSCATT) = 0; WLU(LL_INTER) = 0;
               if constexpr (XF) XI[WXI_BOUNCES * xs] = 0;
             }
             sh->ev_code[pl] = (uint32_t)P.layer |
-                              ((P.st == ST_INTERACT ? WS_EV_INTERACT : (P.st == ST_T2 ? WS_EV_TAU : WS_EV_EMIT)) << 16) |
-                              (P.seq << 18);
+                              ((P.st == ST_INTERACT ? WS_EV_INTERACT
+                                : (P.st == ST_T2 ? WS_EV_TAU : (P.st == ST_EMIT ? WS_EV_EMIT : WS_EV_FRESNEL))) << 16) |
+                              (P.seq << 19);
             __hip_atomic_store(&sh->evq[ix], pl | ws_tick(t), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             P.set(LF_EVQ);
           }
@@ -873,7 +827,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         const uint32_t code = sh->ev_code[o];
         const int32_t layer = (int32_t)(code & 0xFFFFu);
         uint32_t res = 0;
-        const uint32_t kind = (code >> 16) & 3u;
+        const uint32_t kind = (code >> 16) & 7u;
         bool tau_entry = kind == WS_EV_TAU;
         if (kind == WS_EV_EMIT) {  // kernelsMod.f90:1937-1945 (emit until the cell is in the grid)
           Lane L;
@@ -887,12 +841,65 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             emit<GM, false>(K, C, L, 0u);
           }
           rg = L.rng;
-          const uint32_t es = (code >> 18) & 3u;  // the owner's free slot carries the position
+          const uint32_t es = (code >> 19) & 3u;  // the owner's free slot carries the position
           sh->seg[es][SG_OX][o] = L.pos.x; sh->seg[es][SG_OY][o] = L.pos.y; sh->seg[es][SG_OZ][o] = L.pos.z;
           sh->ev_dir[0][o] = L.dir.x; sh->ev_dir[1][o] = L.dir.y; sh->ev_dir[2][o] = L.dir.z;
           if (!fault && (K.flags & SMCRT_FLAG_RENDER_SOURCE) && C->emission)
             atomic_add_nr(C->emission + lin(K, L.xcell, L.ycell, L.zcell), 1.0);
           res = (fault ? EV_RUNAWAY : 0u) | ((uint32_t)L.layer & 0xFFFFu);
+        } else if (XF && kind == WS_EV_FRESNEL) {
+          // reflect_refract (inttau2.f90:248-328, surfaces.f90:14-84) for the owner: the ds pair
+          // at pos and at smallStepPos, which SDF's normal, calcNormal's four taps (sdf_base.f90:
+          // 166-190), the Fresnel draw, then the reflection (with the bounce count) or the
+          // refraction's direction; the owner's pos and step come in its free slot (es), the new
+          // layer in ev_tau; the bounce count and its abort are the owner's (photon waves)
+          const uint32_t es = (code >> 19) & 3u;
+          const V3 pos = v3(sh->seg[es][SG_OX][o], sh->seg[es][SG_OY][o], sh->seg[es][SG_OZ][o]);
+          const V3 dir0 = v3(sh->ev_dir[0][o], sh->ev_dir[1][o], sh->ev_dir[2][o]);
+          const int32_t new_layer = (int32_t)sh->ev_tau[o];
+          const V3 ssp = pos + smul(sh->seg[es][SG_LEN][o], dir0);
+          const EvalOut R0 = eval_sdfs(nodes, prog, K.n_prog, pos, false, new_layer, layer);
+          const EvalOut R1 = eval_sdfs(nodes, prog, K.n_prog, ssp, false, new_layer, layer);
+          const double ds_new = R0.va, ds_old = R0.vb, dn_new = R1.va, dn_old = R1.vb;
+          int32_t ls = 0;
+          if (dn_new < 0.0 && ds_new >= 0.0) ls = new_layer;
+          else if (dn_old >= 0.0 && ds_old < 0.0) ls = layer;
+          else if (dn_new < 0.0 && dn_old < 0.0) ls = new_layer;
+          else if (ds_old >= 0.0 && dn_old >= 0.0) ls = layer;
+          if (ls == 0) {
+            res = EV_RUNAWAY;  // error stop :264-277
+          } else {
+            const double t = 1e-6;
+            const double e1 = eval_sdfs(nodes, prog, K.n_prog, pos + mul(v3(1.0, -1.0, -1.0), t), false, ls, 0).va;
+            const double e2 = eval_sdfs(nodes, prog, K.n_prog, pos + mul(v3(-1.0, -1.0, 1.0), t), false, ls, 0).va;
+            const double e3 = eval_sdfs(nodes, prog, K.n_prog, pos + mul(v3(-1.0, 1.0, -1.0), t), false, ls, 0).va;
+            const double e4 = eval_sdfs(nodes, prog, K.n_prog, pos + mul(v3(1.0, 1.0, 1.0), t), false, ls, 0).va;
+            const V3 xyy = v3(1.0, -1.0, -1.0), yyx = v3(-1.0, -1.0, 1.0), yxy = v3(-1.0, 1.0, -1.0),
+                     xxx = v3(1.0, 1.0, 1.0);
+            const V3 nn = ((mul(xyy, e1) + mul(yyx, e2)) + mul(yxy, e3)) + mul(xxx, e4);
+            const double ln = len(nn);
+            const V3 N = v3(nn.x / ln, nn.y / ln, nn.z / ln);
+            const double n1 = props[layer - 1].n, n2 = props[new_layer - 1].n;
+            ws_count(sh, LC_FRES);
+            const double Rf = fresnel(dir0, N, n1, n2);
+            V3 dn;
+            if (rg.next(K.key0, K.key1) <= Rf) {  // reflect :42-55, :304-316
+              const double s2 = 2.0 * dot(N, dir0);
+              dn = dir0 - smul(s2, N);
+              ws_count(sh, LC_REFL);
+              res = EV_FR_REFLECT;
+            } else {  // refract :57-84 (pos = smallStepPos on the incoming direction, in the slot)
+              sh->seg[es][SG_DX][o] = ssp.x; sh->seg[es][SG_DY][o] = ssp.y; sh->seg[es][SG_DZ][o] = ssp.z;
+              const double eta = n1 / n2;
+              V3 Nt = N;
+              double c1 = dot(Nt, dir0);
+              if (c1 < 0.0) c1 = -c1;
+              else Nt = smul(-1.0, N);
+              const double c2 = sqrt(1.0 - (eta * eta) * (1.0 - c1 * c1));
+              dn = smul(eta, dir0) + smul(eta * c1 - c2, Nt);
+            }
+            sh->ev_dir[0][o] = dn.x; sh->ev_dir[1][o] = dn.y; sh->ev_dir[2][o] = dn.z;
+          }
         } else if (kind == WS_EV_INTERACT) {  // kernelsMod.f90:1958-1975
           const TopProps pr = props[layer - 1];
           const double ran = rg.next(K.key0, K.key1);
