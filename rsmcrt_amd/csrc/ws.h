@@ -2,28 +2,32 @@
 //
 // The path is noBiasPropagation kernelsMod.f90:1901-1976 -> tauint2 inttau2.f90:15-364 ->
 // update_grids :367-465, restated with transport_kernel's arithmetic (kernels.h), with the same
-// results bit for bit, for the scenes lean.h names (no Fresnel events, no detectors, no survival
-// bias, a plain source, bucketed path-length deposition).
+// results bit for bit, for scenes of few tops with no survival bias, a plain source and bucketed
+// path-length deposition (smcrt.hip: lean_ok; the XF instantiation adds Fresnel interfaces and
+// detectors).
 //
 // Why. A photon and its voxel walk want different code and different registers: the walk (a
 // crossing and the bucket emit) holds no photon state, the photon's code holds no walk. Round 4
 // ran both in every wave (lean_kernel, 167 VGPRs, three waves a SIMD); here a block of
-// WS_WAVES = 8 waves splits them, each role within 128 VGPRs (four waves a SIMD):
-//   * photon waves (WS_PW) run fetch, EVAL, P3/P4, the segment hand-out, P5/P6 and P8 on their
-//     64 photons; a segment (update_grids entry) goes into the BLOCK's ring in LDS;
-//   * walker waves take the oldest segments of the ring into idle lanes, walk them one
-//     crossing per iteration with dda_step_r (transport.h), file the records into the block's
-//     buckets (deposit.h) and, at a segment's end, write its final cells and flags into the
-//     owner photon's slot;
-//   * event waves (WS_EW) run the photons' interactions: the albedo roulette, scatter and the
-//     next tauint2 entry (kernelsMod.f90:1958-1975, photon.f90:1045-1103, inttau2.f90:48-60),
-//     the tauint2 entry after an emission, and the emission itself (kernelsMod.f90:1937-1945
-//     with the source's draws, photon.f90:311-710). A photon with such an event writes its
-//     direction, RNG state and layer into its slot, queues its lane in the block's event queue
-//     and waits; an event lane takes the queued owner, runs the event on the owner's values
-//     with the owner's own Philox stream and writes the results back, so the event code runs on
-//     full waves. Completion, the rare terminal interactions and every event of test_kernel
-//     runs (moments) stay in the photon waves, batched once SMCRT_LEAN_EVENT_LANES lanes wait.
+// WS_WAVES = 16 waves splits them, each role within 128 VGPRs (four waves a SIMD):
+//   * photon waves (WS_PW = 8) run fetch, EVAL, P3/P4, the segment hand-out, P5/P6 and P8 on
+//     their 64 photons; a segment (update_grids entry) goes into one of the photon's slots and a
+//     token for it into the block's ring in LDS;
+//   * walker waves (7) take the oldest tokens of the ring into idle lanes, walk the segments
+//     SMCRT_WS_DDA crossings per iteration with dda_step_r (transport.h), file the records into
+//     the block's buckets (deposit.h) and, at a segment's end, write its final cells and flags
+//     into the owner photon's slot;
+//   * event waves (WS_EW = 1, at issue priority 3) run the photons' interactions: the albedo
+//     roulette, scatter and the next tauint2 entry (kernelsMod.f90:1958-1975, photon.f90:
+//     1045-1103, inttau2.f90:48-60), the tauint2 entry after an emission, the emission itself
+//     (kernelsMod.f90:1937-1945 with the source's draws, photon.f90:311-710) and, in the XF
+//     instantiation, reflect_refract (inttau2.f90:248-328, surfaces.f90:14-84). A photon with
+//     such an event writes its direction, RNG state and layer into its event slot, queues its
+//     lane in the block's event queue and waits; an event lane takes the queued owner, runs the
+//     event on the owner's values with the owner's own Philox stream and writes the results
+//     back, so the event code runs on full waves. Completion, the rare terminal interactions
+//     and every event of test_kernel runs (moments) stay in the photon waves, batched once
+//     SMCRT_LEAN_EVENT_LANES lanes wait.
 // A segment's walk is a pure function of (start, direction, length) (the start cell is
 // recomputed from the start with the same cell_of) and the deferred/synchronous rule and the
 // hazard accounting are lean.h's, so the records, counters and tallies are transport_kernel's;
