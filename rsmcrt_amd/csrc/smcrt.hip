@@ -154,13 +154,11 @@ struct smcrt_scene {
   // starts in the grid is deferred (forces hazards on escaping segments)
   uint32_t lean_debug = 0;
   int64_t lean_launches = 0;  // since the last smcrt_scene_kernel_times
-  // voxel crossings per deposit segment, measured by the scene's launches (dep_ctl[6]): the
-  // lean kernel pays for decoupled walks with a refill per crossing step, which long segments
-  // do not repay (M0: 8.2 crossings per segment, -6 %; M1: 3.5, +5 %), so it is chosen only
-  // up to LEAN_MAX_XPS (SMCRT_LEAN=1 forces it, =0 disables it)
-  double xps = 0.0;
-  bool xps_measured = false;
-  int lean_mode = -1;  // -1 automatic, 0 off, 1 forced
+  // SMCRT_LEAN: -1 automatic, 0 off, 1 forced. (Rounds 3-4 chose lean_kernel only up to 5.5
+  // voxel crossings per segment: long walks were cheaper in one lane. ws_kernel's walker waves
+  // take them at any length: M0, 8.2 crossings per segment, 54.9 vs 43.4-44.2 M photons/s on
+  // transport_kernel, profiles/r05_ws/ab_m0.txt.)
+  int lean_mode = -1;
   // source spectrum tables of the last general-emitter run (srcplan.h), device copy
   std::vector<double> h_spec;
   double* d_spec = nullptr;
@@ -213,7 +211,6 @@ struct smcrt_scene {
 };
 
 constexpr size_t MAX_TIMED = 256;
-constexpr double LEAN_MAX_XPS = 5.5;  // the lean kernel's limit in crossings per segment (above)
 constexpr uint64_t COLD_PER_STREAM = 16;
 constexpr uint64_t COLD_SLOTS = COLD_PER_STREAM * (MAX_SLOTS + 1);  // a ring per launch stream
 constexpr uint32_t MAX_FUSED_HIST_TILES = 512;  // 8 KiB of LDS per block for the wave histograms
@@ -775,10 +772,6 @@ static void refine_rpp(smcrt_scene* s) {
       if (pool_log)
         std::fprintf(stderr, "[pool] slot %d: %u photons, %u records, %u overflowed, %u of %llu chunks\n", sl, h[4],
                      h[3], h[1], h[0], (unsigned long long)s->pool_chunks);
-      if (h[6] > 0) {  // voxel crossings per deposit segment of this scene's last launch
-        s->xps = (double)(h[3] + h[1]) / (double)h[6];
-        s->xps_measured = true;
-      }
       if (h[4] > 0) {
         const double rpp = (double)(h[3] + h[1]) / (double)h[4];
         s->rpp_est = std::max(1.0, rpp);
@@ -927,8 +920,7 @@ static int launch_one(smcrt_scene* s, KParams K, KCold Ch, bool xsrc, hipStream_
   // the lean path (ws_kernel, ws.h) when the scene and the run qualify: bucketed path-length
   // deposition, unit weights (no survival bias), a plain source
   const bool lean = !xsrc && s->lean_ok && K.bucket_tiles && (K.flags & SMCRT_FLAG_PATHLENGTH) &&
-                    !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS) &&
-                    (s->lean_mode == 1 || !s->xps_measured || s->xps <= LEAN_MAX_XPS);
+                    !(K.flags & SMCRT_FLAG_SURVIVAL_BIAS);
   const uint64_t ws_needed = (Ch.n_photons + kinst_ws_photon_lanes() - 1) / kinst_ws_photon_lanes();
   const int blocks = (int)std::min<uint64_t>(
       (uint64_t)(lean ? s->grid_blocks_ws : (xsrc ? s->grid_blocks_x : s->grid_blocks)),
