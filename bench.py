@@ -675,7 +675,9 @@ def main():
             # PMC HBM bytes of the whole step (transport + deposit folds) per launch.
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": traffic,
-                         "kernel": (pmc.get("kernel") or "transport_kernel").split("<")[0],
+                         # the kernel the timed launches ran: the lean path's ws_kernel or
+                         # transport_kernel (smcrt_kernel_times.lean_launches)
+                         "kernel": "ws_kernel" if kt.get("lean_launches", 0) > 0 else "transport_kernel",
                          "avg_launch_ms": kern_ms, "timing": timing_src,
                          "launches_timed": launches,
                          "algorithmic_bytes_per_launch": alg_bytes,
