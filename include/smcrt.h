@@ -380,7 +380,8 @@ typedef struct smcrt_kernel_times {
   double deposit_ms;    /* binned jmean fold: bin_hist .. bin_reduce */
   int64_t launches;     /* transport launches timed */
   int64_t lean_launches; /* of all launches since the last query (timed or not), those that ran
-                            the lean kernel (Fresnel-free, detector-free scenes) */
+                            the lean path (ws_kernel: scenes of few tops without detectors or
+                            survival bias) */
   int64_t far_steps;     /* march steps taken by the far-field march (long sphere-tracing runs with
                             only the nearest SDF re-evaluated) since the last query */
   double fold_cu_ms;     /* the deposit fold's own work since the last query: the sum of its reduce
@@ -388,7 +389,7 @@ typedef struct smcrt_kernel_times {
                             i.e. the whole-chip time it took, without the time it queued behind
                             transport launches (which deposit_ms includes) */
   /* ---- ABI 4 (the struct grew from 48 to 56 bytes) ---- */
-  int64_t lean_hazards;  /* deferred lean-kernel voxel walks that ended in tflag or an
+  int64_t lean_hazards;  /* deferred lean-path voxel walks that ended in tflag or an
                             error stop since the last query. Each is also counted in SMCRT_CTR_FAULTS: the
                             photon went on as if the walk had stayed inside the grid, so it no longer
                             follows the reference. Expected 0; only the debug knob

@@ -232,6 +232,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   __syncthreads();
 
   uint32_t w_iters = 0, w_sdf = 0, w_dep = 0, hazards = 0;
+  // per-lane tallies of the frequent counters, summed over the wave at the end (the rare ones
+  // go through ws_count into the wave's LDS counters)
+  uint32_t r_upd = 0, r_scat = 0, r_tau = 0, r_abs = 0;
 #ifdef SMCRT_DIAG
   uint64_t wd[WD_N - WD_WITERS] = {};
   uint64_t tprev = __builtin_amdgcn_s_memtime();
@@ -479,7 +482,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         V3 old = v3(0.0, 0.0, 0.0);
         const uint32_t slot = P.seq;
         if (P.has(LF_REQ) && !(ws_busy(sh, pl) & (1u << slot))) {  // (else: retry next trip)
-          ws_count(sh, LC_UPD);
+          ++r_upd;
           old = v3(P.pos.x + K.xmax, P.pos.y + K.ymax, P.pos.z + K.zmax);
           const int32_t ci = cell_of<GM>(old.x, K.nx, K.xmax, K.inv2x, K.fex),
                         cj = cell_of<GM>(old.y, K.ny, K.ymax, K.inv2y, K.fey),
@@ -672,7 +675,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
               const bool sc = ran < pr.albedo;
               ++WLU(LL_INTER);
               if (!sc) {
-                P.set(LF_TFLAG); WLU(LL_STATUS) = 1; ws_count(sh, LC_ABSORBED);
+                P.set(LF_TFLAG); WLU(LL_STATUS) = 1; ++r_abs;
                 // recordWeight(packet, 1.0) at the photon's cells once they are in (ST_ABSORB)
                 P.st = test_kernel ? ST_DONE : ST_ABSORB;
               } else {
@@ -682,7 +685,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                 P.dir = L.dir; P.rng = L.rng;
                 if (L.fault) P.set(LF_FAULT | LF_TFLAG);  // (renormalisation runaway)
                 const uint32_t st = ++WLU(LL_NSCATT);
-                ws_count(sh, LC_SCATTERS);
+                ++r_scat;
                 if (test_kernel) {
                   if (st >= 1 && st <= 4) {
                     double* const moments = C->moments;
@@ -704,7 +707,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             }
           }
           if (ev && P.st == ST_T2) {  // tauint2 entry, inttau2.f90:48-60
-            ws_count(sh, LC_TAU);
+            ++r_tau;
             t2_entry();
             P.tau = -det_log(P.rng.next(K.key0, K.key1));
             P.taurun = 0.0;
@@ -910,7 +913,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           ++sh->lu[LL_INTER][o];
           if (!(ran < pr.albedo)) {
             sh->lu[LL_STATUS][o] = 1;
-            ws_count(sh, LC_ABSORBED);
+            ++r_abs;
             res = EV_ABSORB;
           } else {
             Lane L;  // scatter, photon.f90:1045-1103
@@ -920,13 +923,13 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             rg = L.rng;
             if (L.fault) res = EV_RUNAWAY;  // (renormalisation runaway: tflag and a fault)
             ++sh->lu[LL_NSCATT][o];
-            ws_count(sh, LC_SCATTERS);
+            ++r_scat;
             sh->ev_dir[0][o] = L.dir.x; sh->ev_dir[1][o] = L.dir.y; sh->ev_dir[2][o] = L.dir.z;
             tau_entry = true;
           }
         }
         if (tau_entry) {  // tauint2 entry, inttau2.f90:48-60
-          ws_count(sh, LC_TAU);
+          ++r_tau;
           sh->ev_tau[o] = -det_log(rg.next(K.key0, K.key1));
         }
         sh->ev_draws[o] = rg.draws;
@@ -1052,23 +1055,25 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   {
     unsigned long long* const counters = C->counters;
     const uint32_t hz = wave_sum_u32(hazards);
+    const uint32_t n_upd = wave_sum_u32(r_upd), n_scat = wave_sum_u32(r_scat), n_tau = wave_sum_u32(r_tau),
+                   n_abs = wave_sum_u32(r_abs);
     if (lane_id == 0) {
       if (hz) {  // reported: smcrt_kernel_times.lean_hazards, and SMCRT_CTR_FAULTS
         atomicAdd(C->dep_ctl + 5, hz);
         atomicAdd(C->lean_hazards, (unsigned long long)hz);
       }
-      if (C->dep_ctl && sh->wctr[wv][LC_UPD]) atomicAdd(C->dep_ctl + 6, sh->wctr[wv][LC_UPD]);  // segments
+      if (C->dep_ctl && n_upd) atomicAdd(C->dep_ctl + 6, n_upd);  // segments
       if (counters) {
         const uint32_t* c = sh->wctr[wv];
-        const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], c[LC_SCATTERS], c[LC_ABSORBED], w_sdf,
-                                             w_dep,         c[LC_UPD],     c[LC_TAU],      c[LC_FRES],     c[LC_REFL],
+        const uint32_t v[SMCRT_NCOUNTERS] = {c[LC_PHOTONS], c[LC_RETRIES], n_scat,        n_abs,          w_sdf,
+                                             w_dep,         n_upd,         n_tau,          c[LC_FRES],     c[LC_REFL],
                                              c[LC_BABORT],  c[LC_FAULTS] + hz, c[LC_DRAWS], c[LC_HITS],   c[LC_ESCAPED],
                                              w_iters};
         for (int i = 0; i < SMCRT_NCOUNTERS; ++i)
           if (v[i]) atomicAdd(counters + i, (unsigned long long)v[i]);
       }
       double* const nscatt = C->nscatt;
-      if (nscatt && sh->wctr[wv][LC_SCATTERS]) atomic_add_nr(nscatt, (double)sh->wctr[wv][LC_SCATTERS]);
+      if (nscatt && n_scat) atomic_add_nr(nscatt, (double)n_scat);
     }
   }
 #ifdef SMCRT_DIAG
