@@ -986,6 +986,22 @@ def test_lean_kernel_paths(monkeypatch, case):
             np.testing.assert_allclose(runs[k].moments, cpu.moments, rtol=1e-12)
 
 
+def test_lean_path_two_slots_by_lds():
+    """A 2048 x 64 x 64 grid: its staged faces (17 KiB) and tile words do not fit beside three
+    segment slots per photon, so the lean path picks its two-slot instantiation by itself
+    (smcrt.hip: ws_slots); same photons as the oracle, bit for bit."""
+    from rsmcrt_amd.engine import Engine as E
+    sc, g = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0), scene.grid(2048, 64, 64, 1, 1, 1)
+    src, n = scene.point_source(), 3000
+    with E(sc, g) as eng:
+        eng.kernel_times()
+        gpu = eng.run(src, n, seed=SEED, flags=abi.FLAG_PATHLENGTH, records=True)
+        kt = eng.kernel_times()
+    assert kt["lean_launches"] > 0 and kt["lean_hazards"] == 0, kt
+    cpu = O.run(sc, g, src, n, seed=SEED, flags=abi.FLAG_PATHLENGTH, records=True)
+    compare(gpu, cpu)
+
+
 @pytest.mark.parametrize("knob", ["0", "all"])
 def test_lean_hazards_counted_as_faults(monkeypatch, knob):
     """A deferred lean-kernel walk (lean.h) must never end in tflag or an error stop; if one
