@@ -915,7 +915,7 @@ def test_multi_accumulate_dynamic_chunks_one_collect(monkeypatch):
 
 
 @pytest.mark.parametrize("case", ["absorbing", "boundary-source", "test-kernel", "fresnel", "detectors",
-                                  "bounce-abort"])
+                                  "bounce-abort", "fresnel-test-kernel"])
 def test_lean_kernel_paths(monkeypatch, case):
     """The lean path (ws_kernel, ws.h: Fresnel-free, detector-free scenes, the voxel walk and
     the interactions decoupled from the photon) against the oracle, photon by photon, on the paths it adds:
@@ -930,7 +930,9 @@ def test_lean_kernel_paths(monkeypatch, case):
       detector at the top face (record_hits from each segment's start point);
     * bounce-abort: an almost transparent n=1.5 sphere with an off-centre source, so photons
       caught by total internal reflection reach 1000 bounces and return to their tauint2
-      entry (inttau2.f90:313-315).
+      entry (inttau2.f90:313-315);
+    * fresnel-test-kernel: the Tran & Jacques sphere with test_kernel semantics, whose events
+      stay in the photon waves while its Fresnel events go to the event waves.
     Each case runs the lean path with three and with two segment slots per photon
     (SMCRT_WS_SLOTS=2, the instantiation of grids whose LDS cannot hold three) and
     transport_kernel (SMCRT_LEAN=0): same counters and records."""
@@ -938,8 +940,10 @@ def test_lean_kernel_paths(monkeypatch, case):
     flags = abi.FLAG_PATHLENGTH
     g = scene.grid(48, 48, 48, 1, 1, 1)
     dets = []
-    if case == "fresnel":
+    if case in ("fresnel", "fresnel-test-kernel"):
         sc, n = builders.setup_tran_and_jacques(), 30000
+        if case == "fresnel-test-kernel":
+            flags |= abi.FLAG_TEST_KERNEL
         src = scene.uniform_source((-0.25, 0.0, 0.99999), (0.5, 0.0, 0.0), (0.0, 0.0, 0.0), (0.0, 0.0, -1.0))
     elif case == "detectors":
         sc, n, g = builders.skin_layers(), 30000, scene.grid(48, 48, 48, 0.05, 0.05, 0.05)
@@ -973,7 +977,7 @@ def test_lean_kernel_paths(monkeypatch, case):
     cpu = O.run(sc, g, src, n, seed=SEED, flags=flags, records=True, dets=dets)
     for r in runs.values():
         compare(r, cpu)
-    if case in ("fresnel", "detectors"):
+    if case in ("fresnel", "detectors", "fresnel-test-kernel"):
         assert cpu.counter("fresnel") > n and cpu.counter("reflections") > 0
     if case == "detectors":
         assert cpu.counter("detector_hits") > 0
