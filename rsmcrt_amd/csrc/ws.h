@@ -304,6 +304,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           const uint64_t rank = __popcll(need & ((1ull << lane_id) - 1ull));
           if (P.st == ST_FETCH && rank < take) {
             P.rng.init(C->first_photon + chunk_base + rank);
+            sh->ev_pid[0][pl] = P.rng.pid_lo; sh->ev_pid[1][pl] = P.rng.pid_hi;  // (the event lanes' key)
             P.st = ST_EMIT;
           }
           chunk_base += take;
@@ -632,7 +633,6 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
               __builtin_amdgcn_s_sleep(1);  // (never in practice: one queued event per photon)
             sh->ev_dir[0][pl] = P.dir.x; sh->ev_dir[1][pl] = P.dir.y; sh->ev_dir[2][pl] = P.dir.z;
             sh->ev_cached[pl] = P.rng.cached;
-            sh->ev_pid[0][pl] = P.rng.pid_lo; sh->ev_pid[1][pl] = P.rng.pid_hi;
             sh->ev_draws[pl] = P.rng.draws;
             if (XF && P.st == ST_F0) {  // reflect_refract's inputs: pos and step in the free slot, the new layer
               sh->seg[P.seq][SG_OX][pl] = P.pos.x; sh->seg[P.seq][SG_OY][pl] = P.pos.y;
@@ -774,7 +774,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       if (__ballot(P.st != ST_IDLE && !(P.has(LF_WAIT) || P.has(LF_REQ) || P.has(LF_EVQ) ||
                                         (P.st == ST_ABSORB && !P.has(LF_CELLS)))) == 0) {
         WSDIAG(WD_PSLEEP, 1);
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(1);  // (0, 3: within noise)
       }
       WST(WD_TP_P8);
     }
