@@ -209,6 +209,15 @@ __device__ __forceinline__ uint32_t record_hits(const KParams& K, double* det_bi
     double t;
     int64_t bin = -1;
     double w = weight;
+    if (D->kind == SMCRT_DET_CIRCLE || D->kind == SMCRT_DET_ANNULUS) {
+      // A hit needs 0 < t <= pointSep for t = dot(pos - start, dir) / dot(dir, dir of the ray)
+      // as intersect_circle rounds it (numerator and denominator computed the same way here):
+      // a segment that cannot reach the detector's plane skips the intersection (no bin, and
+      // value1D is only read after a hit). The 1e-9 margin covers the quotient's rounding.
+      const double den = dot(ddir, dir);
+      const double num = dot(dpos - start, ddir);
+      if (!(den > 1e-6) || !(num > 0.0) || num > pointSep * den * (1.0 + 1e-9)) continue;
+    }
     if (D->kind == SMCRT_DET_CIRCLE) {
       bool hit = intersect_circle(ddir, dpos, D->radius, start, dir, t, value1D);
       if (hit && (t <= 0.0 || t > pointSep)) hit = false;
