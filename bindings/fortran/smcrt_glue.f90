@@ -22,7 +22,7 @@ module smcrt_glue
     implicit none
     private
 
-    public :: smcrt_optprop, smcrt_mono, smcrt_sdf
+    public :: smcrt_optprop, smcrt_mono, smcrt_spectral_props, smcrt_sdf
     public :: smcrt_sphere, smcrt_box, smcrt_torus, smcrt_cylinder, smcrt_triprism, smcrt_segment, &
               smcrt_capsule, smcrt_cone, smcrt_egg, smcrt_plane, smcrt_model
     public :: smcrt_revolution, smcrt_extrude, smcrt_onion, smcrt_twist, smcrt_bend, smcrt_elongate, &
@@ -34,8 +34,10 @@ module smcrt_glue
 
     !> init_mono's inputs (opticalProperties.f90:107-125); the engine derives kappa and the
     !> albedo exactly as init_mono does.
+    !> flags: SMCRT_NODE_ALBEDO_UNGUARDED for properties from updateSpectral.
     type :: smcrt_optprop
         real(c_double) :: mus = 0._c_double, mua = 0._c_double, hgg = 0._c_double, n = 1._c_double
+        integer(c_int32_t) :: flags = 0
     end type smcrt_optprop
 
     !> One element of the reference's array(:) (sdf_base.f90:27-52): a primitive, or a model
@@ -52,6 +54,32 @@ contains
         type(smcrt_optprop) :: o
         o = smcrt_optprop(mus=mus, mua=mua, hgg=hgg, n=n)
     end function smcrt_mono
+
+    !> spectral(mus, mua, hgg, n, flux) (opticalProperties.f90:127-156) and updateSpectral
+    !> (:171-201): each argument an array(n, 2) as the reference takes them. mode is one of
+    !> SMCRT_SPECTRAL_* (default SMCRT_SPECTRAL_INIT); draw is the position in the seed's host
+    !> stream (include/smcrt.h), advanced by the draws taken; wavelength returns the sample.
+    function smcrt_spectral_props(mus, mua, hgg, n, flux, seed, draw, mode, wavelength) result(o)
+        real(c_double), target, intent(in) :: mus(:, :), mua(:, :), hgg(:, :), n(:, :), flux(:, :)
+        integer(c_int64_t), intent(in) :: seed
+        integer(c_int64_t), intent(inout) :: draw
+        integer(c_int32_t), optional, intent(in) :: mode
+        real(c_double), optional, intent(out) :: wavelength
+        type(smcrt_optprop) :: o
+        type(smcrt_spectral) :: sp
+        type(smcrt_optprops) :: p
+        real(c_double), allocatable, target :: a(:, :), b(:, :), c(:, :), d(:, :), e(:, :)
+        integer(c_int32_t) :: m
+        m = SMCRT_SPECTRAL_INIT
+        if (present(mode)) m = mode
+        a = mus; b = mua; c = hgg; d = n; e = flux   ! contiguous copies
+        sp%n_mus = size(a, 1); sp%n_mua = size(b, 1); sp%n_hgg = size(c, 1); sp%n_n = size(d, 1)
+        sp%n_flux = size(e, 1)
+        sp%mus = c_loc(a); sp%mua = c_loc(b); sp%hgg = c_loc(c); sp%n = c_loc(d); sp%flux = c_loc(e)
+        if (smcrt_spectral_sample(sp, m, seed, draw, p) /= 0) error stop "smcrt_spectral_sample failed"
+        o = smcrt_optprop(mus=p%mus, mua=p%mua, hgg=p%hgg, n=p%n, flags=p%node_flags)
+        if (present(wavelength)) wavelength = p%wavelength
+    end function smcrt_spectral_props
 
     ! ------------------------------------------------------------ transforms ---------------
     function smcrt_identity() result(t)
@@ -150,6 +178,7 @@ contains
         s%node%transform = reshape(t, [16])   ! column-major, as sdf_base.f90:21
         s%node%param(1:size(param)) = param
         s%node%mus = op%mus; s%node%mua = op%mua; s%node%hgg = op%hgg; s%node%n = op%n
+        s%node%flags = op%flags
     end function prim
 
     function smcrt_sphere(radius, op, layer, transform) result(s)  ! sphere_init :463-492
@@ -261,6 +290,7 @@ contains
         s%node%layer = array(1)%node%layer
         s%node%mus = array(1)%node%mus; s%node%mua = array(1)%node%mua
         s%node%hgg = array(1)%node%hgg; s%node%n = array(1)%node%n
+        s%node%flags = array(1)%node%flags
         s%node%n_children = int(size(array), c_int32_t)
         allocate(s%children, source=array)
     end function smcrt_model
@@ -279,6 +309,7 @@ contains
         s%node%layer = prim_sdf%node%layer
         s%node%mus = prim_sdf%node%mus; s%node%mua = prim_sdf%node%mua
         s%node%hgg = prim_sdf%node%hgg; s%node%n = prim_sdf%node%n
+        s%node%flags = prim_sdf%node%flags
         s%node%n_children = 1
         allocate(s%children(1))
         s%children(1) = prim_sdf

@@ -20,7 +20,7 @@ module smcrt_mod
     integer(c_int32_t), parameter :: SMCRT_SDF_REVOLUTION = 12, SMCRT_SDF_EXTRUDE = 13, SMCRT_SDF_ONION = 14, &
         SMCRT_SDF_TWIST = 15, SMCRT_SDF_BEND = 16, SMCRT_SDF_ELONGATE = 17, SMCRT_SDF_DISPLACEMENT = 18
     integer(c_int32_t), parameter :: SMCRT_DISP_SINE = 1
-    integer(c_int), parameter :: SMCRT_MOD_ABI_VERSION = 4  ! compare with smcrt_abi_version()
+    integer(c_int), parameter :: SMCRT_MOD_ABI_VERSION = 5  ! compare with smcrt_abi_version()
     ! smcrt_csg_op
     integer(c_int32_t), parameter :: SMCRT_OP_UNION = 0, SMCRT_OP_SMOOTH_UNION = 1, &
         SMCRT_OP_SUBTRACTION = 2, SMCRT_OP_INTERSECTION = 3
@@ -55,7 +55,8 @@ module smcrt_mod
 
     type, bind(C) :: smcrt_sdf_node
         integer(c_int32_t) :: kind = 0, layer = 0, op = 0, first_child = 0, n_children = 0
-        integer(c_int32_t) :: reserved(3) = 0
+        integer(c_int32_t) :: flags = 0       ! SMCRT_NODE_* (ABI 5)
+        integer(c_int32_t) :: reserved(2) = 0
         real(c_double)     :: transform(16) = 0._c_double   ! = reshape(sdf%transform, [16])
         real(c_double)     :: param(12) = 0._c_double
         real(c_double)     :: k = 0._c_double
@@ -122,6 +123,22 @@ module smcrt_mod
         real(c_double)     :: dir(3) = [0._c_double, 0._c_double, 1._c_double], rotation = 0._c_double
     end type smcrt_escape_config
 
+    ! ABI 5: spectral optical properties (opticalProperties.f90:127-201)
+    integer(c_int32_t), parameter :: SMCRT_NODE_ALBEDO_UNGUARDED = 1
+    integer(c_int32_t), parameter :: SMCRT_SPECTRAL_INIT = 0, SMCRT_SPECTRAL_UPDATE = 1, &
+        SMCRT_SPECTRAL_INIT_AS_WRITTEN = 2
+
+    type, bind(C) :: smcrt_spectral               ! five piecewise1D array(n, 2) tables
+        integer(c_int64_t) :: n_mus = 0, n_mua = 0, n_hgg = 0, n_n = 0, n_flux = 0
+        type(c_ptr)        :: mus = c_null_ptr, mua = c_null_ptr, hgg = c_null_ptr, n = c_null_ptr, &
+                              flux = c_null_ptr
+    end type smcrt_spectral
+
+    type, bind(C) :: smcrt_optprops               ! opticalProp_base's fields + the wavelength
+        real(c_double)     :: mus = 0, mua = 0, hgg = 0, g2 = 0, n = 0, kappa = 0, albedo = 0, wavelength = 0
+        integer(c_int32_t) :: node_flags = 0, reserved = 0
+    end type smcrt_optprops
+
     type, bind(C) :: smcrt_inverse_config         ! the [inverse] table
         integer(c_int32_t) :: layer, flags, max_steps = 1000, reserved = 0
         real(c_double)     :: max_step_size = 1._c_double, grad_step_size = 1e-4_c_double, accuracy = 0.01_c_double
@@ -185,6 +202,28 @@ module smcrt_mod
             integer(c_int32_t), value :: top_index
             real(c_double), value     :: mus, mua, hgg, n
         end function smcrt_scene_set_optprops
+
+        integer(c_int) function smcrt_spectral_sample(sp, mode, seed, draw, out) &
+                bind(C, name="smcrt_spectral_sample")
+            import :: c_int, c_int32_t, c_int64_t, smcrt_spectral, smcrt_optprops
+            type(smcrt_spectral), intent(in)  :: sp
+            integer(c_int32_t), value         :: mode
+            integer(c_int64_t), value         :: seed
+            integer(c_int64_t), intent(inout) :: draw
+            type(smcrt_optprops), intent(out) :: out
+        end function smcrt_spectral_sample
+
+        integer(c_int) function smcrt_scene_set_spectral(scene, top_index, sp, mode, seed, draw, out) &
+                bind(C, name="smcrt_scene_set_spectral")
+            import :: c_int, c_int32_t, c_int64_t, c_ptr, smcrt_spectral, smcrt_optprops
+            type(c_ptr), value                :: scene
+            integer(c_int32_t), value         :: top_index
+            type(smcrt_spectral), intent(in)  :: sp
+            integer(c_int32_t), value         :: mode
+            integer(c_int64_t), value         :: seed
+            integer(c_int64_t), intent(inout) :: draw
+            type(smcrt_optprops), intent(out) :: out
+        end function smcrt_scene_set_spectral
 
         integer(c_int) function smcrt_run(scene, src, cfg, io) bind(C, name="smcrt_run")
             import :: c_int, c_ptr, smcrt_source, smcrt_run_config, smcrt_tallies

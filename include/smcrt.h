@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SMCRT_ABI_VERSION 4
+#define SMCRT_ABI_VERSION 5
 
 typedef enum smcrt_status {
   SMCRT_OK = 0,
@@ -109,13 +109,18 @@ typedef struct smcrt_sdf_node {
   int32_t op;          /* smcrt_csg_op, MODEL only */
   int32_t first_child; /* MODEL only */
   int32_t n_children;  /* MODEL only */
-  int32_t reserved[3];
+  int32_t flags;       /* SMCRT_NODE_* (ABI 5; was reserved, 0 keeps init_mono's rules) */
+  int32_t reserved[2];
   double transform[16]; /* Fortran t(4,4), column-major: transform[(c-1)*4+(r-1)] = t(r,c).
                            p = pos .dot. t (vector_class.f90:292-304) */
   double param[12];
   double k;            /* MODEL smoothing parameter */
   double mus, mua, hgg, n;
 } smcrt_sdf_node;
+
+/* smcrt_sdf_node.flags (ABI 5). */
+#define SMCRT_NODE_ALBEDO_UNGUARDED 1 /* albedo = mus / kappa without init_mono's "albedo = 1 when
+                                         mua < 1e-9" (updateSpectral, opticalProperties.f90:197-199) */
 
 /* ----------------------------------------------------------------- grid ---------- */
 /* cart_grid (grid.f90:14-25, init_grid_cart :119-159): voxel faces at (i-1)*2*max/n. */
@@ -323,6 +328,56 @@ int smcrt_scene_det_bins(const smcrt_scene* scene, int64_t* n_doubles);
  * sdf_base.f90:255-263; used by inverse MCRT). */
 int smcrt_scene_set_optprops(smcrt_scene* scene, int32_t top_index,
                              double mus, double mua, double hgg, double n);
+
+/* ---- ABI 5: spectral optical properties (opticalProperties.f90:127-201) -------------------
+ * The reference's `spectral` type holds five piecewise1D tables (init_piecewise1D,
+ * piecewise.f90:142-168; array(n, 2): x = wavelength, y = value) and derives mono-equivalent
+ * properties from them: init_spectral when it is constructed, updateSpectral on each update.
+ * No reference input file selects it and its run_MCRT never calls update, so a spectral layer
+ * is a host-side sampler whose result is written into one top-level SDF's properties between
+ * runs (smcrt_scene_set_spectral); the transport kernels see an ordinary layer.
+ * Draws come from a host Philox4x32-10 stream keyed by `seed` (the reference's global ran2
+ * stream cannot be reproduced): draw d is the (d & 1) half of block (d >> 1, 2, 0, 0xFFFFFFFF).
+ * `*draw` is the caller's position in that stream; each sampled table takes one draw and
+ * advances it, so successive updates continue the stream. */
+typedef struct smcrt_spectral {
+  int64_t n_mus, n_mua, n_hgg, n_n, n_flux; /* rows of each array(n, 2); every n >= 2 */
+  const double* mus;  /* Fortran array(n, 2): x = a[0 .. n), y = a[n .. 2n) */
+  const double* mua;
+  const double* hgg;
+  const double* n;
+  const double* flux; /* the wavelength pdf */
+} smcrt_spectral;
+
+typedef enum smcrt_spectral_mode {
+  /* init_spectral as documented (:141-155): a wavelength from the flux CDF (one draw), then
+   * mus, mua, hgg and n interpolated at it (sample1D with value, piecewise.f90:132-137);
+   * kappa = mus + mua, albedo = 1 when mua < 1e-9. */
+  SMCRT_SPECTRAL_INIT = 0,
+  /* updateSpectral (:171-201): the same draw and interpolation; albedo = mus / kappa with no
+   * guard (out->node_flags = SMCRT_NODE_ALBEDO_UNGUARDED). */
+  SMCRT_SPECTRAL_UPDATE = 1,
+  /* init_spectral as compiled (:142-148): the properties are sampled with sample(x, y), i.e.
+   * without a value, so each is an inverse-CDF draw of its own table's x axis (a wavelength),
+   * one draw each after the flux's (five draws); `wave` is only passed as the unused y. */
+  SMCRT_SPECTRAL_INIT_AS_WRITTEN = 2
+} smcrt_spectral_mode;
+
+typedef struct smcrt_optprops {
+  double mus, mua, hgg, g2, n, kappa, albedo; /* opticalProp_base's fields */
+  double wavelength;  /* the flux-sampled wavelength (updateSpectral's intent(out)) */
+  int32_t node_flags; /* SMCRT_NODE_* that make a node derive kappa/albedo as above */
+  int32_t reserved;
+} smcrt_optprops;
+
+/* Sample a spectral layer's properties. INVALID_ARG for a NULL table, n < 2 or a bad mode. */
+int smcrt_spectral_sample(const smcrt_spectral* sp, int32_t mode, uint64_t seed, uint64_t* draw,
+                          smcrt_optprops* out);
+
+/* smcrt_spectral_sample, then write the result into top-level SDF `top_index` (mus, mua, hgg,
+ * n and the node flags; like smcrt_scene_set_optprops). `out` may be NULL. */
+int smcrt_scene_set_spectral(smcrt_scene* scene, int32_t top_index, const smcrt_spectral* sp, int32_t mode,
+                             uint64_t seed, uint64_t* draw, smcrt_optprops* out);
 
 /* Run cfg->n_photons photons (the body of run_MCRT) and accumulate into `io`.
  * Synchronous: returns when the tallies are in host memory. */

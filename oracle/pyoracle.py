@@ -63,6 +63,8 @@ def lib():
             L.oracle_record_hit.argtypes = [C.POINTER(abi.Detector), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                             C.c_double, C.c_int32, C.c_double, C.POINTER(C.c_double),
                                             C.POINTER(C.c_uint64)]
+            L.oracle_spectral_sample.argtypes = [C.POINTER(abi.Spectral), C.c_int32, C.c_uint64,
+                                                 C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
             _lib = L
     return _lib
 
@@ -89,6 +91,24 @@ def log(x):
 
 def atan(x):
     return lib().oracle_atan(float(x))
+
+
+def spectral_sample(tables, mode, seed, draw=0):
+    """The restatement of init_spectral / updateSpectral (opticalProperties.f90:127-201) on
+    five (n, 2) tables (mus, mua, hgg, n, flux): (dict of mus, mua, hgg, g2, n, kappa, albedo,
+    wavelength; the stream position after it)."""
+    arrs = [np.asfortranarray(np.asarray(a, dtype=np.float64)) for a in tables]
+    sp = abi.Spectral()
+    for name, a in zip(("mus", "mua", "hgg", "n", "flux"), arrs):
+        setattr(sp, "n_" + name, a.shape[0])
+        setattr(sp, name, _dp(a))
+    d = C.c_uint64(draw)
+    out = np.zeros(8)
+    st = lib().oracle_spectral_sample(C.byref(sp), mode, seed, C.byref(d), _dp(out))
+    if st != 0:
+        raise RuntimeError(f"oracle_spectral_sample failed: {abi.STATUS_NAMES.get(st, st)}")
+    keys = ("mus", "mua", "hgg", "g2", "n", "kappa", "albedo", "wavelength")
+    return dict(zip(keys, out.tolist())), d.value
 
 
 def spectrum_sample(source, n, seed=123456789, first=0):

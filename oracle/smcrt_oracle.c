@@ -17,6 +17,8 @@
  *   emitters              src/photon.f90:159-1043 (every source: point, uniform, pencil,
  *                         circular, focus, annulus, dslit, aperture, slm, ...)
  *   source spectra        src/piecewise.f90 (constant, 1-D and 2-D piecewise)
+ *   spectral optical props src/opticalProps/opticalProperties.f90:127-201 (init_spectral,
+ *                         updateSpectral; oracle_spectral_sample below)
  *   scatter               src/photon.f90:1045-1103
  *   detectors             src/detectors/detector_base.f90:137-235, detectors.f90:147-469,
  *                         src/geometryMod.f90:217-270 (circle, annulus, camera, fibre)
@@ -1493,7 +1495,8 @@ static int build_scene(scene_t* S, const smcrt_sdf_node* nodes, int32_t n_nodes,
   for (int32_t i = 0; i < n_top; ++i) {                              /* init_mono :107-125 */
     const smcrt_sdf_node* nd = &nodes[top[i]];
     S->kappa[i] = nd->mus + nd->mua;
-    S->albedo[i] = (nd->mua < 1e-9) ? 1.0 : nd->mus / S->kappa[i];
+    if (nd->flags & SMCRT_NODE_ALBEDO_UNGUARDED) S->albedo[i] = nd->mus / S->kappa[i];  /* updateSpectral :198-199 */
+    else S->albedo[i] = (nd->mua < 1e-9) ? 1.0 : nd->mus / S->kappa[i];
     S->mua[i] = nd->mua; S->hgg[i] = nd->hgg; S->g2[i] = nd->hgg * nd->hgg; S->nidx[i] = nd->n;
   }
   S->xface = calloc((size_t)grid->nx + 1 + grid->ny + 1 + grid->nz + 2, sizeof(double));
@@ -1657,5 +1660,85 @@ ORACLE_API int oracle_spectrum_sample(const smcrt_source* src, uint64_t seed, ui
     if (draws) draws[j] = rng.draws;
   }
   free_plan(&plan);
+  return SMCRT_OK;
+}
+
+/* ===================================================== spectral optical properties ===== */
+/* The `spectral` type (opticalProperties.f90:127-201) over five piecewise1D tables.
+ * Its ran2 draws come from the host stream family 2: draw d is the (d & 1) half of Philox block
+ * (d >> 1, 2, 0, 0xFFFFFFFF) under (seed_lo, seed_hi) (the library's smcrt_spectral_sample
+ * documents the same stream). mode 0: init_spectral as documented (properties at the sampled
+ * wavelength, albedo guarded); 1: updateSpectral (albedo unguarded); 2: init_spectral as
+ * compiled (sample(x, y) without a value: each property is an x-axis draw of its own table).
+ * out[8] = mus, mua, hgg, g2, n, kappa, albedo, wavelength. */
+static double spectral_ran2(uint64_t seed, uint64_t* d) {
+  uint32_t ctr[4] = {(uint32_t)(*d >> 1), 2u, 0u, 0xFFFFFFFFu};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t o[4];
+  oracle_philox4x32_10(ctr, key, o);
+  uint64_t u = (*d & 1u) ? (((uint64_t)o[3] << 32) | o[2]) : (((uint64_t)o[1] << 32) | o[0]);
+  *d += 1;
+  return (double)(u >> 11) * 0x1.0p-53;
+}
+
+/* init_piecewise1D (piecewise.f90:142-168): cdf(1) = 0, cdf(i) = sum_{k=2..i} w(k) y(k) with
+ * stdlib's trapz_weights, then res%cdf = res%cdf / res%cdf(length) */
+static double* pw1d_cdf(const double* a, int64_t n) {
+  const double* x = a;
+  const double* y = a + n;
+  double* cdf = calloc((size_t)n, sizeof(double));
+  double sumer = 0.0;
+  for (int64_t i = 1; i < n; ++i) {
+    double w = (n == 2 || i == n - 1) ? 0.5 * (x[n - 1] - x[n - 2]) : 0.5 * (x[i + 1] - x[i - 1]);
+    sumer = sumer + w * y[i];
+    cdf[i] = sumer;
+  }
+  double last = cdf[n - 1];
+  for (int64_t i = 0; i < n; ++i) cdf[i] = cdf[i] / last;
+  return cdf;
+}
+
+/* sample1D without value (:124-131) */
+static double pw1d_draw(const double* a, int64_t n, uint64_t seed, uint64_t* d) {
+  double* cdf = pw1d_cdf(a, n);
+  double val = spectral_ran2(seed, d);
+  int64_t idx = search_1d(cdf, n, val);
+  double x = a[idx - 1] + ((val - cdf[idx - 1]) * (a[idx] - a[idx - 1])) / (cdf[idx] - cdf[idx - 1]);
+  free(cdf);
+  return x;
+}
+
+/* sample1D with value (:132-137); search_2D (:288-312) bisects the first column */
+static double pw1d_at(const double* a, int64_t n, double value) {
+  int64_t idx = search_1d(a, n, value);
+  const double* y = a + n;
+  return y[idx - 1] + (y[idx] - y[idx - 1]) * ((value - a[idx - 1]) / (a[idx] - a[idx - 1]));
+}
+
+ORACLE_API int oracle_spectral_sample(const smcrt_spectral* sp, int32_t mode, uint64_t seed, uint64_t* draw,
+                                      double out[8]) {
+  if (!sp || !draw || !out || mode < 0 || mode > 2) return SMCRT_ERR_INVALID_ARG;
+  if (!sp->mus || !sp->mua || !sp->hgg || !sp->n || !sp->flux) return SMCRT_ERR_INVALID_ARG;
+  if (sp->n_mus < 2 || sp->n_mua < 2 || sp->n_hgg < 2 || sp->n_n < 2 || sp->n_flux < 2) return SMCRT_ERR_INVALID_ARG;
+  uint64_t d = *draw;
+  double wave = pw1d_draw(sp->flux, sp->n_flux, seed, &d);          /* flux%sample(wave, tmp) */
+  double mus, mua, hgg, n;
+  if (mode == 2) {                                                   /* :144-148 as compiled */
+    mus = pw1d_draw(sp->mus, sp->n_mus, seed, &d);
+    mua = pw1d_draw(sp->mua, sp->n_mua, seed, &d);
+    hgg = pw1d_draw(sp->hgg, sp->n_hgg, seed, &d);
+    n = pw1d_draw(sp->n, sp->n_n, seed, &d);
+  } else {                                                           /* :184-195 */
+    mus = pw1d_at(sp->mus, sp->n_mus, wave);
+    mua = pw1d_at(sp->mua, sp->n_mua, wave);
+    hgg = pw1d_at(sp->hgg, sp->n_hgg, wave);
+    n = pw1d_at(sp->n, sp->n_n, wave);
+  }
+  double kappa = mus + mua, albedo;
+  if (mode == 1) albedo = mus / kappa;                               /* :198-199 */
+  else albedo = (mua < 1e-9) ? 1.0 : mus / kappa;                    /* :150-155 */
+  out[0] = mus; out[1] = mua; out[2] = hgg; out[3] = hgg * hgg; out[4] = n;
+  out[5] = kappa; out[6] = albedo; out[7] = wave;
+  *draw = d;
   return SMCRT_OK;
 }

@@ -5,7 +5,7 @@ against the library's own view of them.
 """
 import ctypes as C
 
-SMCRT_ABI_VERSION = 4
+SMCRT_ABI_VERSION = 5
 
 # smcrt_status
 OK = 0
@@ -76,10 +76,32 @@ ENGINE_COUNTERS = ("wave_iters",)
 class SdfNode(C.Structure):
     _fields_ = [
         ("kind", C.c_int32), ("layer", C.c_int32), ("op", C.c_int32),
-        ("first_child", C.c_int32), ("n_children", C.c_int32), ("reserved", C.c_int32 * 3),
+        ("first_child", C.c_int32), ("n_children", C.c_int32), ("flags", C.c_int32), ("reserved", C.c_int32 * 2),
         ("transform", C.c_double * 16), ("param", C.c_double * 12), ("k", C.c_double),
         ("mus", C.c_double), ("mua", C.c_double), ("hgg", C.c_double), ("n", C.c_double),
     ]
+
+
+# smcrt_sdf_node.flags (ABI 5)
+NODE_ALBEDO_UNGUARDED = 1
+
+# smcrt_spectral_mode (ABI 5)
+SPECTRAL_INIT = 0
+SPECTRAL_UPDATE = 1
+SPECTRAL_INIT_AS_WRITTEN = 2
+
+
+class Spectral(C.Structure):
+    """smcrt_spectral: five piecewise1D tables, each a Fortran array(n, 2)."""
+    _fields_ = [("n_mus", C.c_int64), ("n_mua", C.c_int64), ("n_hgg", C.c_int64), ("n_n", C.c_int64),
+                ("n_flux", C.c_int64), ("mus", C.POINTER(C.c_double)), ("mua", C.POINTER(C.c_double)),
+                ("hgg", C.POINTER(C.c_double)), ("n", C.POINTER(C.c_double)), ("flux", C.POINTER(C.c_double))]
+
+
+class OptProps(C.Structure):
+    _fields_ = [("mus", C.c_double), ("mua", C.c_double), ("hgg", C.c_double), ("g2", C.c_double),
+                ("n", C.c_double), ("kappa", C.c_double), ("albedo", C.c_double), ("wavelength", C.c_double),
+                ("node_flags", C.c_int32), ("reserved", C.c_int32)]
 
 
 class Grid(C.Structure):
@@ -214,4 +236,5 @@ EXPORTED_SYMBOLS = [
     "smcrt_comm_info", "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_multi_create", "smcrt_multi_info",
     "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_accumulate", "smcrt_multi_collect",
     "smcrt_multi_device_photons", "smcrt_multi_destroy", "smcrt_job_run_devices",
+    "smcrt_spectral_sample", "smcrt_scene_set_spectral",
 ]

@@ -2,11 +2,12 @@
 
 Plain hipcc, no torch extension machinery: every source compiles to an object in parallel and
 one link makes the C-ABI shared object (include/smcrt.h) that Fortran/C/Python can bind.
-Objects are kept in rsmcrt_amd/.objs/ (git-ignored) and rebuilt only when their source or a
-header it includes (found by scanning `#include "..."` lines) is newer.
+Objects are kept in rsmcrt_amd/.objs/<arch>-<flags hash>/ (git-ignored) and rebuilt only when
+their source or a header it includes (found by scanning `#include "..."` lines) is newer.
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import re
 import shutil
@@ -18,8 +19,7 @@ from concurrent.futures import ThreadPoolExecutor
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libsmcrt.so")
-OBJDIR = os.path.join(PKG, ".objs")
-SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp", "multi.hip", "cull.cpp")]
+SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp", "spectral.cpp", "multi.hip", "cull.cpp")]
 # the transport kernel instantiations: kinst.hip once per (LDS faces, grid mode), kernel_ptrs.h
 KINST = os.path.join(PKG, "csrc", "kinst.hip")
 UNITS = [(src, ()) for src in SOURCES] + [(KINST, (f"-DKI_F={f}", f"-DKI_G={g}")) for f in (0, 1) for g in (0, 1, 2)]
@@ -29,6 +29,8 @@ ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
 # CPU restatement (oracle/), which is compiled the same way.
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
          f"--offload-arch={ARCH}", "-Wall"]
+# objects are cached per target and flag set, so a change of either never links stale objects
+OBJDIR = os.path.join(PKG, ".objs", ARCH + "-" + hashlib.sha256(" ".join(FLAGS).encode()).hexdigest()[:12])
 _INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
 
 
@@ -73,9 +75,8 @@ def up_to_date() -> bool:
 
 def _compile_and_link(out: str, extra=(), variant: str = "", force: bool = False, verbose: bool = False) -> str:
     os.makedirs(OBJDIR, exist_ok=True)
-    # a variant's flags reach the HIP units (kernels and their host side); the host-only C++
-    # units are the base build's objects
-    var = [bool(variant) and src.endswith(".hip") for src, _ in UNITS]
+    # a variant's flags reach every unit (its objects are tagged with the variant's name)
+    var = [bool(variant) for _ in UNITS]
     objs = [_obj(src, defs, variant if var[i] else "") for i, (src, defs) in enumerate(UNITS)]
     todo = [i for i, (src, _) in enumerate(UNITS) if (force and (var[i] or not variant)) or _stale(objs[i], includes(src))]
 

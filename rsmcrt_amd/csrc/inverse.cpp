@@ -12,38 +12,13 @@
 
 #include "../../include/smcrt.h"
 #include "hosterr.h"
+#include "hostrng.h"
 #include "scene_internal.h"
 
 using smcrt::set_error;
 
-namespace {
-
-// Philox4x32-10 (Salmon et al. 2011), the counter-based generator of the transport kernel
-// (detmath.h), here on the host.
-void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
-  for (int r = 0; r < 10; ++r) {
-    if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c[1] ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c[3] ^ k1;
-    c[1] = (uint32_t)p1; c[3] = (uint32_t)p0; c[0] = n0; c[2] = n2;
-  }
-}
-
 // The guess stream: draw d is the (d & 1) half of block (d >> 1, 1, 0, 0xFFFFFFFF) under
-// the run's key, a counter no photon stream uses (photon counters have word 1 = 0).
-struct GuessRng {
-  uint32_t k0, k1;
-  uint64_t d = 0;
-  double next() {
-    uint32_t c[4] = {(uint32_t)(d >> 1), 1u, 0u, 0xFFFFFFFFu};
-    philox(c, k0, k1);
-    const uint64_t u = (d & 1) ? (((uint64_t)c[3] << 32) | c[2]) : (((uint64_t)c[1] << 32) | c[0]);
-    ++d;
-    return (double)(u >> 11) * 0x1.0p-53;
-  }
-};
-
-}  // namespace
+// the run's key (hostrng.h), a counter no photon stream uses.
 
 extern "C" {
 
@@ -71,12 +46,14 @@ int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_i
   }
   if (idx < 0)  // :1581-1584
     return set_error(SMCRT_ERR_INVALID_ARG, "Selected layer not found in SDF array please choose a layer inside the SDF array");
-  double orig[4];  // the node's stored values, restored at the end
+  double orig[4];  // the node's stored values and flags, restored at the end
+  int32_t orig_flags = 0;
   if ((st = smcrt::scene_node_optprops(scene, idx, orig))) return st;
+  if ((st = smcrt::scene_node_flags(scene, idx, &orig_flags))) return st;
 
   // AdaLIPO bounds, :1588-1602
   const double musl = 0.0, musu = 100.0, mual = 0.0, muau = 100.0, gl = -1.0, gu = 1.0, nl = 1.0, nu = 20.0;
-  GuessRng R{(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32)};
+  smcrt::HostStream R{(uint32_t)cfg->seed, (uint32_t)(cfg->seed >> 32), smcrt::STREAM_INVERSE};
   const int64_t M = cfg->max_steps;
   const bool apply = cfg->flags & SMCRT_INVERSE_APPLY_TRIAL;
   std::vector<double> bins;
@@ -156,7 +133,7 @@ int smcrt_inverse_run(smcrt_scene* scene, const smcrt_source* src, const smcrt_i
     memo.push_back(m);
   }
   if (changed) {  // restore the layer
-    const int rst = smcrt_scene_set_optprops(scene, idx, orig[0], orig[1], orig[2], orig[3]);
+    const int rst = smcrt::scene_set_node_props(scene, idx, orig[0], orig[1], orig[2], orig[3], orig_flags);
     if (!st) st = rst;
   }
   return st;

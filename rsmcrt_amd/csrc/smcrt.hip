@@ -270,7 +270,8 @@ static uint32_t dep_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_
 static TopProps make_props(const smcrt_sdf_node& nd) {
   TopProps p;  // init_mono, opticalProperties.f90:107-125
   p.kappa = nd.mus + nd.mua;
-  p.albedo = (nd.mua < 1e-9) ? 1.0 : nd.mus / p.kappa;
+  if (nd.flags & SMCRT_NODE_ALBEDO_UNGUARDED) p.albedo = nd.mus / p.kappa;  // updateSpectral :198-199
+  else p.albedo = (nd.mua < 1e-9) ? 1.0 : nd.mus / p.kappa;
   p.hgg = nd.hgg;
   p.n = nd.n;
   return p;
@@ -707,15 +708,7 @@ int smcrt_scene_det_bins(const smcrt_scene* s, int64_t* n) {
 }
 
 int smcrt_scene_set_optprops(smcrt_scene* s, int32_t i, double mus, double mua, double hgg, double n) {
-  if (!s || i < 0 || i >= s->n_top) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or index");
-  std::lock_guard<std::mutex> g(s->mu);
-  smcrt_sdf_node& nd = s->h_nodes[s->h_top[i]];
-  nd.mus = mus; nd.mua = mua; nd.hgg = hgg; nd.n = n;
-  s->h_props[i] = make_props(nd);
-  HIPCHK(hipSetDevice(s->device));
-  HIPCHK(hipMemcpyAsync(s->d_props + i, &s->h_props[i], sizeof(TopProps), hipMemcpyHostToDevice, s->stream));
-  HIPCHK(hipStreamSynchronize(s->stream));
-  return SMCRT_OK;
+  return smcrt::scene_set_node_props(s, i, mus, mua, hgg, n, 0);  // a mono: init_mono's rules
 }
 
 int smcrt_scene_get_optprops(const smcrt_scene* s, int32_t i, int32_t* layer, double* mus, double* mua, double* hgg,
@@ -736,6 +729,26 @@ int smcrt::scene_node_optprops(const smcrt_scene* s, int32_t i, double out[4]) {
   if (!s || i < 0 || i >= s->n_top) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or index");
   const smcrt_sdf_node& nd = s->h_nodes[s->h_top[i]];
   out[0] = nd.mus; out[1] = nd.mua; out[2] = nd.hgg; out[3] = nd.n;
+  return SMCRT_OK;
+}
+
+int smcrt::scene_set_node_props(smcrt_scene* s, int32_t i, double mus, double mua, double hgg, double n,
+                                int32_t flags) {
+  if (!s || i < 0 || i >= s->n_top) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or index");
+  std::lock_guard<std::mutex> g(s->mu);
+  smcrt_sdf_node& nd = s->h_nodes[s->h_top[i]];
+  nd.mus = mus; nd.mua = mua; nd.hgg = hgg; nd.n = n;
+  nd.flags = flags;
+  s->h_props[i] = make_props(nd);
+  HIPCHK(hipSetDevice(s->device));
+  HIPCHK(hipMemcpyAsync(s->d_props + i, &s->h_props[i], sizeof(TopProps), hipMemcpyHostToDevice, s->stream));
+  HIPCHK(hipStreamSynchronize(s->stream));
+  return SMCRT_OK;
+}
+
+int smcrt::scene_node_flags(const smcrt_scene* s, int32_t i, int32_t* flags) {
+  if (!s || i < 0 || i >= s->n_top) return fail(SMCRT_ERR_INVALID_ARG, "bad scene or index");
+  *flags = s->h_nodes[s->h_top[i]].flags;
   return SMCRT_OK;
 }
 

@@ -50,6 +50,20 @@ uint32_t pack_bits(uint64_t z) {
 
 }  // namespace
 
+void piecewise1d_cdf(const double* array, int64_t n, std::vector<double>& cdf) {
+  const double* x = array;
+  const double* y = array + n;
+  const std::vector<double> w = trapz_weights(x, n);
+  cdf.assign((size_t)n, 0.0);
+  double sumer = 0.0;
+  for (int64_t i = 1; i < n; ++i) {  // do i = 2, length (the first weight is never used)
+    sumer = sumer + w[i] * y[i];
+    cdf[i] = sumer;
+  }
+  const double last = cdf[n - 1];  // res%cdf = res%cdf / res%cdf(length): the old last element
+  for (int64_t i = 0; i < n; ++i) cdf[i] = cdf[i] / last;
+}
+
 int build_src_plan(const smcrt_source* s, const smcrt_grid* g, SrcPlan* p, std::vector<double>& x,
                    std::vector<double>& y, std::vector<double>& cdf, const char** err) {
   std::memset(p, 0, sizeof *p);
@@ -128,15 +142,7 @@ int build_src_plan(const smcrt_source* s, const smcrt_grid* g, SrcPlan* p, std::
       }
       x.assign(sp->array, sp->array + n);
       y.assign(sp->array + n, sp->array + 2 * n);
-      const std::vector<double> w = trapz_weights(x.data(), n);
-      cdf.assign((size_t)n, 0.0);
-      double sumer = 0.0;
-      for (int64_t i = 1; i < n; ++i) {  // do i = 2, length (the first weight is never used)
-        sumer = sumer + w[i] * y[i];
-        cdf[i] = sumer;
-      }
-      const double last = cdf[n - 1];
-      for (int64_t i = 0; i < n; ++i) cdf[i] = cdf[i] / last;
+      piecewise1d_cdf(sp->array, n, cdf);
       p->spec_n = n;
     } else if (sp->kind == SMCRT_SPEC_2D) {  // init_piecewise2D, piecewise.f90:190-236
       const int32_t width = sp->width, height = sp->height;

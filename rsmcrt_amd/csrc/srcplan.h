@@ -47,6 +47,10 @@ struct SrcPlan {
 int build_src_plan(const smcrt_source* src, const smcrt_grid* g, SrcPlan* p, std::vector<double>& x,
                    std::vector<double>& y, std::vector<double>& cdf, const char** err);
 
+// init_piecewise1D's CDF (piecewise.f90:142-168) of a Fortran array(n, 2) (x = array[0, n),
+// y = array[n, 2n)): trapezoid weights, cdf(1) = 0, normalised by the last element. n >= 2.
+void piecewise1d_cdf(const double* array, int64_t n, std::vector<double>& cdf);
+
 // true when the run needs the general emitter (anything but point/uniform/pencil with a
 // constant spectrum)
 inline bool src_needs_plan(const smcrt_source* s) {  // (batched origins always do)

@@ -146,6 +146,18 @@ class Engine:
     def __exit__(self, *exc):
         self.close()
 
+    def set_spectral(self, top_index: int, sp, mode: int = abi.SPECTRAL_UPDATE) -> float:
+        """Re-sample spectral layer `sp` (rsmcrt_amd.spectral.Spectral; updateSpectral by
+        default) into top-level SDF `top_index` (smcrt_scene_set_spectral); returns the
+        wavelength. sp's stream position and current values advance with it."""
+        from .spectral import _lib
+        d = C.c_uint64(sp.draw)
+        out = abi.OptProps()
+        _check(_lib().smcrt_scene_set_spectral(self._h, top_index, C.byref(sp.struct()), int(mode), sp.seed,
+                                               C.byref(d), C.byref(out)))
+        sp.draw, sp.props = d.value, out
+        return out.wavelength
+
     def set_optprops(self, top_index: int, mus, mua, hgg, n):
         _check(load_library().smcrt_scene_set_optprops(self._h, top_index, mus, mua, hgg, n))
 

@@ -115,11 +115,14 @@ def _colmajor(m) -> List[float]:
 # ------------------------------------------------------------ optical props ----
 @dataclass(frozen=True)
 class Mono:
-    """mono optical properties (opticalProperties.f90:107-125)."""
+    """mono optical properties (opticalProperties.f90:107-125). flags (smcrt_sdf_node.flags):
+    abi.NODE_ALBEDO_UNGUARDED for properties that came from updateSpectral (:198-199), whose
+    albedo has no mua < 1e-9 guard (rsmcrt_amd.spectral)."""
     mus: float
     mua: float
     hgg: float
     n: float
+    flags: int = 0
 
     @property
     def kappa(self) -> float:
@@ -127,11 +130,20 @@ class Mono:
 
     @property
     def albedo(self) -> float:
+        if self.flags & abi.NODE_ALBEDO_UNGUARDED:
+            return self.mus / self.kappa
         return 1.0 if self.mua < 1e-9 else self.mus / self.kappa
 
 
 def mono(mus, mua, hgg, n) -> Mono:
     return Mono(float(mus), float(mua), float(hgg), float(n))
+
+
+def _set_opt(nd: abi.SdfNode, o) -> None:
+    """A node's optical properties from a Mono (or anything with mus/mua/hgg/n, e.g. a
+    rsmcrt_amd.spectral.Spectral's current values) and its derivation flags."""
+    nd.mus, nd.mua, nd.hgg, nd.n = float(o.mus), float(o.mua), float(o.hgg), float(o.n)
+    nd.flags = int(getattr(o, "flags", 0))
 
 
 # ------------------------------------------------------------------ SDFs ----------
@@ -152,7 +164,7 @@ class SDF:
             nd.transform[i] = v
         for i, v in enumerate(self.param):
             nd.param[i] = float(v)
-        nd.mus, nd.mua, nd.hgg, nd.n = self.opt.mus, self.opt.mua, self.opt.hgg, self.opt.n
+        _set_opt(nd, self.opt)
         return nd
 
 
@@ -294,8 +306,7 @@ class Scene:
                     nd.transform[i] = v
                 for i, v in enumerate(s.param):
                     nd.param[i] = float(v)
-                o = s.opt
-                nd.mus, nd.mua, nd.hgg, nd.n = o.mus, o.mua, o.hgg, o.n
+                _set_opt(nd, s.opt)
                 nd.first_child = len(nodes)
                 nd.n_children = 1
                 nodes.append(None)
@@ -309,8 +320,7 @@ class Scene:
                 nd.k = s.k
                 for i, v in enumerate(_colmajor(identity())):
                     nd.transform[i] = v
-                o = s.opt
-                nd.mus, nd.mua, nd.hgg, nd.n = o.mus, o.mua, o.hgg, o.n
+                _set_opt(nd, s.opt)
                 nd.first_child = len(nodes)
                 nd.n_children = len(s.children)
                 first = len(nodes)

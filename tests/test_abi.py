@@ -35,9 +35,12 @@ def test_exports(lib_path):
 
 def test_abi_version_matches_header():
     """The header, the ctypes mirror and the Fortran module agree on the version; version 4 is
-    the 56-byte smcrt_kernel_times (lean_hazards)."""
+    the 56-byte smcrt_kernel_times (lean_hazards), version 5 the node flags and the spectral
+    optical properties."""
     txt = open(HEADER).read()
-    assert int(re.search(r"#define SMCRT_ABI_VERSION (\d+)", txt).group(1)) == abi.SMCRT_ABI_VERSION == 4
+    assert int(re.search(r"#define SMCRT_ABI_VERSION (\d+)", txt).group(1)) == abi.SMCRT_ABI_VERSION == 5
+    f90 = open(os.path.join(ROOT, "bindings", "fortran", "smcrt_mod.f90")).read()
+    assert int(re.search(r"SMCRT_MOD_ABI_VERSION = (\d+)", f90).group(1)) == abi.SMCRT_ABI_VERSION
     assert C.sizeof(abi.KernelTimes) == 56
 
 
@@ -60,7 +63,10 @@ def test_errors_without_compute(lib_path):
 
 
 STRUCTS = {
-    "smcrt_sdf_node": (abi.SdfNode, ["kind", "op", "transform", "param", "k", "mus", "n"]),
+    "smcrt_sdf_node": (abi.SdfNode, ["kind", "op", "n_children", "flags", "reserved", "transform", "param", "k",
+                                     "mus", "n"]),
+    "smcrt_spectral": (abi.Spectral, ["n_mus", "n_flux", "mus", "mua", "hgg", "n", "flux"]),
+    "smcrt_optprops": (abi.OptProps, ["mus", "g2", "albedo", "wavelength", "node_flags"]),
     "smcrt_grid": (abi.Grid, ["nx", "nz", "xmax", "zmax"]),
     "smcrt_source": (abi.Source, ["kind", "pos", "dir", "p1", "p3", "beam", "radius", "sigma", "rotation",
                                   "spectrum"]),

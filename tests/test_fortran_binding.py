@@ -23,7 +23,7 @@ TYPES = {"smcrt_sdf_node": abi.SdfNode, "smcrt_grid": abi.Grid, "smcrt_source": 
          "smcrt_detector": abi.Detector, "smcrt_run_config": abi.RunConfig, "smcrt_tallies": abi.Tallies,
          "smcrt_device_tallies": abi.DeviceTallies, "smcrt_kernel_times": abi.KernelTimes,
          "smcrt_escape_config": abi.EscapeConfig, "smcrt_inverse_config": abi.InverseConfig,
-         "smcrt_pack_layout": abi.PackLayout}
+         "smcrt_pack_layout": abi.PackLayout, "smcrt_spectral": abi.Spectral, "smcrt_optprops": abi.OptProps}
 
 
 def _build_module(tmp):
@@ -187,3 +187,27 @@ def test_glue_tables_match_the_toml_front_end(lib_path, tmp_path):
         for k in SRC_FIELDS:
             want = getattr(d.source, k)
             assert src[k] == (list(want) if hasattr(want, "__len__") else [want]), (name, "source", k)
+
+
+def test_fortran_spectral_unit_test(lib_path, tmp_path):
+    """test_opticalprops.f90:81-142 written against the binding (bindings/fortran/
+    example_spectral.f90: the reference's tables with their default-real literals, spectral()
+    then 10^4 updates in the test's bounds); its first 100 samples equal the restatement's."""
+    import numpy as np
+    from oracle import pyoracle as O
+    from test_opticalprops import reference_tables
+    for f in ("smcrt_mod.f90", "smcrt_glue.f90", "example_spectral.f90"):
+        shutil.copy(os.path.join(FDIR, f), tmp_path)
+    libdir = os.path.dirname(lib_path)
+    subprocess.run([FC, "-O2", "-c", "smcrt_mod.f90"], cwd=tmp_path, check=True)
+    subprocess.run([FC, "-O2", "-c", "smcrt_glue.f90"], cwd=tmp_path, check=True)
+    subprocess.run([FC, "-O2", "-o", "example_spectral", "example_spectral.f90", "smcrt_glue.o", "smcrt_mod.o",
+                    f"-L{libdir}", "-lsmcrt", f"-Wl,-rpath,{libdir}"], cwd=tmp_path, check=True)
+    r = subprocess.run([str(tmp_path / "example_spectral"), str(tmp_path / "s.bin")], capture_output=True, text=True)
+    assert r.returncode == 0 and "spectral OK" in r.stdout, r.stdout + r.stderr
+    got = np.fromfile(tmp_path / "s.bin", dtype=np.float64).reshape(100, 5)
+    tabs = reference_tables()
+    _, d = O.spectral_sample(tabs, abi.SPECTRAL_INIT, 1234569, 0)
+    for i in range(100):
+        ref, d = O.spectral_sample(tabs, abi.SPECTRAL_UPDATE, 1234569, d)
+        assert list(got[i]) == [ref["wavelength"], ref["mus"], ref["mua"], ref["hgg"], ref["n"]], i

@@ -3,7 +3,7 @@
 
   test/photon/test_photon.f90           Uniform/Pencil/Point/Circular/SLM sources
   test/optical_props/test_piecewise.f90 piecewise1D (blood.dat) and piecewise2D sampling
-  test/optical_props/test_opticalprops.f90  spectral optical properties
+  (test/optical_props/test_opticalprops.f90, spectral optical properties: tests/test_opticalprops.py)
 plus geometric properties of the emitters the reference has no test for (focus, annulus,
 dslit, aperture) and the exact RNG draw count of every emitter. CPU only.
 """
