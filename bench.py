@@ -617,6 +617,7 @@ def main():
         dist.all_gather(per_rank, mine)
     per_rank_s = [float(x.item()) for x in per_rank]
     elapsed = max(per_rank_s)  # the max over ranks
+    eng.check()  # (after the timed region) the watchdog of every timed launch: a fault fails the line
     rows = None
     if world > 1:  # every rank's photons, transport time and reduce time (rank_row)
         mine_row = rank_row(rank, args.steps * B, t1 - t0, ev[0].elapsed_time(ev[1]) * 1e-3, ev[1].elapsed_time(ev[2]))

@@ -203,6 +203,11 @@ module smcrt_mod
             real(c_double), value     :: mus, mua, hgg, n
         end function smcrt_scene_set_optprops
 
+        integer(c_int) function smcrt_scene_check(scene) bind(C, name="smcrt_scene_check")
+            import :: c_int, c_ptr
+            type(c_ptr), value :: scene
+        end function smcrt_scene_check
+
         integer(c_int) function smcrt_spectral_sample(sp, mode, seed, draw, out) &
                 bind(C, name="smcrt_spectral_sample")
             import :: c_int, c_int32_t, c_int64_t, smcrt_spectral, smcrt_optprops

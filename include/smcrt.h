@@ -426,6 +426,16 @@ int smcrt_scene_classify(smcrt_scene* scene, const double* points, int64_t n, in
  * next launch's transport kernel (two record-log slots). */
 int smcrt_scene_fence(smcrt_scene* scene, void* stream);
 
+/* ABI 5: wait for every launch and fold of the scene (smcrt_run_device's asynchronous work) and
+ * report the watchdog. Every cross-wave wait inside the kernels (a photon lane waiting for its
+ * event, synchronous segment or slot; a producer waiting for a ring or event-queue word; a
+ * deposit waiting for a bucket claim) is bounded by SMCRT_WATCHDOG_MS of wall clock (default
+ * 2000; 0 = unbounded). A wait past it -- a lost wake-up, which would otherwise hang the GPU --
+ * makes its block leave its loops and the grid drain; this call (and smcrt_run, which checks by
+ * itself) then returns SMCRT_ERR_DEVICE_FAULT with the wait site and block in
+ * smcrt_last_error(). The tallies of such a run are incomplete. */
+int smcrt_scene_check(smcrt_scene* scene);
+
 /* Per-kernel device time (ms) of the launches made since the previous query, from HIP
  * events recorded on the launch stream around each kernel group while timing is enabled
  * (off by default; no reference counterpart: it is the measurement hook of bench.py).

@@ -236,5 +236,5 @@ EXPORTED_SYMBOLS = [
     "smcrt_comm_info", "smcrt_comm_destroy", "smcrt_reduce_device_tallies", "smcrt_multi_create", "smcrt_multi_info",
     "smcrt_multi_scene", "smcrt_multi_run", "smcrt_multi_accumulate", "smcrt_multi_collect",
     "smcrt_multi_device_photons", "smcrt_multi_destroy", "smcrt_job_run_devices",
-    "smcrt_spectral_sample", "smcrt_scene_set_spectral",
+    "smcrt_spectral_sample", "smcrt_scene_set_spectral", "smcrt_scene_check",
 ]

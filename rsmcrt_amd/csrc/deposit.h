@@ -511,14 +511,18 @@ __device__ __forceinline__ void emit_bucketed(const KParams& K, const KCold* __r
     if (!__ballot(claim || spill || wait)) return;
     bucket_slow(K, C, W, claim, spill, w, t, vox, val, overflow, bs);
     if (!__ballot(wait)) return;
+    bool expired = false;
     if (wait) {  // until the pending claim has rebased the word (see the bound above)
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       unsigned long long x;
       do {
         __builtin_amdgcn_s_sleep(2);
         x = __hip_atomic_load(bs + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // (the watchdog: a claim that never lands drops this record and fails the run)
+        if (watchdog_expired(C, t0, WDOG_BUCKET)) { expired = true; break; }
       } while (bw_fill(x) >= 2 * BUCKET_RECORDS && bw_cur(x) == bw_cur(w));
     }
-    todo = wait;
+    todo = wait && !expired;
   }
 }
 

@@ -516,6 +516,10 @@ static int collect_locked(smcrt_multi* m, smcrt_tallies* io) {
       return fail(SMCRT_ERR_DEVICE_FAULT, std::string("device ") + std::to_string(m->devices[g]) + ": " +
                                               hipGetErrorString(e));
   }
+  for (size_t g = 0; g < n; ++g) {  // the watchdog of every device's launches (smcrt_scene_check)
+    const int ws = smcrt_scene_check(m->scenes[g]);
+    if (ws) return ws;
+  }
   std::vector<double> h((size_t)o.total);
   HIPCHK(hipSetDevice(m->devices[0]));
   HIPCHK(hipMemcpy(h.data(), m->d_buf[0], sizeof(double) * h.size(), hipMemcpyDeviceToHost));

@@ -267,6 +267,31 @@ static size_t transport_lds(const smcrt_scene* s, uint32_t dep_words, bool xsrc)
 // 64-bit bucket word per tile shared by the block.
 static uint32_t dep_words(const smcrt_scene* s) { return s->bucketed ? 2 * s->n_tiles : 4 * s->hist_tiles; }
 
+// ---- the watchdog (transport.h watchdog_expired): d_queue[MAX_SLOTS + 4] holds the first
+// expired wait of the scene's launches, site | (block + 1) << 8
+constexpr double DEFAULT_WATCHDOG_MS = 2000.0;  // a wait past 2 s of wall clock is a lost wake-up
+static uint32_t* watchdog_word(smcrt_scene* s) { return (uint32_t*)(s->d_queue + MAX_SLOTS + 4); }
+static const char* watchdog_site(uint32_t site) {
+  switch (site) {
+    case WDOG_PHOTON_WAVE: return "ws_kernel photon wave (every live lane waited for an event, a segment or a slot)";
+    case WDOG_RING: return "ws_kernel ring producer (the token word's previous lap was never consumed)";
+    case WDOG_EVENT_QUEUE: return "ws_kernel event-queue producer (the entry's previous lap was never consumed)";
+    case WDOG_BUCKET: return "bucket wait (deposit.h: the pending claim never rebased the tile word)";
+    default: return "unknown site";
+  }
+}
+// After the scene's launches have finished: SMCRT_ERR_DEVICE_FAULT naming the first expired
+// wait, if any (the word is cleared, so the scene stays usable).
+static int take_watchdog(smcrt_scene* s) {
+  uint32_t w = 0;
+  HIPCHK(hipMemcpy(&w, watchdog_word(s), sizeof w, hipMemcpyDeviceToHost));
+  if (!w) return SMCRT_OK;
+  HIPCHK(hipMemset(watchdog_word(s), 0, sizeof w));
+  return fail(SMCRT_ERR_DEVICE_FAULT, std::string("watchdog: a wait exceeded SMCRT_WATCHDOG_MS at ") +
+                                          watchdog_site(w & 0xFFu) + " in block " + std::to_string((w >> 8) - 1u) +
+                                          "; the run's tallies are incomplete");
+}
+
 static TopProps make_props(const smcrt_sdf_node& nd) {
   TopProps p;  // init_mono, opticalProperties.f90:107-125
   p.kappa = nd.mus + nd.mua;
@@ -524,13 +549,13 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if ((st = dalloc(&s->d_nodes, n_nodes)) || (st = dalloc(&s->d_prog, prog.size())) || (st = dalloc(&s->d_props, n_top)) ||
       (st = dalloc(&s->d_faces, faces.size())) || (st = dalloc(&s->d_dets, std::max(1, n_dets))) ||
-      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 4)) ||
+      (st = dalloc(&s->d_det_off, (size_t)n_dets + 1)) || (st = dalloc(&s->d_queue, MAX_SLOTS + 5)) ||
       (st = dalloc(&s->d_cold, COLD_SLOTS)) ||
       (st = dalloc(&s->d_counters, SMCRT_NCOUNTERS)) ||
       (st = dalloc(&s->d_small, (size_t)s->det_total + 1 + 24)))
     return cleanup_fail(st);
   hipError_t e = hipSuccess;
-  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 4) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(s->d_queue, 0, (MAX_SLOTS + 5) * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemcpy(s->d_nodes, nodes, sizeof(smcrt_sdf_node) * n_nodes, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(s->d_prog, prog.data(), sizeof(ProgOp) * prog.size(), hipMemcpyHostToDevice);
   if (e == hipSuccess && !ctab.empty()) {
@@ -1144,12 +1169,20 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.far_steps = s->d_queue + MAX_SLOTS + 1;
   Ch.lean_hazards = s->d_queue + MAX_SLOTS + 3;
   Ch.lane_scratch = nullptr;  // (per launch stream: launch_one)
+  Ch.watchdog = watchdog_word(s);
+  {  // every cross-wave wait is bounded (transport.h watchdog_expired); 0 ms: unbounded
+    const char* wm = std::getenv("SMCRT_WATCHDOG_MS");
+    const double ms = wm ? std::strtod(wm, nullptr) : (double)DEFAULT_WATCHDOG_MS;
+    Ch.watchdog_ticks = ms > 0.0 ? (uint64_t)(ms * (double)s->wall_khz) : 0ull;
+  }
   K.rec_pool = nullptr; K.n_chunks = 0; K.hist_tiles = 0; K.bucket_tiles = 0; K.n_buckets = 0;
   {
     const char* cd = std::getenv("SMCRT_DEBUG_CLAIM_DELAY");
     K.claim_delay = cd ? (uint32_t)std::strtoul(cd, nullptr, 10) : 0u;
   }
   K.lean_debug = s->lean_debug;
+  if (const char* de = std::getenv("SMCRT_DEBUG_DROP_EVENT"))  // (tests only: the watchdog's proof)
+    if (de[0] == '1') K.lean_debug |= 4u;
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles
@@ -1280,6 +1313,7 @@ static int run_sync(smcrt_scene* s, const smcrt_source* src, const smcrt_run_con
   if (st) return st;
   hipError_t e = hipStreamSynchronize(s->stream);
   if (e != hipSuccess) return fail(SMCRT_ERR_DEVICE_FAULT, std::string("transport kernel: ") + hipGetErrorString(e));
+  if ((st = take_watchdog(s))) return st;
   // copy back and accumulate
   std::vector<double> h;
   float* gf[3] = {io->jmean, io->absorb, io->emission};
@@ -1418,6 +1452,24 @@ int smcrt_scene_fence(smcrt_scene* s, void* stream) {
   if (s->last_slot >= 0 && s->f_pending[s->last_slot])  // folds are serial: the last covers all
     HIPCHK(hipStreamWaitEvent((hipStream_t)stream, s->ev_f[s->last_slot], 0));
   return SMCRT_OK;
+}
+
+int smcrt_scene_check(smcrt_scene* s) {
+  g_last_error.clear();
+  if (!s) return fail(SMCRT_ERR_INVALID_ARG, "scene is NULL");
+  std::lock_guard<std::mutex> g(s->mu);
+  HIPCHK(hipSetDevice(s->device));
+  for (int i = 0; i < MAX_SLOTS; ++i)
+    if (s->lstream[i]) {
+      const hipError_t e = hipStreamSynchronize(s->lstream[i]);
+      if (e != hipSuccess) return fail(SMCRT_ERR_DEVICE_FAULT, std::string("transport kernel: ") + hipGetErrorString(e));
+    }
+  for (hipStream_t st : {s->stream, s->fstream})
+    if (st) {
+      const hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return fail(SMCRT_ERR_DEVICE_FAULT, std::string("transport kernel: ") + hipGetErrorString(e));
+    }
+  return take_watchdog(s);
 }
 
 int smcrt_scene_set_timing(smcrt_scene* s, int32_t enable) {

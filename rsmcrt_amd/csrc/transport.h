@@ -76,8 +76,30 @@ struct KCold {
   unsigned long long* far_steps;  // march steps taken by the far-field march (far.h), running total
   unsigned long long* lean_hazards;  // deferred lean segments ending in tflag / a fault (lean.h), running total
   double* lane_scratch;       // ws_kernel's per-photon-lane Fresnel/detector state (ws.h WX_*), or null
+  // the watchdog (round 6): every cross-wave wait of the kernels is bounded by watchdog_ticks of
+  // s_memrealtime (SMCRT_WATCHDOG_MS; 0 = unbounded); the first wait past it stores
+  // site | (block + 1) << 8 here (smcrt_scene_check / smcrt_run return SMCRT_ERR_DEVICE_FAULT
+  // naming the site) and its wave gives up the wait, so the grid drains instead of hanging
+  uint32_t* watchdog;
+  uint64_t watchdog_ticks;
   SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
+
+// watchdog sites (KCold::watchdog bits 0-7; smcrt.hip names them)
+enum : uint32_t {
+  WDOG_PHOTON_WAVE = 1,  // ws_kernel photon wave: every live lane waited (event, segment, slot)
+  WDOG_RING = 2,         // ws_kernel ring producer: its word's previous lap was never consumed
+  WDOG_EVENT_QUEUE = 3,  // ws_kernel event-queue producer: likewise
+  WDOG_BUCKET = 4        // deposit.h bucket wait: the pending claim never rebased the tile word
+};
+// true once a wait that started at t0 has run past the budget; the first such wait of the
+// launch records its site
+__device__ __forceinline__ bool watchdog_expired(const KCold* __restrict__ C, uint64_t t0, uint32_t site) {
+  const uint64_t budget = C->watchdog_ticks;
+  if (budget == 0 || __builtin_amdgcn_s_memrealtime() - t0 <= budget) return false;
+  atomicCAS(C->watchdog, 0u, site | ((blockIdx.x + 1u) << 8));
+  return true;
+}
 
 struct KParams {
   const smcrt_sdf_node* __restrict__ nodes;
@@ -109,8 +131,10 @@ struct KParams {
   // debug knob (SMCRT_DEBUG_CLAIM_DELAY, tests only): s_sleep 127 this many times before a
   // bucket claim's CAS, so that other waves fill both buckets of the tile and wait (deposit.h)
   uint32_t claim_delay;
-  // debug knob (SMCRT_DEBUG_LEAN_MARGIN, tests only): 0 = lean.h's margin; 1 = no margin;
-  // 2 = every segment that starts in the grid is deferred, so escapes become counted hazards
+  // debug knob (SMCRT_DEBUG_LEAN_MARGIN, tests only), bits 0-1: 0 = lean.h's margin; 1 = no
+  // margin; 2 = every segment that starts in the grid is deferred, so escapes become counted
+  // hazards. Bit 2 (SMCRT_DEBUG_DROP_EVENT, tests only): photon lane 0 of block 0 marks its first
+  // event queued without queueing it (the hang class the watchdog turns into a counted fault)
   uint32_t lean_debug;
   // exact SDF culling (cull.h), many-top scenes in the COOP instantiation; NULL = off
   const CullGrid* __restrict__ cull;

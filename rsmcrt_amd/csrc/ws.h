@@ -121,6 +121,7 @@ struct WsSharedT {
   uint32_t head, tail;        // ring tickets: handed to walker lanes / reserved by photon waves
   uint32_t ev_head, ev_tail;  // event tickets: held by event lanes / reserved by photon waves
   uint32_t alive;
+  uint32_t abort_;            // the watchdog fired in this block: every wave leaves its loop
 };
 // event kinds (ev_code bits 16-18; the photon's free slot in bits 19-20)
 constexpr uint32_t WS_EV_INTERACT = 1u, WS_EV_TAU = 2u, WS_EV_EMIT = 3u, WS_EV_FRESNEL = 4u;
@@ -228,6 +229,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     sh->head = sh->tail = 0;
     sh->ev_head = sh->ev_tail = 0;
     sh->alive = WS_PW;
+    sh->abort_ = 0;
   }
   __syncthreads();
 
@@ -247,10 +249,13 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     const uint32_t pl = threadIdx.x;  // photon lane (the photon waves come first)
 #define WLU(f) (sh->lu[(f)][pl])
     // lean_margin (lean.h), per axis, corner coordinates; SMCRT_DEBUG_LEAN_MARGIN (tests only)
-    const double mf = K.lean_debug ? 0.0 : 2.0 * eps;
+    const double mf = (K.lean_debug & 3u) ? 0.0 : 2.0 * eps;
     const double mx = mf * (double)(K.nx + 2), my = mf * (double)(K.ny + 2), mz = mf * (double)(K.nz + 2);
     const double ex = 2.0 * K.xmax - mx, ey = 2.0 * K.ymax - my, ez = 2.0 * K.zmax - mz;
-    const bool defer_all = K.lean_debug == 2u;
+    const bool defer_all = (K.lean_debug & 3u) == 2u;
+    // SMCRT_DEBUG_DROP_EVENT (tests only): this lane's first event is marked queued, never queued
+    bool drop_event = (K.lean_debug & 4u) && blockIdx.x == 0 && pl == 0;
+    uint64_t wait_t0 = 0;  // (the watchdog: since when every live lane of this wave has waited)
     // the lane scratch (see WX_*): field f of this lane at X[f * xs]
     const size_t xs = (size_t)gridDim.x * WS_NPL;
     double* const X = XF ? C->lane_scratch + (size_t)blockIdx.x * WS_NPL + pl : nullptr;
@@ -535,9 +540,12 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             atomicOr(&sh->busy[pl], 1u << slot);
             // the token's previous lap must have been consumed (see the header; no wait in practice)
             const uint32_t prev = t < WS_RING ? 0u : (ws_tick(t - WS_RING) | WS_CONSUMED);
+            uint64_t t0 = 0;
             while (__hip_atomic_load(&sh->meta[ix], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != prev) {
               WSDIAG(WD_PRODWAIT, 1);
               __builtin_amdgcn_s_sleep(1);
+              if (!t0) t0 = __builtin_amdgcn_s_memrealtime();
+              else if (watchdog_expired(C, t0, WDOG_RING)) break;  // (the run fails; the grid drains)
             }
             __hip_atomic_store(&sh->meta[ix], pl | (slot << 9) | (sync ? (1u << 11) : 0u) | ws_tick(t),
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -614,11 +622,15 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         // waves; a Fresnel event always goes to the event waves. Keeping them in the photon waves
         // for detector scenes too measured M5 34.3-34.9 vs 30.8-30.9 M photons/s, still short of
         // transport_kernel's 42.7-43.5, profiles/r05_ws/ab_m5_inline.txt)
-        const bool qev = free_ && !P.has(LF_EVQ) &&
-                         ((!test_kernel && ((P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT)) &&
-                                           WLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS) ||
-                                          P.st == ST_T2 || (P.st == ST_EMIT && !(ws_busy(sh, pl) & (1u << P.seq))))) ||
-                          (XF && P.st == ST_F0 && !(ws_busy(sh, pl) & (1u << P.seq))));
+        bool qev = free_ && !P.has(LF_EVQ) &&
+                   ((!test_kernel && ((P.st == ST_INTERACT && !(P.f & (LF_TFLAG | LF_FAULT)) &&
+                                     WLU(LL_INTER) + 1u <= (uint32_t)MAX_INTERACTIONS) ||
+                                    P.st == ST_T2 || (P.st == ST_EMIT && !(ws_busy(sh, pl) & (1u << P.seq))))) ||
+                    (XF && P.st == ST_F0 && !(ws_busy(sh, pl) & (1u << P.seq))));
+        if (drop_event && qev) {  // (debug knob: a missed enqueue; the photon waits for nothing)
+          drop_event = qev = false;
+          P.set(LF_EVQ);
+        }
         const uint64_t qm = __ballot(qev);
         if (qm) {
           const int first = __builtin_ctzll(qm);
@@ -629,8 +641,12 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             const uint32_t t = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
             const uint32_t ix = t & (WS_EQ - 1);
             const uint32_t prev = t < WS_EQ ? 0u : (ws_tick(t - WS_EQ) | WS_CONSUMED);
-            while (__hip_atomic_load(&sh->evq[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev)
+            uint64_t t0 = 0;
+            while (__hip_atomic_load(&sh->evq[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != prev) {
               __builtin_amdgcn_s_sleep(1);  // (never in practice: one queued event per photon)
+              if (!t0) t0 = __builtin_amdgcn_s_memrealtime();
+              else if (watchdog_expired(C, t0, WDOG_EVENT_QUEUE)) break;
+            }
             sh->ev_dir[0][pl] = P.dir.x; sh->ev_dir[1][pl] = P.dir.y; sh->ev_dir[2][pl] = P.dir.z;
             sh->ev_cached[pl] = P.rng.cached;
             sh->ev_draws[pl] = P.rng.draws;
@@ -775,6 +791,17 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                                         (P.st == ST_ABSORB && !P.has(LF_CELLS)))) == 0) {
         WSDIAG(WD_PSLEEP, 1);
         __builtin_amdgcn_s_sleep(1);  // (0, 3: within noise)
+        // the watchdog: an event, segment or slot that never comes (a lost enqueue) would hold
+        // the wave here forever; past the budget the wave fails the run and leaves, and so does
+        // every wave of the block (abort_)
+        if (!wait_t0) {
+          wait_t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (ws_load(&sh->abort_) || watchdog_expired(C, wait_t0, WDOG_PHOTON_WAVE)) {
+          if (lane_id == 0) __hip_atomic_store(&sh->abort_, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          break;
+        }
+      } else {
+        wait_t0 = 0;
       }
       WST(WD_TP_P8);
     }
@@ -819,7 +846,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
         }
       }
       if (!__ballot(run)) {
-        // nothing queued: done once every photon wave has finished (the final tail is known)
+        // nothing queued: done once every photon wave has finished (the final tail is known), or
+        // at once when the watchdog fired in this block
+        if (ws_load(&sh->abort_)) break;
         if (ws_load(&sh->alive) == 0) {
           const uint32_t T = ws_load(&sh->ev_tail);
           if (pend && (int32_t)(tk - T) >= 0) pend = false;  // (a ticket nobody will write)
@@ -1014,7 +1043,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       WST(WD_TW_CLAIM);
       if (!am) {
         // nothing to walk: once every photon wave has finished, the final tail is known and the
-        // tickets past it are never reserved; done when no lane holds an earlier one
+        // tickets past it are never reserved; done when no lane holds an earlier one (or at once
+        // when the watchdog fired in this block)
+        if (ws_load(&sh->abort_)) break;
         if (ws_load(&sh->alive) == 0) {
           const uint32_t T = ws_load(&sh->tail);
           if (pend && (int32_t)(tk - T) >= 0) pend = false;  // (a ticket nobody will write)

@@ -54,6 +54,7 @@ def load_library(path: str = LIB_PATH):
                                        C.POINTER(abi.DeviceTallies), C.c_void_p]
         L.smcrt_scene_set_timing.argtypes = [C.c_void_p, C.c_int32]
         L.smcrt_scene_fence.argtypes = [C.c_void_p, C.c_void_p]
+        L.smcrt_scene_check.argtypes = [C.c_void_p]
         L.smcrt_scene_kernel_times.argtypes = [C.c_void_p, C.POINTER(abi.KernelTimes)]
         L.smcrt_normalise_fluence.argtypes = [C.POINTER(C.c_float), C.POINTER(abi.Grid), C.c_uint64]
         L.smcrt_scene_info.argtypes = [C.c_void_p, C.POINTER(abi.Grid), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -256,6 +257,11 @@ class Engine:
     def fence(self, stream: int = 0):
         """Make `stream` wait for the deposit folds of FLAG_ASYNC_FOLD launches."""
         _check(load_library().smcrt_scene_fence(self._h, C.c_void_p(stream)))
+
+    def check(self):
+        """Wait for the scene's launches and folds; raise SmcrtError (DEVICE_FAULT, naming the
+        wait site) if the watchdog fired in any of them (smcrt_scene_check)."""
+        _check(load_library().smcrt_scene_check(self._h))
 
     def set_timing(self, enable: bool = True):
         """Record HIP events around each kernel group of later launches."""

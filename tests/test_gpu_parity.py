@@ -1076,3 +1076,49 @@ def test_modifier_scenes():
         gpu, cpu = both(sc, g, src, n)
         compare(gpu, cpu)
         assert cpu.counter("fresnel") > 0
+
+
+def test_watchdog_lost_event_is_an_error_not_a_hang(monkeypatch):
+    """The watchdog: a photon whose event is marked queued but never
+    queued (SMCRT_DEBUG_DROP_EVENT: photon lane 0 of block 0, its first event -- the class of
+    the round-5 test_kernel Fresnel bug) would wait forever. With every cross-wave wait bounded
+    (SMCRT_WATCHDOG_MS) its wave gives up, the block's waves leave their loops, the grid
+    drains, and the run returns DEVICE_FAULT naming the photon-wave wait -- in well under the
+    test's time limit. The word is cleared, so the same resident scene then runs exactly."""
+    import time
+    from rsmcrt_amd.engine import SmcrtError
+    sc = builders.setup_sphere(10.0, 0.1, 0.9, 1.0, 1.0)
+    g = scene.grid(64, 64, 64, 1, 1, 1)
+    src = scene.point_source()
+    monkeypatch.setenv("SMCRT_LEAN", "1")
+    monkeypatch.setenv("SMCRT_WATCHDOG_MS", "300")
+    with Engine(sc, g) as eng:
+        monkeypatch.setenv("SMCRT_DEBUG_DROP_EVENT", "1")
+        t0 = time.time()
+        with pytest.raises(SmcrtError, match=r"DEVICE_FAULT.*watchdog.*photon wave.*block 0"):
+            eng.run(src, 20000, seed=SEED)
+        assert time.time() - t0 < 60
+        monkeypatch.delenv("SMCRT_DEBUG_DROP_EVENT")
+        eng.kernel_times()
+        gpu = eng.run(src, 3000, seed=SEED, records=True)
+        assert eng.kernel_times()["lean_launches"] > 0
+        eng.check()  # (nothing pending, no fault)
+    cpu = O.run(sc, g, src, 3000, seed=SEED, records=True)
+    compare(gpu, cpu)
+
+
+def test_watchdog_bucket_wait(monkeypatch):
+    """The bucket wait of deposit.h under the watchdog: every claim held open ~27 us
+    (SMCRT_DEBUG_CLAIM_DELAY=8) against a 5 us budget, so the lanes that wait for a claim give
+    up; the run returns DEVICE_FAULT naming the bucket wait (transport_kernel: SMCRT_LEAN=0, so
+    no photon-wave wait can fire first). Without the tiny budget the same run is exact
+    (test_bucket_claim_delayed_waits_stay_exact)."""
+    from rsmcrt_amd.engine import SmcrtError
+    monkeypatch.setenv("SMCRT_LEAN", "0")
+    monkeypatch.setenv("SMCRT_DEBUG_CLAIM_DELAY", "8")
+    monkeypatch.setenv("SMCRT_WATCHDOG_MS", "0.005")
+    sc = builders.setup_sphere(0.5, 0.01, 0.9, 1.0, 1.0)
+    src = scene.pencil_source((0.0, 0.0, -0.99), (0.0, 0.0, 1.0))
+    with Engine(sc, scene.grid(64, 64, 64, 1, 1, 1)) as eng:
+        with pytest.raises(SmcrtError, match=r"DEVICE_FAULT.*watchdog.*bucket wait"):
+            eng.run(src, 60000, seed=SEED)
