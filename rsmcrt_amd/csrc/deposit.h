@@ -384,6 +384,8 @@ __global__ __launch_bounds__(BIN_THREADS) void bin_scatter(const unsigned long l
 #ifndef SMCRT_REC6
 #define SMCRT_REC6 1
 #endif
+// 6-byte records keep the voxel within the tile as a u16
+static_assert(!SMCRT_REC6 || TILE_SHIFT <= 16, "SMCRT_REC6 records need tiles of at most 2^16 voxels");
 constexpr uint32_t BUCKET_SHIFT = 8;
 constexpr uint32_t BUCKET_RECORDS = 1u << BUCKET_SHIFT;  // 2 KiB per bucket
 #ifndef SMCRT_BUCKET_BATCH

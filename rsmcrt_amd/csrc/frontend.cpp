@@ -332,7 +332,12 @@ class ListReader {
 // get_vessels, setupGeometry.f90:552-652: a vessel net read from edges.dat (pairs of 1-based
 // node indices), nodes.dat (x y z per node) and radii.dat (one radius per node), next to the
 // input file (the reference opens res/<name>.dat). Capsules (vessel optics, layer 1) per edge,
-// then the .32 x .18 x .26 dermis box (layer 2). Kept from the reference:
+// then the .32 x .18 x .26 dermis box (layer 2). One deliberate deviation: the reference never
+// closes the unit it counts nodes.dat with (:596-602) and opens the same file again at :614;
+// gfortran refuses to connect a file already connected to another unit (iostat /= 0), so as
+// built the node loop reads nothing and nodes() stays undefined. This follows the intended
+// read (the nodes are read), as the Fortran glue does; parity with the reference as compiled
+// is unpinned there. Otherwise the reads follow the reference:
 //  * the counts are the number of successful reads (:585-602); reading stops at the first
 //    failed read in each loop (:605-627);
 //  * nodes.dat is read with the EDGE count as the loop bound (:615), so with fewer edges than

@@ -6,9 +6,11 @@
 //
 // Same path as transport_kernel (noBiasPropagation kernelsMod.f90:1901-1976 -> tauint2
 // inttau2.f90:15-364 -> update_grids :367-465), same arithmetic, same results bit for bit,
-// for the scenes the north-star workload is made of: every top-level SDF has the same
-// refractive index (no Fresnel events: reflect_refract is never reached, :248), no detectors,
-// no survival bias, path-length deposition into buckets (deposit.h), the three plain sources.
+// for scenes of few tops with no survival bias, path-length deposition into buckets
+// (deposit.h) and the three plain sources. Scenes with Fresnel interfaces (reflect_refract,
+// :248-328, in the event waves) take it by default through ws_kernel's XF instantiation (round
+// 5); scenes with detectors run the XF instantiation only with SMCRT_LEAN=1 (record_hits at
+// every segment end in the photon waves: transport_kernel measured faster on M5).
 //
 // Why a second kernel. In transport_kernel a photon that starts a deposit segment
 // (update_grids) walks it before it may take its next step, and every lane of a wave walks its

@@ -917,15 +917,16 @@ def test_multi_accumulate_dynamic_chunks_one_collect(monkeypatch):
 @pytest.mark.parametrize("case", ["absorbing", "boundary-source", "test-kernel", "fresnel", "detectors",
                                   "bounce-abort", "fresnel-test-kernel"])
 def test_lean_kernel_paths(monkeypatch, case):
-    """The lean path (ws_kernel, ws.h: Fresnel-free, detector-free scenes, the voxel walk and
-    the interactions decoupled from the photon) against the oracle, photon by photon, on the paths it adds:
+    """The lean path (ws_kernel, ws.h: scenes of few tops, the voxel walk and the interactions
+    decoupled from the photon; Fresnel scenes by default and detector scenes with SMCRT_LEAN=1
+    through its XF instantiation) against the oracle, photon by photon, on the paths it adds:
     * absorbing: mua = 2 (albedo 0.83), so many photons are absorbed while their last
       segment is still being walked (ST_ABSORB waits for the cells recordWeight needs);
     * boundary-source: a uniform source on the top face, so segments near the grid faces are
       synchronous (the photon waits for tflag/cells) and escapes through the walk are common;
     * test-kernel: test_kernel semantics (no re-emission, ds<=0 mask, scatter moments);
-    * fresnel: the Tran & Jacques sphere (n=1.33 in air, M3's scene): reflect_refract's program
-      points (F0/F1, the calcNormal taps, reflection and refraction) in the photon waves;
+    * fresnel: the Tran & Jacques sphere (n=1.33 in air, M3's scene): reflect_refract (the ds
+      pair, the calcNormal taps, reflection and refraction) as an event of the event waves;
     * detectors: M5's layered skin with Fresnel at every interface and a circle and an annulus
       detector at the top face (record_hits from each segment's start point);
     * bounce-abort: an almost transparent n=1.5 sphere with an off-centre source, so photons
