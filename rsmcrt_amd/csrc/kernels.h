@@ -767,6 +767,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           else if (LU(LU_STATUS) == 0) { LU(LU_STATUS) = 2; LCTR(LC_ESCAPED)++; }
           LCTR(LC_PHOTONS)++;
           LCTR(LC_DRAWS) += L.rng.draws;
+#ifdef SMCRT_DIAG
+          if (C->done_time)
+            C->done_time[(((uint64_t)L.rng.pid_hi << 32) | L.rng.pid_lo) - C->done_base] = __builtin_amdgcn_s_memrealtime();
+#endif
           smcrt_photon_record* const records = C->records;
           if ((K.flags & SMCRT_FLAG_RECORD_PHOTONS) && records) {
             const uint64_t pid = ((uint64_t)L.rng.pid_hi << 32) | L.rng.pid_lo;

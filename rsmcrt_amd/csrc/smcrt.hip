@@ -154,6 +154,10 @@ struct smcrt_scene {
   // starts in the grid is deferred (forces hazards on escaping segments)
   uint32_t lean_debug = 0;
   int64_t lean_launches = 0;  // since the last smcrt_scene_kernel_times
+#ifdef SMCRT_DIAG
+  unsigned long long* d_done = nullptr;  // per-photon completion times of the last run (SMCRT_DIAG_DONE)
+  uint64_t n_done = 0;
+#endif
   // SMCRT_LEAN: -1 automatic, 0 off, 1 forced. (Rounds 3-4 chose lean_kernel only up to 5.5
   // voxel crossings per segment: long walks were cheaper in one lane. ws_kernel's walker waves
   // take them at any length: M0, 8.2 crossings per segment, 54.9 vs 43.4-44.2 M photons/s on
@@ -1170,6 +1174,20 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   Ch.lean_hazards = s->d_queue + MAX_SLOTS + 3;
   Ch.lane_scratch = nullptr;  // (per launch stream: launch_one)
   Ch.watchdog = watchdog_word(s);
+#ifdef SMCRT_DIAG
+  Ch.done_time = nullptr;
+  Ch.done_base = cfg->first_photon;
+  if (const char* dd = std::getenv("SMCRT_DIAG_DONE")) {  // (diagnostic builds: completion times)
+    if (dd[0] == '1' && !orun) {
+      if (s->d_done) (void)hipFree(s->d_done);
+      s->d_done = nullptr;
+      s->n_done = cfg->n_photons;
+      HIPCHK(hipMalloc(&s->d_done, sizeof(unsigned long long) * s->n_done));
+      HIPCHK(hipMemsetAsync(s->d_done, 0, sizeof(unsigned long long) * s->n_done, stream));
+      Ch.done_time = s->d_done;
+    }
+  }
+#endif
   {  // every cross-wave wait is bounded (transport.h watchdog_expired); 0 ms: unbounded
     const char* wm = std::getenv("SMCRT_WATCHDOG_MS");
     const double ms = wm ? std::strtod(wm, nullptr) : (double)DEFAULT_WATCHDOG_MS;
@@ -1401,6 +1419,15 @@ int smcrt_diag_read(unsigned long long* out) {
   HIPCHK(hipDeviceSynchronize());
   unsigned long long hc[6];
   kinst_diag_gather(out, out + 72, hc);
+  return SMCRT_OK;
+}
+// The completion time (s_memrealtime ticks) of each photon of the scene's last run made with
+// SMCRT_DIAG_DONE=1 (n of them; 0 = not completed), and the tick rate in kHz.
+int smcrt_diag_done_times(smcrt_scene* s, unsigned long long* out, uint64_t n, int32_t* khz) {
+  if (!s || !out || !s->d_done || n > s->n_done) return fail(SMCRT_ERR_INVALID_ARG, "no completion times");
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, s->d_done, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost));
+  if (khz) *khz = s->wall_khz;
   return SMCRT_OK;
 }
 #endif

@@ -82,6 +82,12 @@ struct KCold {
   // naming the site) and its wave gives up the wait, so the grid drains instead of hanging
   uint32_t* watchdog;
   uint64_t watchdog_ticks;
+#ifdef SMCRT_DIAG
+  // diagnostic builds: each photon's completion time (s_memrealtime) at done_time[pid - done_base]
+  // (smcrt_diag_done_times; SMCRT_DIAG_DONE=1), or null
+  unsigned long long* done_time;
+  uint64_t done_base;
+#endif
   SrcPlan plan;               // the general emitter's constants (XSRC instantiations only)
 };
 

@@ -763,6 +763,10 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             else if (WLU(LL_STATUS) == 0) { WLU(LL_STATUS) = 2; ws_count(sh, LC_ESCAPED); }
             ws_count(sh, LC_PHOTONS);
             atomicAdd(&sh->wctr[wv][LC_DRAWS], P.rng.draws);
+#ifdef SMCRT_DIAG
+            if (C->done_time)
+              C->done_time[(((uint64_t)P.rng.pid_hi << 32) | P.rng.pid_lo) - C->done_base] = __builtin_amdgcn_s_memrealtime();
+#endif
             if (records_on) {
               const uint64_t pid = ((uint64_t)P.rng.pid_hi << 32) | P.rng.pid_lo;
               smcrt_photon_record* r = C->records + (pid - C->first_photon);
