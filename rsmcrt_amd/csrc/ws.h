@@ -629,6 +629,7 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                     (XF && P.st == ST_F0 && !(ws_busy(sh, pl) & (1u << P.seq))));
         if (drop_event && qev) {  // (debug knob: a missed enqueue; the photon waits for nothing)
           drop_event = qev = false;
+          __hip_atomic_store(&sh->ev_code[pl], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           P.set(LF_EVQ);
         }
         const uint64_t qm = __ballot(qev);
