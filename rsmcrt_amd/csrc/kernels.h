@@ -213,7 +213,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
         chunk_left -= take;
         need = __ballot(L.st == ST_FETCH);
       }
-      if (__ballot(L.st != ST_IDLE) == 0) break;
+      const uint64_t live = __ballot(L.st != ST_IDLE);
+      if (live == 0) break;
     }
 
 #ifdef SMCRT_DIAG_STATES  // (diagnostic builds: lane states per trip into g_diag[0..66])

@@ -471,7 +471,9 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   // A sparse wave evaluates its lanes' SDF arrays one lane at a time across the wave when
   // that is cheaper than the serial per-lane chain over all n_top tops (transport.h).
   for (const ProgOp& op : prog) s->nested = s->nested || (op.action & PROG_SUB) != 0;
-  s->coop_lanes = n_top >= 8 ? std::min(16, n_top / ((n_top + 63) / 64 + 3)) : 0;
+  int32_t coop_min = 8;  // (SMCRT_COOP_MIN_TOPS: the fewest tops that get the COOP instantiation)
+  if (const char* cm = std::getenv("SMCRT_COOP_MIN_TOPS")) coop_min = std::max(1, std::atoi(cm));
+  s->coop_lanes = n_top >= coop_min ? std::max(1, std::min(16, n_top / ((n_top + 63) / 64 + 3))) : 0;
   // The cooperative EVAL's LDS table: at most 64 tops, none of them a model (transport.h).
   // SMCRT_COOP_TAB=0 keeps the global-memory cooperative EVAL.
   std::vector<double> ctab;

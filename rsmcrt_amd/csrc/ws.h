@@ -317,7 +317,8 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           need = __ballot(P.st == ST_FETCH);
         }
         if (!more && P.st == ST_FETCH) P.st = ST_IDLE;
-        if (__ballot(P.st != ST_IDLE) == 0) break;  // (walkers finish this wave's segments)
+        const uint64_t live = __ballot(P.st != ST_IDLE);
+        if (live == 0) break;  // (walkers finish this wave's segments)
       }
       WST(WD_TP_FETCH);
       // an event lane's results (see "Event waves"): the photon evaluates this trip

@@ -38,6 +38,7 @@ with Engine(sc, g, dets) as eng:
     khz = C.c_int32()
     st = L.smcrt_diag_done_times(eng._h, t.ctypes.data_as(C.POINTER(C.c_ulonglong)), n, C.byref(khz))
     assert st == 0, st
+slow = np.argsort(t)[-64:][::-1]  # the 64 last photons (indices from first_photon = 2^40)
 done = t[t > 0].astype(np.float64)
 assert done.size == n, (done.size, n)
 ms = (done - done.min()) / khz.value  # ms after the first completion
@@ -54,9 +55,12 @@ res = {
     "bulk_photons_per_s": bulk, "photons_per_s_launch": n / (launch_ms * 1e-3),
     "sdf_evals_per_s": cd["sdf_evals"] / (launch_ms * 1e-3), "sdf_evals_per_photon": cd["sdf_evals"] / n,
     "far_steps": kt.get("far_steps"),
+    "slowest_photons": [int(i) + (1 << 40) for i in slow],
+    "slowest_ms": [float((t[i] - t[t > 0].min()) / khz.value) for i in slow],
     "hist_ms": np.histogram(ms, bins=200)[0].tolist(), "hist_edges_ms": [0.0, float(span)],
 }
-print(json.dumps({k: v for k, v in res.items() if not k.startswith("hist")}, indent=1))
+print(json.dumps({k: v for k, v in res.items() if not k.startswith("hist") and not k.startswith("slowest")}, indent=1))
+print("slowest photons (index, ms):", list(zip(res["slowest_photons"][:8], [round(x, 2) for x in res["slowest_ms"][:8]])))
 os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
 with open(out_path, "w") as f:
     json.dump(res, f)
