@@ -77,6 +77,11 @@ namespace smcrt {
 #ifndef SMCRT_WS_WAVES
 #define SMCRT_WS_WAVES 16
 #endif
+// the photon hands a segment's start cell to its walker in the slot's cell word (1) instead of
+// the walker recomputing it from the start (0); the same cell_of on the same start either way
+#ifndef SMCRT_WS_START_CELLS
+#define SMCRT_WS_START_CELLS 1
+#endif
 constexpr int WS_WAVES = SMCRT_WS_WAVES;  // waves per block (8: two blocks per CU, 16: one)
 constexpr int WS_THREADS = 64 * WS_WAVES;
 constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (waves 0 .. WS_PW-1)
@@ -509,6 +514,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
                                 e.z <= ez;
             push = true;
             sync = !inside && !defer_all;
+#if SMCRT_WS_START_CELLS
+            sh->pcell[pl][slot] = lean_pack(ci, cj, ck);  // the start cell for the walker (slot free)
+#endif
             if constexpr (GM != 2) {
               // faces k*2max/n and the cell of a point are rounded separately, so a start
               // within an ulp of a face may lie outside its own cell: the walk's first wall
@@ -1033,9 +1041,16 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           W.slen = l;
           wmeta = m;
           // the start cell, as the photon computed it from the same start (update_grids :401-415)
+#if SMCRT_WS_START_CELLS
+          {  // (written by the photon into the slot's cell word before the token)
+            const unsigned long long cw = sh->pcell[m & 511u][(m >> 9) & 3u];
+            W.xcell = lean_cell(cw, 0); W.ycell = lean_cell(cw, 1); W.zcell = lean_cell(cw, 2);
+          }
+#else
           W.xcell = cell_of<GM>(W.old.x, K.nx, K.xmax, K.inv2x, K.fex);
           W.ycell = cell_of<GM>(W.old.y, K.ny, K.ymax, K.inv2y, K.fey);
           W.zcell = cell_of<GM>(W.old.z, K.nz, K.zmax, K.inv2z, K.fez);
+#endif
           W.sd = 0.0; W.dda_it = 0;
           W.seg = true; W.tflag = false; W.fault = false;
           pend = false;
