@@ -82,11 +82,6 @@ namespace smcrt {
 #ifndef SMCRT_WS_START_CELLS
 #define SMCRT_WS_START_CELLS 1
 #endif
-// segments a walker lane holds at once (1, or 2: see the walker waves)
-#ifndef SMCRT_WS_WSEG
-#define SMCRT_WS_WSEG 1
-#endif
-static_assert(SMCRT_WS_WSEG == 1 || SMCRT_WS_START_CELLS, "two walker segments take the photon's start cells");
 constexpr int WS_WAVES = SMCRT_WS_WAVES;  // waves per block (8: two blocks per CU, 16: one)
 constexpr int WS_THREADS = 64 * WS_WAVES;
 constexpr int WS_PW = SMCRT_WS_PHOTON_WAVES;  // photon waves per block (waves 0 .. WS_PW-1)
@@ -993,7 +988,6 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
   } else {
     WS_MARK(10);
     // =================================================================== walker waves ======
-#if SMCRT_WS_WSEG == 1
     WalkSeg W;
     W.old = v3(0.0, 0.0, 0.0);
     W.sd = W.slen = 0.0;
@@ -1109,136 +1103,6 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
       }
       WST(WD_TW_FIN);
     }
-#else
-    // Two segments per walker lane (SMCRT_WS_WSEG = 2): each lane keeps up to NS segments, each
-    // with its own ticket; an iteration walks one crossing of every held segment, so the
-    // crossings of a lane's segments are independent chains (their latencies overlap) and a
-    // long segment does not hold back the lane's other one. Ticket order, the sequence locks and
-    // the end condition are the one-segment loop's, per segment slot.
-    constexpr int NS = SMCRT_WS_WSEG;
-    WalkSeg W[NS];
-    V3 wdir[NS], wrcp[NS];
-    uint32_t wmeta[NS], tk[NS];
-    bool pend[NS];
-#pragma unroll
-    for (int q = 0; q < NS; ++q) {
-      W[q].old = v3(0.0, 0.0, 0.0);
-      W[q].sd = W[q].slen = 0.0;
-      W[q].xcell = W[q].ycell = W[q].zcell = 0;
-      W[q].dda_it = 0;
-      W[q].seg = W[q].tflag = W[q].fault = false;
-      wdir[q] = wrcp[q] = v3(0.0, 0.0, 0.0);
-      wmeta[q] = tk[q] = 0;
-      pend[q] = false;
-    }
-    BucketLog WB;
-    WB.next = WB.end = 0;
-    uint32_t overflow = 0;
-    for (;; ++w_iters) {
-      WS_MARK(11);
-      {  // one ticket per free, non-pending segment slot: one LDS add for the wave
-        uint64_t cmq[NS];
-        uint32_t tot = 0;
-#pragma unroll
-        for (int q = 0; q < NS; ++q) { cmq[q] = __ballot(!W[q].seg && !pend[q]); tot += (uint32_t)__popcll(cmq[q]); }
-        if (tot) {
-          uint32_t base = 0;
-          if (lane_id == 0) base = atomicAdd(&sh->head, tot);
-          base = __builtin_amdgcn_readfirstlane(base);
-#pragma unroll
-          for (int q = 0; q < NS; ++q) {
-            if (!W[q].seg && !pend[q]) {
-              tk[q] = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(cmq[q] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cmq[q], 0u));
-              pend[q] = true;
-            }
-            base += (uint32_t)__popcll(cmq[q]);
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {
-        if (pend[q]) {
-          const uint32_t ix = tk[q] & (WS_RING - 1);
-          const uint32_t m = __hip_atomic_load(&sh->meta[ix], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if ((m & WS_SEQ_MASK) == ws_tick(tk[q])) {
-            __hip_atomic_store(&sh->meta[ix], ws_tick(tk[q]) | WS_CONSUMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const double* const sg = &sh->seg[(m >> 9) & 3u][0][m & 511u];
-            const V3 dd = v3(sg[SG_DX * WS_NPL], sg[SG_DY * WS_NPL], sg[SG_DZ * WS_NPL]);
-            W[q].old = v3(sg[SG_OX * WS_NPL], sg[SG_OY * WS_NPL], sg[SG_OZ * WS_NPL]);
-            wdir[q] = dd;
-            wrcp[q] = v3(ieee_rcp_f64(dd.x), ieee_rcp_f64(dd.y), ieee_rcp_f64(dd.z));
-            W[q].slen = sg[SG_LEN * WS_NPL];
-            wmeta[q] = m;
-            // the start cell the photon computed from the same start (update_grids :401-415)
-            const unsigned long long cw = sh->pcell[m & 511u][(m >> 9) & 3u];
-            W[q].xcell = lean_cell(cw, 0); W[q].ycell = lean_cell(cw, 1); W[q].zcell = lean_cell(cw, 2);
-            W[q].sd = 0.0; W[q].dda_it = 0;
-            W[q].seg = true; W[q].tflag = false; W[q].fault = false;
-            pend[q] = false;
-          }
-        }
-      }
-      bool any_seg = false, any_pend = false;
-#pragma unroll
-      for (int q = 0; q < NS; ++q) { any_seg = any_seg || W[q].seg; any_pend = any_pend || pend[q]; }
-      const uint64_t am = __ballot(any_seg);
-      WSDIAG(WD_WITERS, 1);
-      WSDIAG(WD_WIDLE, am ? 0 : 1);
-      WSDIAG(WD_WBUSY, __popcll(am));
-      WSDIAG(WD_WPEND, __popcll(__ballot(any_pend)));
-      WST(WD_TW_CLAIM);
-      if (!am) {
-        // nothing to walk: as the one-segment loop (every pending ticket of the lane checked)
-        if (ws_load(&sh->abort_)) break;
-        if (ws_load(&sh->alive) == 0) {
-          const uint32_t T = ws_load(&sh->tail);
-          bool pp = false;
-#pragma unroll
-          for (int q = 0; q < NS; ++q) {
-            if (pend[q] && (int32_t)(tk[q] - T) >= 0) pend[q] = false;  // (a ticket nobody will write)
-            pp = pp || pend[q];
-          }
-          if (!__ballot(pp) && (int32_t)(ws_load(&sh->head) - T) >= 0) break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        WST(WD_TW_IDLE);
-        continue;
-      }
-      WS_MARK(12);
-      bool was[NS];
-#pragma unroll
-      for (int q = 0; q < NS; ++q) was[q] = W[q].seg;
-#pragma unroll
-      for (int k = 0; k < SMCRT_WS_DDA; ++k) {
-        bool dep[NS];
-        uint32_t vox[NS];
-        double val[NS];
-#pragma unroll
-        for (int q = 0; q < NS; ++q) {  // independent crossings (one per held segment)
-          dep[q] = false; vox[q] = 0; val[q] = 0.0;
-          if (W[q].seg) dda_step_r<GM>(K, W[q], wdir[q], wrcp[q], xf, yf, zf, dep[q], vox[q], val[q], 1.0);
-          w_dep += __popcll(__ballot(dep[q]));
-        }
-        WS_MARK(13);
-#pragma unroll
-        for (int q = 0; q < NS; ++q) emit_bucketed(K, C, WB, dep[q], vox[q], val[q], overflow, bstate);
-      }
-      WS_MARK(14);
-      WST(WD_TW_WALK);
-#pragma unroll
-      for (int q = 0; q < NS; ++q) {  // a finished segment: cells and flags to the owner's slot
-        if (was[q] && !W[q].seg) {
-          const uint32_t owner = wmeta[q] & 511u, slot = (wmeta[q] >> 9) & 3u;
-          const bool sync = (wmeta[q] & (1u << 11)) != 0;
-          if (!sync && (W[q].tflag || W[q].fault)) ++hazards;  // cannot happen (lean.h); counted as a fault
-          sh->pcell[owner][slot] = lean_pack(W[q].xcell, W[q].ycell, W[q].zcell) | (W[q].tflag ? LEAN_TFLAG : 0ull) |
-                                   (W[q].fault ? LEAN_FAULT : 0ull);
-          __hip_atomic_fetch_and(&sh->busy[owner], ~(1u << slot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-      WST(WD_TW_FIN);
-    }
-#endif
     WS_MARK(15);
     close_buckets(K, C, WB, w_dep - overflow, overflow);
   }
