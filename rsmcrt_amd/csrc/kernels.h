@@ -443,7 +443,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
           if (lane_id == l) R = o;
         }
       } else if (COOP && K.cull) {  // many tops: exact culling (cull.h)
-        R = eval_culled<XSRC>(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj);
+        R = eval_culled<XSRC>(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj,
+                              K.ctab ? ctab : nullptr);
       } else {
         R = eval_sdfs<XSRC>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }

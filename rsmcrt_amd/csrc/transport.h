@@ -1130,11 +1130,20 @@ static __device__ unsigned long long g_cull_diag[6];
 #ifndef SMCRT_CULL_PREFETCH
 #define SMCRT_CULL_PREFETCH 1
 #endif
+// (ct: the cooperative EVAL's LDS table when the block staged it (at most 64 single-primitive
+// tops): a listed top's kind, transform and parameters then come from LDS by its index, not
+// from its node in device memory; sdf_prim_s of the same doubles, so the same value bit for bit)
+#ifndef SMCRT_CULL_CTAB
+#define SMCRT_CULL_CTAB 1
+#endif
+#ifndef SMCRT_CULL_UNROLL
+#define SMCRT_CULL_UNROLL 4  // (M2: 17.4-18.2 with 4, 17.1-17.4 with 2, 15.1-17.2 with 1, profiles/r06_s6/ab_m2_cull.txt)
+#endif
 template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict__ nodes,
                                                const ProgOp* __restrict__ prog, int32_t n_prog,
                                                const CullGrid* __restrict__ G, V3 q, bool have, bool mask_le,
-                                               int32_t capi, int32_t capj) {
+                                               int32_t capi, int32_t capj, const double* ct = nullptr) {
   EvalOut r;
   r.minabs = __builtin_inf();
   r.minv = __builtin_inf();
@@ -1172,12 +1181,57 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     const uint32_t c = (uint32_t)ix + (uint32_t)G->n[0] * ((uint32_t)iy + (uint32_t)G->n[1] * (uint32_t)iz);
     const uint32_t b = G->off[c], e = G->off[c + 1];
     const uint2* __restrict__ ent = (const uint2*)G->list;
+    uint32_t k0 = b;
+#if SMCRT_CULL_UNROLL > 1
+    // SMCRT_CULL_UNROLL listed tops at a time when the block staged the LDS table: if they are
+    // all translation-only spheres, their evaluations are straight-line code (sdf_prim_s's
+    // sphere formula, the same operations), so the square-root chains overlap. The fold is
+    // order free (min, abs-min; maxloc ties go to the lowest index by its explicit compare).
+    // (The same for capsules from device memory, M4, measured -12 %: not done.)
+    if (SMCRT_CULL_CTAB && ct) {
+      constexpr int U = SMCRT_CULL_UNROLL;
+      for (; k0 + (U - 1) < e; k0 += U) {
+        uint2 eu[U];
+        uint32_t anymodel = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) { eu[u] = ent[k0 + u]; anymodel |= eu[u].x; }
+        if (anymodel & CULL_MODEL) break;  // (the loop below takes the rest)
+        int32_t iu[U];
+        double ku[U], du[U];
+        bool spheres = true;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          iu[u] = (int32_t)(eu[u].x & CULL_TOP_MASK);
+          ku[u] = ct[20 * 64 + iu[u]];
+          spheres = spheres && ku[u] == (double)(SMCRT_SDF_SPHERE + 16);
+        }
+        if (spheres) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) du[u] = sdf_prim_s<64>(SMCRT_SDF_SPHERE, ct + iu[u], ct + 12 * 64 + iu[u], q, true);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            du[u] = sdf_prim_s<64>((int32_t)ku[u] & 15, ct + iu[u], ct + 12 * 64 + iu[u], q, ku[u] >= 16.0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const double d = du[u];
+          const int32_t t = iu[u] + 1;
+          const double a = fabs(d);
+          if (a < r.minabs) r.minabs = a;
+          if (d < r.minv) r.minv = d;
+          const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+          if (neg && (r.maxloc == 0 || d > best || (d == best && t < r.maxloc))) { best = d; r.maxloc = t; }
+        }
+      }
+    }
+#endif
 #if SMCRT_CULL_PREFETCH
     // the next entry's load is issued before this entry's SDF, so the list walk pays one
     // memory latency per entry (the node's) instead of two
-    uint2 nxt = b < e ? ent[b] : make_uint2(0u, 0u);
+    uint2 nxt = k0 < e ? ent[k0] : make_uint2(0u, 0u);
 #endif
-    for (uint32_t k = b; k < e; ++k) {  // per lane: its cell's tops, ascending
+    for (uint32_t k = k0; k < e; ++k) {  // per lane: its cell's tops, ascending
 #if SMCRT_CULL_PREFETCH
       const uint2 en = nxt;
       if (k + 1 < e) nxt = ent[k + 1];
@@ -1196,6 +1250,9 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
           else acc = csg(op.op, acc, v, op.k);
         }
         d = acc;
+      } else if (SMCRT_CULL_CTAB && ct) {
+        const double kc = ct[20 * 64 + i];
+        d = sdf_prim_s<64>((int32_t)kc & 15, ct + i, ct + 12 * 64 + i, q, kc >= 16.0);
       } else {
         d = sdf_prim(nodes + en.y, q, (en.x & CULL_TRANSLATE) != 0);
       }
