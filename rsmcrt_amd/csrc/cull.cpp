@@ -260,7 +260,10 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
       const bool tr = m[0] == 1.0 && m[1] == 0.0 && m[2] == 0.0 && m[4] == 0.0 && m[5] == 1.0 && m[6] == 0.0 &&
                       m[8] == 0.0 && m[9] == 0.0 && m[10] == 1.0;  // (smcrt_scene_create's test)
       const bool model = nd.kind == SMCRT_SDF_MODEL;
-      H.list.push_back(t | (model ? CULL_MODEL : 0u) | (!model && tr ? CULL_TRANSLATE : 0u));
+      const bool prim = !model && tr;  // (the flags of the culled EVAL's straight-line groups)
+      H.list.push_back(t | (model ? CULL_MODEL : 0u) | (prim ? CULL_TRANSLATE : 0u) |
+                       (prim && nd.kind == SMCRT_SDF_SPHERE ? CULL_SPHERE : 0u) |
+                       (prim && nd.kind == SMCRT_SDF_CAPSULE ? CULL_CAPSULE : 0u));
       H.list.push_back(model ? 0u : (uint32_t)top[t]);
     }
   H.mean_list = (double)total / (double)ncell;

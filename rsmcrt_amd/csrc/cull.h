@@ -36,7 +36,9 @@ namespace smcrt {
 // node index, so a lane reaches the primitive's parameters with one dependent load.
 constexpr uint32_t CULL_MODEL = 1u << 31;      // the top is a model: walk its program ops
 constexpr uint32_t CULL_TRANSLATE = 1u << 30;  // the node's transform is a pure translation
-constexpr uint32_t CULL_TOP_MASK = CULL_TRANSLATE - 1;
+constexpr uint32_t CULL_SPHERE = 1u << 29;     // (round 6) a translation-only sphere
+constexpr uint32_t CULL_CAPSULE = 1u << 28;    // (round 6) a translation-only capsule
+constexpr uint32_t CULL_TOP_MASK = CULL_CAPSULE - 1;
 
 // Device view of the culling grid (one copy per scene in device memory).
 struct CullGrid {

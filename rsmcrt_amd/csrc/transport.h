@@ -1137,7 +1137,10 @@ static __device__ unsigned long long g_cull_diag[6];
 #define SMCRT_CULL_CTAB 1
 #endif
 #ifndef SMCRT_CULL_UNROLL
-#define SMCRT_CULL_UNROLL 4  // (M2: 17.4-18.2 with 4, 17.1-17.4 with 2, 15.1-17.2 with 1, profiles/r06_s6/ab_m2_cull.txt)
+#define SMCRT_CULL_UNROLL 4  // spheres (M2: 17.4-18.2 with 4, 17.1-17.4 with 2, 15.1-17.2 with 1, profiles/r06_s6/ab_m2_cull.txt)
+#endif
+#ifndef SMCRT_CULL_UNROLL_CAP
+#define SMCRT_CULL_UNROLL_CAP 2  // capsules (M4: 13.1-13.2 with 2, 12.7 with 4, 12.5 with 1, profiles/r06_s6/ab_m4_cull.txt)
 #endif
 template <bool NEST = false>
 __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict__ nodes,
@@ -1183,46 +1186,62 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     const uint2* __restrict__ ent = (const uint2*)G->list;
     uint32_t k0 = b;
 #if SMCRT_CULL_UNROLL > 1
-    // SMCRT_CULL_UNROLL listed tops at a time when the block staged the LDS table: if they are
-    // all translation-only spheres, their evaluations are straight-line code (sdf_prim_s's
-    // sphere formula, the same operations), so the square-root chains overlap. The fold is
-    // order free (min, abs-min; maxloc ties go to the lowest index by its explicit compare).
-    // (The same for capsules from device memory, M4, measured -12 %: not done.)
-    if (SMCRT_CULL_CTAB && ct) {
-      constexpr int U = SMCRT_CULL_UNROLL;
-      for (; k0 + (U - 1) < e; k0 += U) {
+    // Groups of listed tops as straight-line code (sdf_prim_s with the kind a constant: the
+    // same operations), so their load and square-root latencies overlap: SMCRT_CULL_UNROLL
+    // translation-only spheres from the LDS table, or SMCRT_CULL_UNROLL_CAP translation-only
+    // capsules (from the table or their nodes); the first other entry ends the groups and the
+    // loop below takes the rest. The fold is order free (min, abs-min; maxloc ties go to the
+    // lowest index by its explicit compare).
+    for (;;) {
+      constexpr int U = SMCRT_CULL_UNROLL, UC = SMCRT_CULL_UNROLL_CAP;
+      double du[U];
+      int32_t iu[U];
+      int n = 0;
+      if (SMCRT_CULL_CTAB && ct && k0 + (U - 1) < e) {
         uint2 eu[U];
-        uint32_t anymodel = 0;
+        uint32_t all = ~0u;
 #pragma unroll
-        for (int u = 0; u < U; ++u) { eu[u] = ent[k0 + u]; anymodel |= eu[u].x; }
-        if (anymodel & CULL_MODEL) break;  // (the loop below takes the rest)
-        int32_t iu[U];
-        double ku[U], du[U];
-        bool spheres = true;
+        for (int u = 0; u < U; ++u) { eu[u] = ent[k0 + u]; all &= eu[u].x; }
+        if (all & CULL_SPHERE) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          iu[u] = (int32_t)(eu[u].x & CULL_TOP_MASK);
-          ku[u] = ct[20 * 64 + iu[u]];
-          spheres = spheres && ku[u] == (double)(SMCRT_SDF_SPHERE + 16);
+          for (int u = 0; u < U; ++u) {
+            iu[u] = (int32_t)(eu[u].x & CULL_TOP_MASK);
+            du[u] = sdf_prim_s<64>(SMCRT_SDF_SPHERE, ct + iu[u], ct + 12 * 64 + iu[u], q, true);
+          }
+          n = U;
         }
-        if (spheres) {
+      }
+      if (n == 0 && UC > 1 && k0 + (UC - 1) < e) {
+        uint2 eu[UC];
+        uint32_t all = ~0u;
 #pragma unroll
-          for (int u = 0; u < U; ++u) du[u] = sdf_prim_s<64>(SMCRT_SDF_SPHERE, ct + iu[u], ct + 12 * 64 + iu[u], q, true);
-        } else {
+        for (int u = 0; u < UC; ++u) { eu[u] = ent[k0 + u]; all &= eu[u].x; }
+        if (all & CULL_CAPSULE) {
 #pragma unroll
-          for (int u = 0; u < U; ++u)
-            du[u] = sdf_prim_s<64>((int32_t)ku[u] & 15, ct + iu[u], ct + 12 * 64 + iu[u], q, ku[u] >= 16.0);
+          for (int u = 0; u < UC; ++u) {
+            iu[u] = (int32_t)(eu[u].x & CULL_TOP_MASK);
+            if (SMCRT_CULL_CTAB && ct) {
+              du[u] = sdf_prim_s<64>(SMCRT_SDF_CAPSULE, ct + iu[u], ct + 12 * 64 + iu[u], q, true);
+            } else {
+              const smcrt_sdf_node* nd = nodes + eu[u].y;
+              du[u] = sdf_prim_s<1>(SMCRT_SDF_CAPSULE, nd->transform, nd->param, q, true);
+            }
+          }
+          n = UC;
         }
+      }
+      if (n == 0) break;  // (the loop below takes the rest)
+      k0 += (uint32_t)n;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const double d = du[u];
-          const int32_t t = iu[u] + 1;
-          const double a = fabs(d);
-          if (a < r.minabs) r.minabs = a;
-          if (d < r.minv) r.minv = d;
-          const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
-          if (neg && (r.maxloc == 0 || d > best || (d == best && t < r.maxloc))) { best = d; r.maxloc = t; }
-        }
+      for (int u = 0; u < U; ++u) {
+        if (u >= n) break;
+        const double d = du[u];
+        const int32_t t = iu[u] + 1;
+        const double a = fabs(d);
+        if (a < r.minabs) r.minabs = a;
+        if (d < r.minv) r.minv = d;
+        const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+        if (neg && (r.maxloc == 0 || d > best || (d == best && t < r.maxloc))) { best = d; r.maxloc = t; }
       }
     }
 #endif
