@@ -446,7 +446,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
         R = eval_culled<XSRC>(nodes, prog, K.n_prog, K.cull, eval_query(L), have, mask_le, capi, capj,
                               K.ctab ? ctab : nullptr);
       } else {
-        R = eval_sdfs<XSRC>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
+        R = eval_sdfs<XSRC, true>(nodes, prog, K.n_prog, eval_query(L), mask_le, capi, capj);
       }
       // packet%cnts counts the evaluations of tauint2's ds/dsNew arrays only (inttau2.f90:67,83,
       // 138,183,219,232): not the initial layer search, the Fresnel ds lookups or calcNormal.

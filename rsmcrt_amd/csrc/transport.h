@@ -910,6 +910,9 @@ __device__ __forceinline__ void dda_step_r(const KParams& K, S& L, const V3 dir,
 #endif
 }
 
+#ifndef SMCRT_EVAL_PAIRS
+#define SMCRT_EVAL_PAIRS 1
+#endif
 // The EVAL phase: ds(i) for every top-level SDF at L.q, reduced to minval(abs(ds)),
 // minval(ds), maxloc(ds, mask) and the captured ds(capi), ds(capj).
 struct EvalOut {
@@ -921,7 +924,10 @@ struct EvalOut {
 // the compiler prove them unclobbered and keep the wave-uniform loads on the scalar path.
 // NEST: the program may hold nested-model ops (PROG_SUB); only the general instantiation
 // evaluates such scenes (smcrt.hip), so every other caller compiles without them.
-template <bool NEST = false>
+// PAIRS: two consecutive top-level spheres or boxes at a time (see below); transport_kernel
+// (M5 46.3-47.6 vs 43.4-43.8 M photons/s) but not ws_kernel's photon waves (M1 -1.4 %, M0
+// -2.3 %), profiles/r06_s6/ab_eval_pairs.txt
+template <bool NEST = false, bool PAIRS = false>
 __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ nodes,
                                              const ProgOp* __restrict__ prog, int32_t n_prog, V3 q,
                                              bool mask_le, int32_t capi, int32_t capj) {
@@ -934,6 +940,55 @@ __device__ __forceinline__ EvalOut eval_sdfs(const smcrt_sdf_node* __restrict__ 
   double acc = 0.0;
   for (int32_t ip = 0; ip < n_prog; ++ip) {
     const ProgOp op = prog[ip];
+#if SMCRT_EVAL_PAIRS
+    // two consecutive top-level spheres or boxes (any order) as straight-line code: the kinds
+    // are constants there (sdf_prim_s: the same operations), so the two evaluations' latency
+    // chains overlap; folded in program order, as below (wave-uniform branch)
+    if (PAIRS && !NEST && ip + 1 < n_prog && op.action == PROG_TOP && op.top > 0) {
+      const ProgOp op2 = prog[ip + 1];
+      if (op2.action == PROG_TOP && op2.top > 0) {
+        const smcrt_sdf_node* n1 = nodes + __builtin_amdgcn_readfirstlane(op.node);
+        const smcrt_sdf_node* n2 = nodes + __builtin_amdgcn_readfirstlane(op2.node);
+        const int32_t k1 = n1->kind, k2 = n2->kind;
+        const bool t1 = op.translate_only != 0, t2 = op2.translate_only != 0;
+        double v1 = 0.0, v2 = 0.0;
+        bool pair = true;
+        if (k1 == SMCRT_SDF_SPHERE && k2 == SMCRT_SDF_BOX) {
+          v1 = sdf_prim_s<1>(SMCRT_SDF_SPHERE, n1->transform, n1->param, q, t1);
+          v2 = sdf_prim_s<1>(SMCRT_SDF_BOX, n2->transform, n2->param, q, t2);
+        } else if (k1 == SMCRT_SDF_BOX && k2 == SMCRT_SDF_BOX) {
+          v1 = sdf_prim_s<1>(SMCRT_SDF_BOX, n1->transform, n1->param, q, t1);
+          v2 = sdf_prim_s<1>(SMCRT_SDF_BOX, n2->transform, n2->param, q, t2);
+        } else if (k1 == SMCRT_SDF_BOX && k2 == SMCRT_SDF_SPHERE) {
+          v1 = sdf_prim_s<1>(SMCRT_SDF_BOX, n1->transform, n1->param, q, t1);
+          v2 = sdf_prim_s<1>(SMCRT_SDF_SPHERE, n2->transform, n2->param, q, t2);
+        } else if (k1 == SMCRT_SDF_SPHERE && k2 == SMCRT_SDF_SPHERE) {
+          v1 = sdf_prim_s<1>(SMCRT_SDF_SPHERE, n1->transform, n1->param, q, t1);
+          v2 = sdf_prim_s<1>(SMCRT_SDF_SPHERE, n2->transform, n2->param, q, t2);
+        } else {
+          pair = false;
+        }
+        if (pair) {
+          const double dv[2] = {v1, v2};
+          const int32_t tv[2] = {op.top, op2.top};
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {
+            const double d = dv[u];
+            const int32_t i = tv[u];
+            const double a = fabs(d);
+            if (a < r.minabs) r.minabs = a;
+            if (d < r.minv) r.minv = d;
+            const bool neg = mask_le ? (d <= 0.0) : (d < 0.0);
+            if (neg && (r.maxloc == 0 || d > best)) { best = d; r.maxloc = i; }
+            if (i == capi) r.va = d;
+            if (i == capj) r.vb = d;
+          }
+          ++ip;
+          continue;
+        }
+      }
+    }
+#endif
     // the program is wave-uniform: keep node parameters on the scalar path
     const int32_t node = __builtin_amdgcn_readfirstlane(op.node);
     const double v = prog_value<NEST>(nodes, node, op.action, op.translate_only != 0, q);
