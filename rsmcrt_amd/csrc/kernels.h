@@ -65,6 +65,7 @@ constexpr uint32_t COOP_CULL_LANES = SMCRT_COOP_CULL_LANES;
 #ifndef SMCRT_SOLO_LANES
 #define SMCRT_SOLO_LANES 4
 #endif
+
 constexpr int SOLO_LANES = SMCRT_SOLO_LANES;
 
 // Waves per SIMD the register allocation aims at: 3 (<= 168 VGPRs) for the plain
@@ -242,7 +243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(COOP ? SMCR
     // segment's crossings at once. The photon's own sequence of operations is exactly the
     // main loop's, so its trajectory, counters and records are unchanged. The loop ends as
     // soon as the photon leaves the cycle (boundary probe ST_B0, a fault, a new event).
-    if constexpr (COOP) {
+    if constexpr (COOP) {  // (the plain instantiations too: 432 B of spills, M5 -30 %, profiles/r06_s6/ab_solo_plain.txt)
       const bool ev_wait = (L.st == ST_INTERACT || L.st == ST_T2 || L.st == ST_EMIT || L.st == ST_DONE);
       const uint64_t act = __ballot(L.st != ST_IDLE && !ev_wait);
       const uint64_t cand = __ballot(L.st == ST_M1 && L.pend && !L.seg);
