@@ -1203,6 +1203,12 @@ static int launch(smcrt_scene* s, const smcrt_source* src, const smcrt_run_confi
   K.lean_debug = s->lean_debug;
   if (const char* de = std::getenv("SMCRT_DEBUG_DROP_EVENT"))  // (tests only: the watchdog's proof)
     if (de[0] == '1') K.lean_debug |= 4u;
+  {  // lean_margin per axis (lean.h, ws.h), with the operations the kernel used to do
+    const double eps = 1e-8, mf = (K.lean_debug & 3u) ? 0.0 : 2.0 * eps;
+    const double mx = mf * (double)(K.nx + 2), my = mf * (double)(K.ny + 2), mz = mf * (double)(K.nz + 2);
+    K.lean_lo[0] = mx; K.lean_lo[1] = my; K.lean_lo[2] = mz;
+    K.lean_hi[0] = 2.0 * K.xmax - mx; K.lean_hi[1] = 2.0 * K.ymax - my; K.lean_hi[2] = 2.0 * K.zmax - mz;
+  }
 
   // binned deposition needs path-length tallies into jmean with unit weights (fp32 record
   // values are exact only then) and a grid of at most MAX_TILES tiles

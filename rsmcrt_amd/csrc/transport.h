@@ -142,6 +142,10 @@ struct KParams {
   // hazards. Bit 2 (SMCRT_DEBUG_DROP_EVENT, tests only): photon lane 0 of block 0 marks its first
   // event queued without queueing it (the hang class the watchdog turns into a counted fault)
   uint32_t lean_debug;
+  // the lean path's deferral box (lean.h lean_margin, corner coordinates), formed on the host so
+  // that the photon waves read six wave-uniform doubles with scalar loads instead of keeping
+  // them in VGPRs (they were spilled to scratch and reloaded at every hand-out)
+  double lean_lo[3], lean_hi[3];
   // exact SDF culling (cull.h), many-top scenes in the COOP instantiation; NULL = off
   const CullGrid* __restrict__ cull;
   // the cooperative EVAL's table of primitives (CTAB_ROWS x 64 doubles, column = top - 1),

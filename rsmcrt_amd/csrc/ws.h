@@ -254,9 +254,10 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
     const uint32_t pl = threadIdx.x;  // photon lane (the photon waves come first)
 #define WLU(f) (sh->lu[(f)][pl])
     // lean_margin (lean.h), per axis, corner coordinates; SMCRT_DEBUG_LEAN_MARGIN (tests only)
+    // (the XF instantiation reads the box from KParams at the hand-out instead, see there)
     const double mf = (K.lean_debug & 3u) ? 0.0 : 2.0 * eps;
-    const double mx = mf * (double)(K.nx + 2), my = mf * (double)(K.ny + 2), mz = mf * (double)(K.nz + 2);
-    const double ex = 2.0 * K.xmax - mx, ey = 2.0 * K.ymax - my, ez = 2.0 * K.zmax - mz;
+    const double mx0 = mf * (double)(K.nx + 2), my0 = mf * (double)(K.ny + 2), mz0 = mf * (double)(K.nz + 2);
+    const double ex0 = 2.0 * K.xmax - mx0, ey0 = 2.0 * K.ymax - my0, ez0 = 2.0 * K.zmax - mz0;
     const bool defer_all = (K.lean_debug & 3u) == 2u;
     // SMCRT_DEBUG_DROP_EVENT (tests only): this lane's first event is marked queued, never queued
     bool drop_event = (K.lean_debug & 4u) && blockIdx.x == 0 && pl == 0;
@@ -509,6 +510,12 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
           } else {
             const double len = P.d;
             const V3 e = v3(old.x + P.dir.x * len, old.y + P.dir.y * len, old.z + P.dir.z * len);
+            // The XF instantiation takes the deferral box from KParams (scalar loads; in VGPRs it
+            // spilled to scratch and was reloaded here): M3 181.0/181.6 vs 172.9/173.1 M photons/s.
+            // The other one keeps it in VGPRs, where its register allocation is faster: M1 with
+            // KParams 252.3 vs 257.5 M (profiles/r06_s7/ab_kparams_bounds.txt).
+            const double mx = XF ? K.lean_lo[0] : mx0, my = XF ? K.lean_lo[1] : my0, mz = XF ? K.lean_lo[2] : mz0;
+            const double ex = XF ? K.lean_hi[0] : ex0, ey = XF ? K.lean_hi[1] : ey0, ez = XF ? K.lean_hi[2] : ez0;
             const bool inside = old.x >= mx && old.x <= ex && old.y >= my && old.y <= ey && old.z >= mz &&
                                 old.z <= ez && e.x >= mx && e.x <= ex && e.y >= my && e.y <= ey && e.z >= mz &&
                                 e.z <= ez;
