@@ -22,7 +22,13 @@ LIB = os.path.join(PKG, "libsmcrt.so")
 SOURCES = [os.path.join(PKG, "csrc", f) for f in ("smcrt.hip", "writers.cpp", "frontend.cpp", "sources.cpp", "png.cpp", "escape.cpp", "inverse.cpp", "spectral.cpp", "multi.hip", "cull.cpp")]
 # the transport kernel instantiations: kinst.hip once per (LDS faces, grid mode), kernel_ptrs.h
 KINST = os.path.join(PKG, "csrc", "kinst.hip")
-UNITS = [(src, ()) for src in SOURCES] + [(KINST, (f"-DKI_F={f}", f"-DKI_G={g}")) for f in (0, 1) for g in (0, 1, 2)]
+# Part 1 (the plain ws_kernel, M1's lean path) schedules with the AMDGPU register-pressure
+# trackers: M1 259.0/260.2 vs 257.8/257.3 M photons/s same box, while the XF ws_kernel (M3)
+# lost 1.7 % with them (profiles/r06_s7/ab_sched_strategy.txt), so part 0 keeps the default.
+PLAIN_WS_FLAGS = ("-mllvm", "--amdgpu-use-amdgpu-trackers")
+UNITS = [(src, ()) for src in SOURCES] + [
+    (KINST, (f"-DKI_F={f}", f"-DKI_G={g}", f"-DKI_P={p}") + (PLAIN_WS_FLAGS if p else ()))
+    for f in (0, 1) for g in (0, 1, 2) for p in (0, 1)]
 DEPS = SOURCES + [KINST] + sorted(glob.glob(os.path.join(PKG, "csrc", "*.h"))) + [os.path.join(ROOT, "include", "smcrt.h")]
 ARCH = os.environ.get("SMCRT_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: no fused multiply-add, so fp64 trajectories are bit-identical to the

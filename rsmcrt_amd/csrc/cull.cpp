@@ -149,6 +149,7 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
   auto env = [](const char* k, double d) { const char* v = std::getenv(k); return v ? std::atof(v) : d; };
   const double CELLS_PER_TOP = env("SMCRT_CULL_CPT", 64.0), MAX_CELLS = env("SMCRT_CULL_MAX_CELLS", 1 << 18);
   const int32_t MAX_LIST = (int32_t)env("SMCRT_CULL_MAX_LIST", 64), K_NEAREST = (int32_t)env("SMCRT_CULL_K", 8);
+  const double U_FRAC = env("SMCRT_CULL_UFRAC", 1.0);  // (the reach U below is scaled by this)
   if (n_top < MIN_TOPS) return H;
   std::vector<Bound> bd((size_t)n_top);
   Bound dom;
@@ -215,7 +216,7 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
       };
       for (int32_t t : H.always) probe(t);
       for (int32_t j = 0; j < np; ++j) probe(cull[ord[j]]);
-      const double cut = U * (1.0 + 1e-6);
+      const double cut = U * U_FRAC * (1.0 + 1e-6);
       std::vector<int32_t> pick;
       for (int32_t j = 0; j < nc; ++j)
         if (d[j] <= cut) pick.push_back(j);

@@ -1,6 +1,7 @@
 // kernel_ptrs.h — the transport kernel instantiations, reached through pointers.
 //
-// build.py compiles kinst.hip once per (LDS faces F, grid mode G) with -DKI_F=F -DKI_G=G, so
+// build.py compiles kinst.hip once per (LDS faces F, grid mode G, part P) with -DKI_F=F -DKI_G=G
+// -DKI_P=P (part 1: the plain ws_kernel, with its own scheduler flags), so
 // the instantiations of transport_kernel and ws_kernel (kernels.h, ws.h) build in parallel
 // instead of in one translation unit. Each object exports these getters; hipLaunchKernel and
 // the occupancy queries take the host stubs they return.
@@ -17,7 +18,9 @@ size_t kinst_ws_scratch_bytes(size_t lanes);  // ws_kernel lane scratch (ws.h WX
 #define SMCRT_KINST_DECL(F, G)                                                               \
   const void* kinst_transport_##F##_##G(int xsrc, int coop);                                 \
   const void* kinst_ws_##F##_##G(int xf, int slots);                                         \
-  void kinst_diag_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6);
+  const void* kinst_wsp_##F##_##G(int slots);                                                \
+  void kinst_diag_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6); \
+  void kinst_diagp_##F##_##G(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6);
 SMCRT_KINST_DECL(0, 0)
 SMCRT_KINST_DECL(0, 1)
 SMCRT_KINST_DECL(0, 2)
@@ -59,6 +62,8 @@ inline void kinst_diag_gather(unsigned long long* d72, unsigned long long* t9, u
   for (int i = 0; i < 6; ++i) c6[i] = 0;
   kinst_diag_0_0(d72, t9, c6); kinst_diag_0_1(d72, t9, c6); kinst_diag_0_2(d72, t9, c6);
   kinst_diag_1_0(d72, t9, c6); kinst_diag_1_1(d72, t9, c6); kinst_diag_1_2(d72, t9, c6);
+  kinst_diagp_0_0(d72, t9, c6); kinst_diagp_0_1(d72, t9, c6); kinst_diagp_0_2(d72, t9, c6);
+  kinst_diagp_1_0(d72, t9, c6); kinst_diagp_1_1(d72, t9, c6); kinst_diagp_1_2(d72, t9, c6);
 }
 
 }  // namespace smcrt

@@ -1,10 +1,12 @@
 // kinst.hip — one (LDS faces, grid mode) slice of the transport kernel instantiations.
-// Compiled six times by build.py (-DKI_F=0/1 -DKI_G=0/1/2); see kernel_ptrs.h.
+// Compiled twelve times by build.py (-DKI_F=0/1 -DKI_G=0/1/2 -DKI_P=0/1); see kernel_ptrs.h.
+// Part 0 holds transport_kernel and the XF ws_kernel, part 1 the plain ws_kernel (the lean path
+// of M1), which build.py compiles with its own scheduler flags (see UNITS there).
 #include "kernels.h"
 #include "kernel_ptrs.h"
 
-#if !defined(KI_F) || !defined(KI_G)
-#error "kinst.hip is compiled with -DKI_F=<0|1> -DKI_G=<0|1|2> (rsmcrt_amd/build.py)"
+#if !defined(KI_F) || !defined(KI_G) || !defined(KI_P)
+#error "kinst.hip is compiled with -DKI_F=<0|1> -DKI_G=<0|1|2> -DKI_P=<0|1> (rsmcrt_amd/build.py)"
 #endif
 #define KI_NAME3(a, f, g) a##_##f##_##g
 #define KI_NAME2(a, f, g) KI_NAME3(a, f, g)
@@ -12,6 +14,13 @@
 
 namespace smcrt {
 
+#if KI_P == 1
+// the plain ws_kernel (no Fresnel program points, no detectors)
+const void* KI_NAME(kinst_wsp)(int slots) {
+  return slots == 3 ? (const void*)ws_kernel<KI_F != 0, KI_G, false, 3> : (const void*)ws_kernel<KI_F != 0, KI_G, false, 2>;
+}
+#define KI_DIAG_NAME KI_NAME(kinst_diagp)
+#else
 const void* KI_NAME(kinst_transport)(int xsrc, int coop) {
   constexpr bool F = KI_F != 0;
   if (xsrc && coop) {
@@ -32,11 +41,14 @@ size_t kinst_ws_scratch_bytes(size_t lanes) { return ws_scratch_bytes(lanes); }
 
 const void* KI_NAME(kinst_ws)(int xf, int slots) {
   if (xf) return slots == 3 ? (const void*)ws_kernel<KI_F != 0, KI_G, true, 3> : (const void*)ws_kernel<KI_F != 0, KI_G, true, 2>;
-  return slots == 3 ? (const void*)ws_kernel<KI_F != 0, KI_G, false, 3> : (const void*)ws_kernel<KI_F != 0, KI_G, false, 2>;
+  return KI_NAME(kinst_wsp)(slots);
 }
+#define KI_DIAG_NAME KI_NAME(kinst_diag)
+#endif
 
 
-void KI_NAME(kinst_diag)(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6) {
+// (each part has its own copy of the static tallies)
+void KI_DIAG_NAME(unsigned long long* d72, unsigned long long* t9, unsigned long long* c6) {
 #ifdef SMCRT_DIAG
   unsigned long long h[72] = {0}, z[72] = {0};
   if (hipDeviceSynchronize() != hipSuccess) return;

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Static ISA breakdown of ws_kernel<F, G> (or transport_kernel) by region (no GPU needed).
 
-Compiles rsmcrt_amd/csrc/kinst.hip for one (LDS faces, grid mode) slice with
+Compiles rsmcrt_amd/csrc/kinst.hip for one (LDS faces, grid mode) slice (the part that holds the
+kernel, with build.py's flags for it) with
 -DSMCRT_ASM_MARKERS, which turns ws.h's WS_MARK(i) region starts into `; @@LPHASE i` comments
 in the device assembly, takes the kernel's body and counts its instructions per region and
 class (ws.h: 1 photon waves, 2 event waves, 10-15 the walker waves: setup, claim + take,
@@ -71,8 +72,12 @@ def main(argv):
             extra.append(argv[i])
             i += 1
     out = f"/tmp/isa_phases_{f}{g}.s"
+    # the plain ws_kernel lives in kinst.hip's part 1 with build.py's flags for it
+    sys.path.insert(0, ROOT)
+    from rsmcrt_amd.build import PLAIN_WS_FLAGS
+    part = ["-DKI_P=1", *PLAIN_WS_FLAGS] if kern == "ws" else ["-DKI_P=0"]
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                    "--offload-arch=gfx950", "--cuda-device-only", "-S", f"-DKI_F={f}", f"-DKI_G={g}",
+                    "--offload-arch=gfx950", "--cuda-device-only", "-S", f"-DKI_F={f}", f"-DKI_G={g}", *part,
                     "-DSMCRT_ASM_MARKERS", "-o", out, os.path.join(ROOT, "rsmcrt_amd", "csrc", "kinst.hip")] + extra,
                    check=True, cwd="/tmp", stderr=subprocess.DEVNULL)
     s = open(out).read()
