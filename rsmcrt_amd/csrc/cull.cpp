@@ -145,9 +145,11 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
   CullHost H;
   constexpr int32_t MIN_TOPS = 16, N_PROBE = 16;
   constexpr double ALWAYS_FRACTION = 0.25;
-  // grid resolution and list cap (SMCRT_CULL_CPT / _MAX_CELLS / _MAX_LIST override, experiments)
+  // grid resolution and list cap (SMCRT_CULL_CPT / _MAX_CELLS / _MAX_LIST override, experiments).
+  // 512 cells per top (round 6; 64 before): M4 15.3 vs 13.5-13.7 M photons/s same box (1024 and
+  // 2048 with more cells: 15.5, 15.6), M2 unchanged within its spread (profiles/r06_s7/ab_cull_rule.txt)
   auto env = [](const char* k, double d) { const char* v = std::getenv(k); return v ? std::atof(v) : d; };
-  const double CELLS_PER_TOP = env("SMCRT_CULL_CPT", 64.0), MAX_CELLS = env("SMCRT_CULL_MAX_CELLS", 1 << 18);
+  const double CELLS_PER_TOP = env("SMCRT_CULL_CPT", 512.0), MAX_CELLS = env("SMCRT_CULL_MAX_CELLS", 1 << 18);
   const int32_t MAX_LIST = (int32_t)env("SMCRT_CULL_MAX_LIST", 64), K_NEAREST = (int32_t)env("SMCRT_CULL_K", 8);
   const double U_FRAC = env("SMCRT_CULL_UFRAC", 1.0);  // (the reach U below is scaled by this)
   if (n_top < MIN_TOPS) return H;
