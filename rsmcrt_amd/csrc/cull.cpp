@@ -195,6 +195,7 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
   // |ds| at the cell's corners: a distance the nearest surface is (almost always) within for
   // every point of the cell. The device test m < max(h, lb) decides; U only sizes the list.
   std::vector<std::vector<uint32_t>> lists((size_t)ncell);
+  std::vector<std::vector<float>> elbs((size_t)ncell);
   H.lb.assign((size_t)ncell, 0.0);
   auto work = [&](int64_t c0, int64_t c1) {
     std::vector<double> d((size_t)nc);
@@ -229,13 +230,23 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
       for (int32_t j = 0; j < std::min(K_NEAREST, nc); ++j) pick.push_back(ord[j]);
       std::sort(pick.begin(), pick.end());
       pick.erase(std::unique(pick.begin(), pick.end()), pick.end());
+      // nearest box first (ties: ascending top index), so the device may stop a list walk at
+      // the first entry whose box is farther than the min|ds| it holds (cull.h)
+      std::stable_sort(pick.begin(), pick.end(), [&](int32_t a, int32_t b) { return d[a] < d[b]; });
       std::vector<char> in((size_t)nc, 0);
       for (int32_t j : pick) in[(size_t)j] = 1;
       double lb = INFINITY;
       for (int32_t j = 0; j < nc; ++j)
         if (!in[(size_t)j]) lb = std::min(lb, d[j]);
       std::vector<uint32_t>& L = lists[(size_t)c];
-      for (int32_t j : pick) L.push_back((uint32_t)cull[j]);  // ascending: cull[] and pick are
+      std::vector<float>& E = elbs[(size_t)c];
+      for (int32_t j : pick) {
+        L.push_back((uint32_t)cull[j]);
+        // rounded down to a float (the boxes are already grown by eps, so this stays a bound)
+        float f = (float)d[j];
+        if ((double)f > d[j]) f = std::nextafter(f, -INFINITY);
+        E.push_back(f);
+      }
       H.lb[(size_t)c] = std::isfinite(lb) ? lb * (1.0 - 1e-9) : 1e300;
     }
   };
@@ -256,6 +267,8 @@ CullHost build_cull(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32_t*
   if (total >= 0xFFFFFFFFull) return CullHost();
   H.off[(size_t)ncell] = (uint32_t)total;
   H.list.reserve(2 * total);
+  H.elb.reserve(total);
+  for (auto& E : elbs) H.elb.insert(H.elb.end(), E.begin(), E.end());
   for (auto& L : lists)
     for (uint32_t t : L) {
       const smcrt_sdf_node& nd = nodes[top[t]];

@@ -17,6 +17,12 @@
 // evaluation (tests/test_gpu_parity.py checks them against the CPU restatement, which never
 // culls).
 //
+// The same bound applies entry by entry (round 6): a cell's entries are stored nearest box
+// first with elb = their box's distance from the cell (rounded down), so a lane that already
+// holds min|ds| < elb[k] stops its list walk at k: every later top j has ds_j >= elb[j] >=
+// elb[k] > min|ds| >= 0, which changes neither min|ds| nor min ds (both <= min|ds|) nor maxloc
+// (ds_j is not negative).
+//
 // Cullable: sphere, box, torus, capsule, segment and capped cylinder (exact Euclidean SDFs,
 // sdfs.f90:494-648) under a rigid transform; models whose CSG fold keeps a bound (union: the
 // union of the children's boxes; smooth union: that box grown by k/6, the most the smoothing
@@ -47,7 +53,9 @@ struct CullGrid {
   int32_t n[3];               // cells per axis
   int32_t n_prog_always;      // ops of the always-evaluated program
   const uint32_t* off;        // [ncells + 1] list offsets
-  const uint32_t* list;       // 2 words per entry (above), ascending top index within a cell
+  const uint32_t* list;       // 2 words per entry (above); a cell's entries ascending by elb
+  const float* elb;           // per entry: a lower bound of its top's ds at any point of the cell
+                              // (its box's distance from the cell, rounded down; round 6)
   const double* lb;           // [ncells] lower bound of ds over the unlisted tops (safety margin applied)
   const void* prog_always;    // ProgOp[]: the tops evaluated for every query
 };
@@ -57,6 +65,7 @@ struct CullHost {
   double lo[3] = {0, 0, 0}, cell = 0;
   int32_t n[3] = {0, 0, 0};
   std::vector<uint32_t> off, list;  // off[] counts entries; list holds 2 words per entry
+  std::vector<float> elb;           // per entry (CullGrid::elb)
   std::vector<double> lb;
   std::vector<int32_t> always;  // 0-based tops evaluated for every query
   double mean_list = 0.0;       // diagnostics

@@ -581,18 +581,20 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   }
   if (e == hipSuccess) e = hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming);
   if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("scene upload: ") + hipGetErrorString(e)));
-  if (cull.enabled) {  // [ProgOp always | u32 off | u32 list | double lb], each 16-B aligned
+  if (cull.enabled) {  // [ProgOp always | u32 off | u32 list | double lb | float elb], each 16-B aligned
     std::vector<ProgOp> pa;
     for (int32_t t : cull.always)
       for (int32_t ip = top_first[t]; ip < top_first[t + 1]; ++ip) pa.push_back(prog[ip]);
     auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
     const size_t b_pa = al(pa.size() * sizeof(ProgOp)), b_off = al(cull.off.size() * 4),
-                 b_list = al(std::max<size_t>(1, cull.list.size()) * 4), b_lb = al(cull.lb.size() * 8);
-    std::vector<unsigned char> blob(b_pa + b_off + b_list + b_lb, 0);
+                 b_list = al(std::max<size_t>(1, cull.list.size()) * 4), b_lb = al(cull.lb.size() * 8),
+                 b_elb = al(std::max<size_t>(1, cull.elb.size()) * 4);
+    std::vector<unsigned char> blob(b_pa + b_off + b_list + b_lb + b_elb, 0);
     std::memcpy(blob.data(), pa.data(), pa.size() * sizeof(ProgOp));
     std::memcpy(blob.data() + b_pa, cull.off.data(), cull.off.size() * 4);
     std::memcpy(blob.data() + b_pa + b_off, cull.list.data(), cull.list.size() * 4);
     std::memcpy(blob.data() + b_pa + b_off + b_list, cull.lb.data(), cull.lb.size() * 8);
+    std::memcpy(blob.data() + b_pa + b_off + b_list + b_lb, cull.elb.data(), cull.elb.size() * 4);
     if ((st = dalloc((unsigned char**)&s->d_cull_data, blob.size())) || (st = dalloc(&s->d_cull, 1)))
       return cleanup_fail(st);
     unsigned char* base = (unsigned char*)s->d_cull_data;
@@ -605,6 +607,7 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
     G.off = (const uint32_t*)(base + b_pa);
     G.list = (const uint32_t*)(base + b_pa + b_off);
     G.lb = (const double*)(base + b_pa + b_off + b_list);
+    G.elb = (const float*)(base + b_pa + b_off + b_list + b_lb);
     e = hipMemcpy(s->d_cull_data, blob.data(), blob.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(s->d_cull, &G, sizeof G, hipMemcpyHostToDevice);
     if (e != hipSuccess) return cleanup_fail(fail(SMCRT_ERR_HIP, std::string("cull upload: ") + hipGetErrorString(e)));

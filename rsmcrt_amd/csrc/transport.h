@@ -1195,6 +1195,11 @@ static __device__ unsigned long long g_cull_diag[6];
 #ifndef SMCRT_CULL_CTAB
 #define SMCRT_CULL_CTAB 1
 #endif
+// a lane stops its list walk at the first entry whose box lies farther than the min|ds| it
+// holds (1, round 6: the entries are stored nearest box first with that distance, cull.h)
+#ifndef SMCRT_CULL_ELB
+#define SMCRT_CULL_ELB 1
+#endif
 #ifndef SMCRT_CULL_UNROLL
 #define SMCRT_CULL_UNROLL 4  // spheres (M2: 17.4-18.2 with 4, 17.1-17.4 with 2, 15.1-17.2 with 1, profiles/r06_s6/ab_m2_cull.txt)
 #endif
@@ -1256,6 +1261,8 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
       double du[U];
       int32_t iu[U];
       int n = 0;
+      // (the rest of the list is farther than the min|ds| this lane holds: cull.h)
+      if (SMCRT_CULL_ELB && k0 < e && (double)G->elb[k0] > r.minabs) { k0 = e; break; }
       if (SMCRT_CULL_CTAB && ct && k0 + (U - 1) < e) {
         uint2 eu[U];
         uint32_t all = ~0u;
@@ -1309,7 +1316,8 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
     // memory latency per entry (the node's) instead of two
     uint2 nxt = k0 < e ? ent[k0] : make_uint2(0u, 0u);
 #endif
-    for (uint32_t k = k0; k < e; ++k) {  // per lane: its cell's tops, ascending
+    for (uint32_t k = k0; k < e; ++k) {  // per lane: its cell's tops, nearest box first
+      if (SMCRT_CULL_ELB && (double)G->elb[k] > r.minabs) break;  // (cull.h)
 #if SMCRT_CULL_PREFETCH
       const uint2 en = nxt;
       if (k + 1 < e) nxt = ent[k + 1];
