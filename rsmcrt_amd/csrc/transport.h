@@ -1195,6 +1195,10 @@ static __device__ unsigned long long g_cull_diag[6];
 #ifndef SMCRT_CULL_CTAB
 #define SMCRT_CULL_CTAB 1
 #endif
+// a capture EVAL folds only the captured tops (1, round 6) instead of a full EVAL (0)
+#ifndef SMCRT_CULL_CAPTURE
+#define SMCRT_CULL_CAPTURE 1
+#endif
 // a lane stops its list walk at the first entry whose box lies farther than the min|ds| it
 // holds (1, round 6: the entries are stored nearest box first with that distance, cull.h)
 #ifndef SMCRT_CULL_ELB
@@ -1237,13 +1241,38 @@ __device__ __forceinline__ EvalOut eval_culled(const smcrt_sdf_node* __restrict_
       }
     }
   }
+#if SMCRT_CULL_CAPTURE
+  // A capture (the Fresnel ds lookups, calcNormal's taps: capi or capj set) uses only the
+  // captured tops' values, ds(capi) and ds(capj) (kernels.h P3, ST_F0..ST_N4), so such a lane
+  // folds those tops' own ops, as eval_sdfs folds them, instead of taking the wave to a full
+  // EVAL of every top (round 6; min|ds|, min ds and maxloc are left unset: nothing reads them)
+  const bool capture = have && (capi != 0 || capj != 0);
+  if (capture) {
+    auto top_ds = [&](int32_t i) {  // top i (0-based): its ops of the flattened program
+      const int32_t o0 = prog[n_prog + i].node, o1 = prog[n_prog + i + 1].node;
+      double acc = 0.0;
+      for (int32_t ip = o0; ip < o1; ++ip) {
+        const ProgOp op = prog[ip];
+        const double v = prog_value<NEST>(nodes, op.node, op.action, op.translate_only != 0, q);
+        if ((op.action & 3) == PROG_TOP || (op.action & 3) == PROG_CHILD_FIRST) acc = v;
+        else acc = csg(op.op, acc, v, op.k);
+      }
+      return acc;
+    };
+    if (capi != 0) r.va = top_ds(capi - 1);
+    if (capj != 0) r.vb = top_ds(capj - 1);
+  }
+  bool full = !have;
+#else
+  const bool capture = false;
   bool full = !have || capi != 0 || capj != 0;
+#endif
   const double fx = (q.x - G->lo[0]) * G->inv_cell, fy = (q.y - G->lo[1]) * G->inv_cell,
                fz = (q.z - G->lo[2]) * G->inv_cell;
-  if (!(fx >= 0.0 && fx < (double)G->n[0] && fy >= 0.0 && fy < (double)G->n[1] && fz >= 0.0 &&
-        fz < (double)G->n[2]))
+  if (!capture && !(fx >= 0.0 && fx < (double)G->n[0] && fy >= 0.0 && fy < (double)G->n[1] && fz >= 0.0 &&
+                    fz < (double)G->n[2]))
     full = true;
-  if (!full) {
+  if (!full && !capture) {
     const int32_t ix = (int32_t)fx, iy = (int32_t)fy, iz = (int32_t)fz;
     const uint32_t c = (uint32_t)ix + (uint32_t)G->n[0] * ((uint32_t)iy + (uint32_t)G->n[1] * (uint32_t)iz);
     const uint32_t b = G->off[c], e = G->off[c + 1];
