@@ -474,6 +474,8 @@ int smcrt_scene_create(const smcrt_sdf_node* nodes, int32_t n_nodes, const int32
   int32_t coop_min = 8;  // (SMCRT_COOP_MIN_TOPS: the fewest tops that get the COOP instantiation)
   if (const char* cm = std::getenv("SMCRT_COOP_MIN_TOPS")) coop_min = std::max(1, std::atoi(cm));
   s->coop_lanes = n_top >= coop_min ? std::max(1, std::min(16, n_top / ((n_top + 63) / 64 + 3))) : 0;
+  if (const char* cl = std::getenv("SMCRT_COOP_LANES"))  // (experiments: the sparse-wave threshold)
+    if (s->coop_lanes > 0) s->coop_lanes = std::max(1, std::min(64, std::atoi(cl)));
   // The cooperative EVAL's LDS table: at most 64 tops, none of them a model (transport.h).
   // SMCRT_COOP_TAB=0 keeps the global-memory cooperative EVAL.
   std::vector<double> ctab;
