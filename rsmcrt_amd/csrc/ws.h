@@ -79,6 +79,10 @@ namespace smcrt {
 #endif
 // the photon hands a segment's start cell to its walker in the slot's cell word (1) instead of
 // the walker recomputing it from the start (0); the same cell_of on the same start either way
+// the plain instantiation reads the deferral box from KParams too (1) or keeps it in VGPRs (0)
+#ifndef SMCRT_WS_KBOUNDS_PLAIN
+#define SMCRT_WS_KBOUNDS_PLAIN 0
+#endif
 #ifndef SMCRT_WS_START_CELLS
 #define SMCRT_WS_START_CELLS 1
 #endif
@@ -514,8 +518,9 @@ __global__ __launch_bounds__(WS_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
             // spilled to scratch and was reloaded here): M3 181.0/181.6 vs 172.9/173.1 M photons/s.
             // The other one keeps it in VGPRs, where its register allocation is faster: M1 with
             // KParams 252.3 vs 257.5 M (profiles/r06_s7/ab_kparams_bounds.txt).
-            const double mx = XF ? K.lean_lo[0] : mx0, my = XF ? K.lean_lo[1] : my0, mz = XF ? K.lean_lo[2] : mz0;
-            const double ex = XF ? K.lean_hi[0] : ex0, ey = XF ? K.lean_hi[1] : ey0, ez = XF ? K.lean_hi[2] : ez0;
+            constexpr bool KB = XF || SMCRT_WS_KBOUNDS_PLAIN;
+            const double mx = KB ? K.lean_lo[0] : mx0, my = KB ? K.lean_lo[1] : my0, mz = KB ? K.lean_lo[2] : mz0;
+            const double ex = KB ? K.lean_hi[0] : ex0, ey = KB ? K.lean_hi[1] : ey0, ez = KB ? K.lean_hi[2] : ez0;
             const bool inside = old.x >= mx && old.x <= ex && old.y >= my && old.y <= ey && old.z >= mz &&
                                 old.z <= ez && e.x >= mx && e.x <= ex && e.y >= my && e.y <= ey && e.z >= mz &&
                                 e.z <= ez;
