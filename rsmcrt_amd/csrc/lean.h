@@ -1,6 +1,7 @@
 // lean.h — the lean path: the transport of simple scenes with the voxel walk decoupled from the
 // photon. This header holds its shared definitions (the photon and walker state, the flags, the
-// segment-safety margin below, computed per axis at the top of ws_kernel); the kernel is ws_kernel (ws.h), which runs the photons, their
+// segment-safety margin below, computed per axis at the top of ws_kernel, or on the host into
+// KParams::lean_lo/hi for the XF instantiation); the kernel is ws_kernel (ws.h), which runs the photons, their
 // events and the walks in separate waves of a block. (Rounds 3-4 ran it as lean_kernel, whose
 // waves were both photons and walkers; ws_kernel replaced it in round 5.)
 //
